@@ -1,0 +1,204 @@
+"""Headline benchmark: faces/s recognised (projection + L2 nearest neighbour) against a
+1M-row gallery, 128x128 faces, k=128 eigenfaces, probe batch 4096 (BASELINE.json
+configs[2]; configs[3] when launched on N GPUs: the gallery is row-sharded across ranks
+and one RCCL all-reduce(MIN) over packed (score, index) keys picks the global match).
+
+One step = project 4096 uint8 probe faces (p - mean).W + search the gallery + (N>1)
+all-reduce of the 4096 keys.  Inputs are resident in HBM before timing.  Data are
+synthetic (eigenface.synth): planted probes, so the step's result is also checked.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "face-detection-recognization-pca_amd"))
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (/opt/skills/guides/MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (gallery rows, face side, k, probe batch)
+    "c3": (1_000_000, 128, 128, 4096),
+    "c2": (10_000, 128, 64, 4096),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(P, mean, W, G, targets, budget_s):
+    """Oracle fp32 BLAS restatement on the host cores, bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import eigenface_oracle as orc
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max(int(i.get("num_threads", 1)) for i in threadpool_info()) if threadpool_info() else os.cpu_count()
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count()
+    gn = np.einsum("ij,ij->i", G, G)
+    # calibrate on 32 probes, then size the sample for ~budget_s
+    t = time.perf_counter()
+    orc.recognize_l2_f32(P[:32], mean, W, G, gn)
+    per = (time.perf_counter() - t) / 32
+    b = int(min(len(P), max(32, budget_s / max(per, 1e-9))))
+    b = max(32, (b // 32) * 32)
+    t = time.perf_counter()
+    idx, _ = orc.recognize_l2_f32(P[:b], mean, W, G, gn)
+    dt = time.perf_counter() - t
+    return {
+        "value": b / dt,
+        "unit": "faces/s",
+        "cores": int(cores),
+        "kind": "port",
+        "sample": f"{b} probes x full {len(G)}-row gallery, fp32 NumPy/OpenBLAS "
+                  f"(oracle.recognize_l2_f32), {dt:.1f} s",
+        "match": float((idx == targets[:b]).mean()),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--metric", default="l2", choices=["l2", "cosine"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from eigenface import Engine, decode_keys, synth
+
+    n_total, side, k, bsz = CONFIGS[args.config]
+    d = side * side
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+
+    t_setup = time.perf_counter()
+    B = synth.basis(d, k, 0)
+    mean = synth.mean_face(side).astype(np.float32)
+    W = B.astype(np.float32)
+    G = synth.gallery_rows(lo, hi, k)
+    targets = np.random.default_rng(2024).integers(0, n_total, bsz)
+    P = synth.probes(targets, n_total, k, side, B=B)
+
+    eng = Engine(local)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    eng.set_model(mean, W)
+    eng.set_gallery(G, global_offset=lo)
+    P_dev = torch.from_numpy(P).to(dev)
+    keys = torch.empty(bsz, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s gallery rows [{lo},{hi})")
+
+    def step():
+        eng.recognize_keys(P_dev, args.metric, keys=keys)
+        if world > 1:
+            dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.timing(True)
+    eng.timing_reset()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    eng.timing(False)
+    s_ms, s_n = eng.timing_get("search")
+    p_ms, p_n = eng.timing_get("project")
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    idx, best = decode_keys(keys.cpu().numpy(), args.metric)
+    match = float((idx == targets).mean())
+
+    if rank == 0:
+        ms_step = el / args.steps * 1e3
+        value = bsz * args.steps / el
+        search_avg_ms = s_ms / max(s_n, 1)
+        flops_launch = 2.0 * bsz * (hi - lo) * k  # algorithmic: 2 k N per face x B faces
+        achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
+        rec = {
+            "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128",
+            "value": round(value, 1),
+            "unit": "faces/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (eigenface.synth planted probes; gallery = eigen-coefficients)",
+            "config": {
+                "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
+                            f"probe batch {bsz}, metric {args.metric}",
+                "gallery": n_total, "face": f"{side}x{side}", "k": k, "batch": bsz,
+                "parallelism": f"gallery row-shard x{world} + RCCL all-reduce(MIN) of packed keys"
+                               if world > 1 else "1 GPU",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "search_kernel (fp32 MFMA distance GEMM + fused arg-best)",
+                "achieved": round(achieved, 2),
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(search_avg_ms, 4),
+                "launches": s_n,
+                "flops_per_launch": flops_launch,
+            },
+            "project_avg_ms": round(p_ms / max(p_n, 1), 4),
+            "check": {"planted_match": match},
+        }
+        if world == 1 and not args.no_cpu:
+            rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
+        else:
+            rec["cpu_baseline"] = None
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

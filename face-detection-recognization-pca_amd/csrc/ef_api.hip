@@ -1,0 +1,432 @@
+// C ABI: context, recognition model, gallery, search, timing (include/eigenface.h).
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "ef_internal.hpp"
+
+namespace ef {
+
+int set_err(ef_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_err(ef_ctx* c, hipError_t e, const char* what) {
+  return set_err(c, e == hipErrorOutOfMemory ? EF_E_NOMEM : EF_E_HIP,
+                 std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(ef_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return EF_OK;
+  release(b);
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    b.bytes = 0;
+    return hip_err(c, e, "hipMalloc");
+  }
+  b.bytes = bytes;
+  return EF_OK;
+}
+
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+void timer_begin(ef_ctx* c, int kernel, TimerEvt* t) {
+  t->kernel = -1;
+  if (!c->timing) return;
+  if (hipEventCreate(&t->a) != hipSuccess) return;
+  if (hipEventCreate(&t->b) != hipSuccess) { (void)hipEventDestroy(t->a); return; }
+  t->kernel = kernel;
+  (void)hipEventRecord(t->a, c->stream);
+}
+
+void timer_end(ef_ctx* c, TimerEvt* t) {
+  if (t->kernel < 0) return;
+  (void)hipEventRecord(t->b, c->stream);
+  c->pending.push_back(*t);
+}
+
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+#define EF_TRY(expr)                         \
+  do {                                       \
+    int _rc = (expr);                        \
+    if (_rc != EF_OK) return _rc;            \
+  } while (0)
+#define EF_HIP(ctx, expr, what)                           \
+  do {                                                    \
+    hipError_t _e = (expr);                               \
+    if (_e != hipSuccess) return hip_err(ctx, _e, what);  \
+  } while (0)
+
+// Search the probes already in ctx->q_pad (bpad rows, kp = ctx->g_kp) into keys_dev.
+static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev) {
+  if (c->n_gallery == 0) {
+    EF_HIP(c, launch_keys_none(c->stream, keys_dev, b), "keys");
+    return EF_OK;
+  }
+  const SearchPlan pl = search_plan(bpad, c->n_gallery);
+  // workspace carve-out (16-byte aligned pieces)
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t nkb = al((size_t)pl.nchunks * bpad * 8), nb2 = al((size_t)pl.nchunks * bpad * 4);
+  const size_t ncnt = al(16), nlist = al((size_t)bpad * 4), nthr = al((size_t)bpad * 4);
+  const size_t ncand = al((size_t)bpad * kCandMax * 4), ncc = al((size_t)bpad * 4);
+  EF_TRY(ensure(c, c->search_ws, nkb + nb2 + ncnt + nlist + nthr + ncand + ncc));
+  char* base = static_cast<char*>(c->search_ws.p);
+  SearchWs ws;
+  ws.part_key = reinterpret_cast<long long*>(base);
+  base += nkb;
+  ws.part_b2 = reinterpret_cast<float*>(base);
+  base += nb2;
+  ws.amb_count = reinterpret_cast<int*>(base);
+  base += ncnt;
+  ws.amb_list = reinterpret_cast<int*>(base);
+  base += nlist;
+  ws.thr = reinterpret_cast<float*>(base);
+  base += nthr;
+  ws.cand = reinterpret_cast<int*>(base);
+  base += ncand;
+  ws.cand_cnt = reinterpret_cast<int*>(base);
+  const float* aux = static_cast<const float*>(metric == EF_METRIC_L2 ? c->gnorm2.p : c->ginv.p);
+  EF_HIP(c,
+         launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), bpad, b,
+                       static_cast<const float*>(c->G.p), aux, c->n_gallery, c->g_offset, c->gmax2_host, ws,
+                       keys_dev, c),
+         "search");
+  return EF_OK;
+}
+
+// Project b probes (device pointer P) into ctx->q_pad; optional feature output (device).
+static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t bpad, float* f_dev) {
+  EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->kp * sizeof(float)));
+  int64_t pps = 0;
+  const int ns = project_nsplit(bpad, c->d, &pps);
+  EF_TRY(ensure(c, c->proj_part, (size_t)ns * bpad * c->kpw * sizeof(float)));
+  TimerEvt t;
+  timer_begin(c, EF_KERNEL_PROJECT, &t);
+  EF_HIP(c,
+         launch_project(c->stream, c->kpw, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean.p),
+                        static_cast<const float*>(c->W.p), static_cast<float*>(c->proj_part.p), ns, pps),
+         "project kernel");
+  timer_end(c, &t);
+  EF_HIP(c,
+         launch_project_reduce(c->stream, static_cast<const float*>(c->proj_part.p), ns, b, bpad, c->kpw,
+                               c->k, c->kp, static_cast<float*>(c->q_pad.p), f_dev),
+         "project reduce");
+  return EF_OK;
+}
+
+static int stage_probes(ef_ctx* c, const void* P, int dtype, int64_t b, uint32_t flags, const void** Pd) {
+  if (flags & EF_MEM_DEVICE) {
+    *Pd = P;
+    return EF_OK;
+  }
+  const size_t bytes = (size_t)b * c->d * (dtype == EF_U8 ? 1 : 4);
+  EF_TRY(ensure(c, c->p_stage, bytes));
+  EF_HIP(c, hipMemcpyAsync(c->p_stage.p, P, bytes, hipMemcpyHostToDevice, c->stream), "H2D probes");
+  *Pd = c->p_stage.p;
+  return EF_OK;
+}
+
+}  // namespace ef
+
+using namespace ef;
+
+extern "C" {
+
+int ef_api_version(void) { return EF_API_VERSION; }
+
+int ef_device_count(int* out) {
+  if (!out) return EF_E_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *out = n;
+  return EF_OK;
+}
+
+int ef_create(int device, ef_ctx** out) {
+  if (!out) return EF_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return EF_E_HIP;
+  if (device < 0 || device >= n) return EF_E_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return EF_E_HIP;
+  ef_ctx* c = new ef_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return EF_E_HIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return EF_OK;
+}
+
+void ef_destroy(ef_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& t : c->pending) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  DevBuf* bufs[] = {&c->mean, &c->W,     &c->G,         &c->gnorm2,    &c->ginv,      &c->gmax2,
+                    &c->q_pad, &c->keys, &c->search_ws, &c->p_stage, &c->proj_part, &c->feats_dev};
+  for (DevBuf* b : bufs) release(*b);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char* ef_last_error(const ef_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ef_set_stream(ef_ctx* c, void* s) {
+  if (!c) return EF_E_INVALID;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return EF_OK;
+}
+
+int ef_synchronize(ef_ctx* c) {
+  if (!c) return EF_E_INVALID;
+  EF_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return EF_OK;
+}
+
+int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_t k, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (!mean || !W || d < 1 || k < 1) return set_err(c, EF_E_INVALID, "ef_model_set: bad arguments");
+  const int kp = feature_pad(k);
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_model_set: k > 128 is not supported by this build");
+  (void)hipSetDevice(c->device);
+  const int kpw = proj_pad(kp);
+  EF_TRY(ensure(c, c->mean, (size_t)d * sizeof(float)));
+  EF_TRY(ensure(c, c->W, (size_t)d * kpw * sizeof(float)));
+  const hipMemcpyKind kind = (flags & EF_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  EF_HIP(c, hipMemcpyAsync(c->mean.p, mean, (size_t)d * sizeof(float), kind, c->stream), "copy mean");
+  const float* wsrc = W;
+  DevBuf tmp;
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_TRY(ensure(c, tmp, (size_t)d * k * sizeof(float)));
+    hipError_t e = hipMemcpyAsync(tmp.p, W, (size_t)d * k * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) { release(tmp); return hip_err(c, e, "copy W"); }
+    wsrc = static_cast<const float*>(tmp.p);
+  }
+  hipError_t e = launch_pad_rows(c->stream, wsrc, d, k, d, static_cast<float*>(c->W.p), kpw);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  release(tmp);
+  if (e != hipSuccess) return hip_err(c, e, "pad W");
+  c->d = d;
+  c->k = k;
+  c->kp = kp;
+  c->kpw = kpw;
+  return EF_OK;
+}
+
+int ef_project(ef_ctx* c, const void* P, int32_t dtype, int64_t b, float* F, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (c->d == 0) return set_err(c, EF_E_STATE, "ef_project: no model (call ef_model_set)");
+  if (!P || !F || b < 0 || (dtype != EF_U8 && dtype != EF_F32))
+    return set_err(c, EF_E_INVALID, "ef_project: bad arguments");
+  if (b == 0) return EF_OK;
+  (void)hipSetDevice(c->device);
+  const int64_t bpad = round_up(b, kSearchProbeTile);
+  const void* Pd = nullptr;
+  EF_TRY(stage_probes(c, P, dtype, b, flags, &Pd));
+  float* fdev = F;
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_TRY(ensure(c, c->feats_dev, (size_t)b * c->k * sizeof(float)));
+    fdev = static_cast<float*>(c->feats_dev.p);
+  }
+  EF_TRY(project_dev(c, Pd, dtype, b, bpad, fdev));
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_HIP(c, hipMemcpyAsync(F, fdev, (size_t)b * c->k * sizeof(float), hipMemcpyDeviceToHost, c->stream),
+           "D2H features");
+    EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  }
+  return EF_OK;
+}
+
+int ef_gallery_set(ef_ctx* c, const float* G, int64_t n, int32_t k, int64_t offset, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if ((!G && n > 0) || n < 0 || k < 1 || offset < 0 || n + offset > (int64_t)UINT_MAX)
+    return set_err(c, EF_E_INVALID, "ef_gallery_set: bad arguments");
+  const int kp = feature_pad(k);
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 128 is not supported by this build");
+  (void)hipSetDevice(c->device);
+  c->n_gallery = 0;
+  if (n > 0) {
+    EF_TRY(ensure(c, c->G, (size_t)n * kp * sizeof(float)));
+    EF_TRY(ensure(c, c->gnorm2, (size_t)n * sizeof(float)));
+    EF_TRY(ensure(c, c->ginv, (size_t)n * sizeof(float)));
+    EF_TRY(ensure(c, c->gmax2, 16));
+    const hipMemcpyKind kind = (flags & EF_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (k == kp) {
+      EF_HIP(c, hipMemcpyAsync(c->G.p, G, (size_t)n * k * sizeof(float), kind, c->stream), "copy gallery");
+    } else {
+      const float* src = G;
+      DevBuf tmp;
+      if (!(flags & EF_MEM_DEVICE)) {
+        EF_TRY(ensure(c, tmp, (size_t)n * k * sizeof(float)));
+        hipError_t e = hipMemcpyAsync(tmp.p, G, (size_t)n * k * sizeof(float), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) { release(tmp); return hip_err(c, e, "copy gallery"); }
+        src = static_cast<const float*>(tmp.p);
+      }
+      hipError_t e = launch_pad_rows(c->stream, src, n, k, n, static_cast<float*>(c->G.p), kp);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+      release(tmp);
+      if (e != hipSuccess) return hip_err(c, e, "pad gallery");
+    }
+    EF_HIP(c,
+           launch_gallery_aux(c->stream, static_cast<const float*>(c->G.p), n, kp,
+                              static_cast<float*>(c->gnorm2.p), static_cast<float*>(c->ginv.p),
+                              static_cast<unsigned*>(c->gmax2.p)),
+           "gallery norms");
+    EF_HIP(c, hipMemcpyAsync(&c->gmax2_host, c->gmax2.p, sizeof(float), hipMemcpyDeviceToHost, c->stream),
+           "D2H gmax2");
+    EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  }
+  c->n_gallery = n;
+  c->g_offset = offset;
+  c->g_k = k;
+  c->g_kp = kp;
+  return EF_OK;
+}
+
+int ef_search(ef_ctx* c, const float* Q, int64_t b, int32_t metric, int64_t* keys, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (c->g_k == 0) return set_err(c, EF_E_STATE, "ef_search: no gallery (call ef_gallery_set)");
+  if (!Q || !keys || b < 0 || (metric != EF_METRIC_L2 && metric != EF_METRIC_COSINE))
+    return set_err(c, EF_E_INVALID, "ef_search: bad arguments");
+  if (b == 0) return EF_OK;
+  (void)hipSetDevice(c->device);
+  const int64_t bpad = round_up(b, kSearchProbeTile);
+  EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->g_kp * sizeof(float)));
+  const float* qsrc = Q;
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_TRY(ensure(c, c->p_stage, (size_t)b * c->g_k * sizeof(float)));
+    EF_HIP(c, hipMemcpyAsync(c->p_stage.p, Q, (size_t)b * c->g_k * sizeof(float), hipMemcpyHostToDevice, c->stream),
+           "H2D queries");
+    qsrc = static_cast<const float*>(c->p_stage.p);
+  }
+  EF_HIP(c, launch_pad_rows(c->stream, qsrc, b, c->g_k, bpad, static_cast<float*>(c->q_pad.p), c->g_kp),
+         "pad queries");
+  long long* kdev = reinterpret_cast<long long*>(keys);
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long)));
+    kdev = static_cast<long long*>(c->keys.p);
+  }
+  EF_TRY(search_qpad(c, bpad, b, metric, kdev));
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
+           "D2H keys");
+    EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  }
+  return EF_OK;
+}
+
+int ef_recognize(ef_ctx* c, const void* P, int32_t dtype, int64_t b, int32_t metric, int64_t* keys,
+                 float* feats, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (c->d == 0) return set_err(c, EF_E_STATE, "ef_recognize: no model (call ef_model_set)");
+  if (c->g_k == 0) return set_err(c, EF_E_STATE, "ef_recognize: no gallery (call ef_gallery_set)");
+  if (c->g_k != c->k) return set_err(c, EF_E_INVALID, "ef_recognize: gallery k != model k");
+  if (!P || !keys || b < 0 || (dtype != EF_U8 && dtype != EF_F32) ||
+      (metric != EF_METRIC_L2 && metric != EF_METRIC_COSINE))
+    return set_err(c, EF_E_INVALID, "ef_recognize: bad arguments");
+  if (b == 0) return EF_OK;
+  (void)hipSetDevice(c->device);
+  const int64_t bpad = round_up(b, kSearchProbeTile);
+  const void* Pd = nullptr;
+  EF_TRY(stage_probes(c, P, dtype, b, flags, &Pd));
+  float* fdev = nullptr;
+  if (feats) {
+    if (flags & EF_MEM_DEVICE) {
+      fdev = feats;
+    } else {
+      EF_TRY(ensure(c, c->feats_dev, (size_t)b * c->k * sizeof(float)));
+      fdev = static_cast<float*>(c->feats_dev.p);
+    }
+  }
+  EF_TRY(project_dev(c, Pd, dtype, b, bpad, fdev));
+  long long* kdev = reinterpret_cast<long long*>(keys);
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long)));
+    kdev = static_cast<long long*>(c->keys.p);
+  }
+  EF_TRY(search_qpad(c, bpad, b, metric, kdev));
+  if (!(flags & EF_MEM_DEVICE)) {
+    EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
+           "D2H keys");
+    if (feats)
+      EF_HIP(c, hipMemcpyAsync(feats, fdev, (size_t)b * c->k * sizeof(float), hipMemcpyDeviceToHost, c->stream),
+             "D2H features");
+    EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  }
+  return EF_OK;
+}
+
+void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx) {
+  for (int64_t i = 0; i < b; ++i) {
+    const int64_t key = keys[i];
+    if (key == EF_KEY_NONE) {
+      if (best) best[i] = NAN;
+      if (idx) idx[i] = -1;
+      continue;
+    }
+    const int32_t s = (int32_t)(key >> 32);
+    const int32_t bits = s >= 0 ? s : (s ^ 0x7FFFFFFF);
+    float v;
+    std::memcpy(&v, &bits, sizeof(v));
+    if (best) best[i] = metric == EF_METRIC_COSINE ? -v : v;
+    if (idx) idx[i] = (int64_t)(uint32_t)(key & 0xffffffffll);
+  }
+}
+
+int ef_timing_enable(ef_ctx* c, int on) {
+  if (!c) return EF_E_INVALID;
+  c->timing = on != 0;
+  return EF_OK;
+}
+
+static int timing_drain(ef_ctx* c) {
+  if (c->pending.empty()) return EF_OK;
+  EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  for (auto& t : c->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess && t.kernel >= 0 && t.kernel < 4) {
+      c->t_ms[t.kernel] += ms;
+      c->t_n[t.kernel] += 1;
+    }
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  c->pending.clear();
+  return EF_OK;
+}
+
+int ef_timing_get(ef_ctx* c, int32_t kernel, double* total_ms, int64_t* launches) {
+  if (!c || kernel < 0 || kernel >= 4) return EF_E_INVALID;
+  EF_TRY(timing_drain(c));
+  if (total_ms) *total_ms = c->t_ms[kernel];
+  if (launches) *launches = c->t_n[kernel];
+  return EF_OK;
+}
+
+int ef_timing_reset(ef_ctx* c) {
+  if (!c) return EF_E_INVALID;
+  EF_TRY(timing_drain(c));
+  for (int i = 0; i < 4; ++i) {
+    c->t_ms[i] = 0;
+    c->t_n[i] = 0;
+  }
+  return EF_OK;
+}
+
+}  // extern "C"

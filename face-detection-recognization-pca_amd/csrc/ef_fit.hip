@@ -1,0 +1,229 @@
+// ef_fit: the eigenfaces fit on the GPU (mean -> centre -> covariance -> eigensolve ->
+// back-project -> unit eigenfaces -> training projection), float64 throughout.
+//
+// Restates manual_pca (useless/train.py:56-128) and, with EF_FIT_STANDARDIZE, the
+// StandardScaler + PCA(svd_solver='full') fit of train-v4.py:126-146:
+//   * covariance: Gram A.A^T/(n-1) when n < d (useless/train.py:82-85), else the d x d
+//     A^T.A/(n-1) (np.cov branch, :97-99), formed by the f64 MFMA GEMM with the centring
+//     (and 1/scale) applied in the operand loads;
+//   * eigensolve: orders <= kJacobiMax go straight to the LDS Jacobi kernel; larger ones
+//     run block subspace iteration (Y = C.Q; G = Y^T.Y; G = W.L.W^T by Jacobi in LDS;
+//     Q = Y.W.L^-1/2) to convergence, then a Rayleigh-Ritz step (T = Q^T.C.Q, Jacobi)
+//     — the top-k pairs are all manual_pca keeps (:114-116) and all sklearn reports
+//     (explained_variance_ratio_ uses trace(C) as the total, _pca.py:644-646);
+//   * eigenfaces: E = A^T.U (:91), unit columns (:94-95), sklearn svd_flip sign rule.
+#include <cmath>
+#include <vector>
+
+#include "ef_linalg.hpp"
+
+namespace {
+
+using namespace ef;
+
+struct Bufs {
+  std::vector<DevBuf> v;
+  ~Bufs() {
+    for (auto& b : v) release(b);
+  }
+  template <class T>
+  int get(ef_ctx* c, size_t count, T** out) {
+    v.emplace_back();
+    const int rc = ensure(c, v.back(), count * sizeof(T) + 16);
+    *out = static_cast<T*>(v.back().p);
+    return rc;
+  }
+};
+
+#define EF_TRY(expr)              \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != EF_OK) return _rc; \
+  } while (0)
+#define EF_HIP(ctx, expr, what)                          \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return hip_err(ctx, _e, what); \
+  } while (0)
+
+constexpr int kMaxSweeps = 60;
+constexpr int kMaxIters = 500;
+constexpr size_t kWorkElems = size_t(1) << 24;  // split-K slab budget (128 MiB)
+
+// Top-kk eigenpairs of the symmetric dim x dim matrix C (device, ld = dim).
+// U_out: dim x kk (row-major, ld kk), lam_out: kk (device).  iters: host.
+int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* work, double* U_out,
+             double* lam_out, int* iters) {
+  hipStream_t s = c->stream;
+  int* info = nullptr;
+  EF_TRY(B.get(c, 4, &info));
+  int hinfo = 0;
+  if (dim <= kJacobiMax) {
+    double *ev, *V;
+    EF_TRY(B.get(c, (size_t)dim, &ev));
+    EF_TRY(B.get(c, (size_t)dim * dim, &V));
+    EF_HIP(c, launch_jacobi(s, C, (int)dim, dim, ev, V, dim, kMaxSweeps, info), "jacobi");
+    EF_HIP(c, hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
+    EF_HIP(c, hipMemcpy2DAsync(U_out, kk * sizeof(double), V, dim * sizeof(double), kk * sizeof(double), dim,
+                               hipMemcpyDeviceToDevice, s),
+           "copy U");
+    EF_HIP(c, hipMemcpyAsync(lam_out, ev, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
+    EF_HIP(c, hipStreamSynchronize(s), "sync");
+    if (hinfo < 0) return set_err(c, EF_E_NUMERIC, "Jacobi eigensolver did not converge");
+    *iters = 0;
+    return EF_OK;
+  }
+
+  const int m = kJacobiMax;  // subspace width (even)
+  double *Q, *Y, *G, *Wm, *W2, *lam;
+  EF_TRY(B.get(c, (size_t)dim * m, &Q));
+  EF_TRY(B.get(c, (size_t)dim * m, &Y));
+  EF_TRY(B.get(c, (size_t)m * m, &G));
+  EF_TRY(B.get(c, (size_t)m * m, &Wm));
+  EF_TRY(B.get(c, (size_t)m * m, &W2));
+  EF_TRY(B.get(c, (size_t)m, &lam));
+  EF_HIP(c, launch_rand_init(s, Q, dim * m, 0x5eedULL), "rand init");
+
+  std::vector<double> th(m), prev(m, 0.0);
+  int stable = 0, it = 0;
+  for (it = 1; it <= kMaxIters; ++it) {
+    EF_HIP(c, gemm64(s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
+                     work, kWorkElems),
+           "Y = C.Q");
+    EF_HIP(c, gemm64(s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+                     kWorkElems),
+           "G = Y^T.Y");
+    EF_HIP(c, launch_jacobi(s, G, m, m, lam, Wm, m, kMaxSweeps, info), "jacobi(G)");
+    EF_HIP(c, launch_scale_cols_rsqrt(s, Wm, m, m, lam, W2), "W.L^-1/2");
+    EF_HIP(c, gemm64(s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
+                     kWorkElems),
+           "Q = Y.W");
+    EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
+    EF_HIP(c, hipStreamSynchronize(s), "sync");
+    for (auto& t : th) t = std::sqrt(t > 0 ? t : 0.0);
+    double worst = 0.0;
+    for (int i = 0; i < kk; ++i) worst = std::fmax(worst, std::fabs(th[i] - prev[i]));
+    prev = th;
+    if (!(std::isfinite(th[0]))) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
+    if (it > 2 && worst <= 1e-15 * th[0]) {
+      if (++stable >= 3) break;
+    } else {
+      stable = 0;
+    }
+  }
+  if (it > kMaxIters) it = kMaxIters;
+  // Rayleigh-Ritz on C itself: T = Q^T.C.Q, T = V.L.V^T, U = Q.V[:, :kk]
+  EF_HIP(c, gemm64(s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
+                   kWorkElems),
+         "Y = C.Q");
+  EF_HIP(c, gemm64(s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+                   kWorkElems),
+         "T = Q^T.Y");
+  EF_HIP(c, launch_jacobi(s, G, m, m, lam, Wm, m, kMaxSweeps, info), "jacobi(T)");
+  EF_HIP(c, gemm64(s, Operand::dense(Q, m, false), Operand::dense(Wm, m, false), dim, kk, m, 1.0, U_out, kk, work,
+                   kWorkElems),
+         "U = Q.V");
+  EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
+  EF_HIP(c, hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  if (hinfo < 0) return set_err(c, EF_E_NUMERIC, "Jacobi (Rayleigh-Ritz) did not converge");
+  *iters = it;
+  return EF_OK;
+}
+
+}  // namespace
+
+extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint32_t flags,
+                      double* mean_out, double* var_out, double* scale_out, double* comps_out,
+                      double* eig_out, double* proj_out, double* tv_out, int32_t* k_out, int32_t* iters_out) {
+  if (!c) return EF_E_INVALID;
+  if (!X || n < 2 || d < 1 || k < 1 || !mean_out || !comps_out || !eig_out)
+    return set_err(c, EF_E_INVALID, "ef_fit: bad arguments (need X, n >= 2, d >= 1, k >= 1, outputs)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->stream;
+  const bool dev = flags & EF_MEM_DEVICE;
+  const bool stdz = flags & EF_FIT_STANDARDIZE;
+  const bool gram = n < d;
+  const int64_t dim = gram ? n : d;
+  const int kk = (int)(k < dim ? k : dim);
+  if (dim > kJacobiMax && kk > kJacobiMax - 8)
+    return set_err(c, EF_E_INVALID, "ef_fit: k too large for the LDS subspace eigensolver (max 80)");
+
+  Bufs B;
+  const uint8_t* Xd = X;
+  if (!dev) {
+    uint8_t* xb;
+    EF_TRY(B.get(c, (size_t)n * d, &xb));
+    EF_HIP(c, hipMemcpyAsync(xb, X, (size_t)n * d, hipMemcpyHostToDevice, s), "H2D X");
+    Xd = xb;
+  }
+  unsigned long long *S1, *S2;
+  double *mean, *var, *scale, *w, *C, *work, *U, *lam, *E = nullptr, *comps, *En, *proj = nullptr, *tv;
+  EF_TRY(B.get(c, (size_t)d, &S1));
+  EF_TRY(B.get(c, (size_t)d, &S2));
+  EF_TRY(B.get(c, (size_t)d, &mean));
+  EF_TRY(B.get(c, (size_t)d, &var));
+  EF_TRY(B.get(c, (size_t)d, &scale));
+  EF_TRY(B.get(c, (size_t)d, &w));
+  EF_TRY(B.get(c, (size_t)dim * dim, &C));
+  EF_TRY(B.get(c, kWorkElems, &work));
+  EF_TRY(B.get(c, (size_t)dim * kk, &U));
+  EF_TRY(B.get(c, (size_t)kk, &lam));
+  EF_TRY(B.get(c, (size_t)kk * d, &comps));
+  EF_TRY(B.get(c, (size_t)d * kk, &En));
+  EF_TRY(B.get(c, 1, &tv));
+
+  // K1: exact column statistics -> mean / var / scale / centring weights
+  EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
+  EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
+  EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
+  EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
+  const double* wp = stdz ? w : nullptr;
+
+  // K2+K3: covariance with the centring fused into the operand loads
+  const double inv = 1.0 / (double)(n - 1);
+  if (gram)
+    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::pixels(Xd, d, true, mean, wp), n, n, d,
+                     inv, C, n, work, kWorkElems),
+           "Gram");
+  else
+    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, true, mean, wp), Operand::pixels(Xd, d, false, mean, wp), d, d, n,
+                     inv, C, d, work, kWorkElems),
+           "covariance");
+  EF_HIP(c, launch_trace(s, C, dim, dim, tv), "trace");
+
+  // K4: top-kk eigenpairs
+  int iters = 0;
+  EF_TRY(eig_topk(c, B, C, dim, kk, work, U, lam, &iters));
+
+  // K5: back-project (Gram path), unit columns + sign rule
+  if (gram) {
+    EF_TRY(B.get(c, (size_t)d * kk, &E));
+    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, true, mean, wp), Operand::dense(U, kk, false), d, kk, n, 1.0, E, kk,
+                     work, kWorkElems),
+           "E = A^T.U");
+    EF_HIP(c, launch_normalize_sign(s, E, d, kk, kk, comps, En), "normalize");
+  } else {
+    EF_HIP(c, launch_normalize_sign(s, U, d, kk, kk, comps, En), "normalize");
+  }
+  // training projection A.E (projected_data / fit_transform output)
+  if (proj_out) {
+    EF_TRY(B.get(c, (size_t)n * kk, &proj));
+    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::dense(En, kk, false), n, kk, d, 1.0, proj,
+                     kk, work, kWorkElems),
+           "F = A.E");
+  }
+
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  EF_HIP(c, hipMemcpyAsync(mean_out, mean, d * sizeof(double), kind, s), "out mean");
+  if (var_out) EF_HIP(c, hipMemcpyAsync(var_out, var, d * sizeof(double), kind, s), "out var");
+  if (scale_out) EF_HIP(c, hipMemcpyAsync(scale_out, scale, d * sizeof(double), kind, s), "out scale");
+  EF_HIP(c, hipMemcpyAsync(comps_out, comps, (size_t)kk * d * sizeof(double), kind, s), "out comps");
+  EF_HIP(c, hipMemcpyAsync(eig_out, lam, kk * sizeof(double), kind, s), "out eig");
+  if (proj_out) EF_HIP(c, hipMemcpyAsync(proj_out, proj, (size_t)n * kk * sizeof(double), kind, s), "out proj");
+  if (tv_out) EF_HIP(c, hipMemcpyAsync(tv_out, tv, sizeof(double), kind, s), "out tv");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  if (k_out) *k_out = kk;
+  if (iters_out) *iters_out = iters;
+  return EF_OK;
+}

@@ -1,0 +1,124 @@
+// Internal declarations shared by the libeigenface translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/eigenface.h"
+
+namespace ef {
+
+// ---- padded widths ------------------------------------------------------------------
+// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,96,128}
+// (zero padding is exact for dot products and distances).
+inline int feature_pad(int k) {
+  if (k <= 16) return 16;
+  if (k <= 32) return 32;
+  if (k <= 64) return 64;
+  if (k <= 96) return 96;
+  if (k <= 128) return 128;
+  return -1;
+}
+// The projection GEMM writes KPW = 64 or 128 columns.
+inline int proj_pad(int kp) { return kp <= 64 ? 64 : 128; }
+
+constexpr int kSearchProbeTile = 256;   // probes per search workgroup (4 waves x 64)
+constexpr int kProjRowTile = 128;       // probes per projection workgroup
+constexpr int kJacobiMax = 88;          // largest (even) order the LDS Jacobi handles
+constexpr int kCandMax = 32;            // fp64 re-rank candidates kept per ambiguous probe
+
+// Workspace of one search call (device pointers).
+struct SearchWs {
+  long long* part_key;  // [nchunks][bpad] best (score, row) per chunk
+  float* part_b2;       // [nchunks][bpad] runner-up score per chunk
+  int* amb_count;       // probes queued for fp64 resolution
+  int* amb_list;        // [bpad] probe of each queued slot
+  float* thr;           // [bpad] fp32 score threshold of each slot
+  int* cand;            // [bpad][kCandMax] candidate rows
+  int* cand_cnt;        // [bpad]
+};
+
+struct SearchPlan {
+  int n_ptiles = 0, nchunks = 0, tiles_per_chunk = 0;
+};
+
+// ---- device buffer ------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct TimerEvt {
+  hipEvent_t a, b;
+  int kernel;
+};
+
+}  // namespace ef
+
+struct ef_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // recognition model (p - mean) . W
+  int64_t d = 0;
+  int k = 0, kp = 0, kpw = 0;
+  ef::DevBuf mean;  // float[d]
+  ef::DevBuf W;     // float[d][kpw]
+
+  // gallery
+  int64_t n_gallery = 0, g_offset = 0;
+  int g_k = 0, g_kp = 0;
+  ef::DevBuf G;      // float[n][g_kp]
+  ef::DevBuf gnorm2; // float[n]  ||g||^2
+  ef::DevBuf ginv;   // float[n]  1/||g|| (0 for a zero row)
+  ef::DevBuf gmax2;  // uint (float bits) max ||g||^2
+  float gmax2_host = 0.f;
+
+  // per-call scratch (grown on demand, never shrunk)
+  ef::DevBuf q_pad;     // float[bpad][kp]
+  ef::DevBuf keys;      // int64[bpad]
+  ef::DevBuf search_ws; // SearchWs carve-out
+  ef::DevBuf p_stage;   // probe pixels staged from host
+  ef::DevBuf proj_part; // float[nsplit][bpad][kpw]
+  ef::DevBuf feats_dev; // float[b][k] staging for host output
+
+  bool timing = false;
+  std::vector<ef::TimerEvt> pending;
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_n[4] = {0, 0, 0, 0};
+};
+
+namespace ef {
+
+int set_err(ef_ctx* c, int code, const std::string& msg);
+int hip_err(ef_ctx* c, hipError_t e, const char* what);
+int ensure(ef_ctx* c, DevBuf& b, size_t bytes);
+void release(DevBuf& b);
+void timer_begin(ef_ctx* c, int kernel, TimerEvt* t);
+void timer_end(ef_ctx* c, TimerEvt* t);
+
+// ---- launchers (defined in the .hip files) -------------------------------------------
+SearchPlan search_plan(int64_t bpad, int64_t n);
+hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
+                         int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
+                         float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
+hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b);
+hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,
+                           float* dst, int kp);
+hipError_t launch_gallery_aux(hipStream_t s, const float* G, int64_t n, int kp, float* gnorm2,
+                              float* ginv, unsigned* gmax2_bits);
+
+hipError_t launch_project(hipStream_t s, int kpw, int p_dtype, const void* P, int64_t b,
+                          int64_t bpad, int64_t d, const float* mean, const float* W,
+                          float* part, int nsplit, int64_t pix_per_split);
+int project_nsplit(int64_t bpad, int64_t d, int64_t* pix_per_split);
+hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, int64_t b,
+                                 int64_t bpad, int kpw, int k, int kp, float* qpad, float* f_out);
+
+}  // namespace ef

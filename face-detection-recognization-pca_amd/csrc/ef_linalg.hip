@@ -1,0 +1,460 @@
+// Fit-path kernels (SURVEY.md K1 column statistics, K3 Gram/covariance, K4 eigensolver,
+// K5 back-projection helpers).  Everything here is float64: the survey measured that
+// fp32 eigenvectors cannot meet 1e-4 on the trailing real-face components
+// (SURVEY.md §7 "fp32 conditioning"), and the reference itself is fp64 LAPACK
+// (useless/train.py:84-95).
+#include "ef_linalg.hpp"
+
+#include <climits>
+#include <cmath>
+
+namespace ef {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- K1: column stats
+// Exact integer sums: S1[c] = sum_i x_ic, S2[c] = sum_i x_ic^2 (uint64 atomics are exact,
+// so the result does not depend on arrival order).
+__global__ void colstats_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d, int64_t rows_per,
+                                unsigned long long* __restrict__ S1,
+                                unsigned long long* __restrict__ S2) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  int64_t r1 = r0 + rows_per;
+  if (r1 > n) r1 = n;
+  unsigned long long s1 = 0, s2 = 0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const unsigned v = X[r * d + c];
+    s1 += v;
+    s2 += v * v;
+  }
+  atomicAdd(&S1[c], s1);
+  atomicAdd(&S2[c], s2);
+}
+
+// mean, population variance, StandardScaler scale_ (sklearn _data.py:1040-1051:
+// near-constant features -> scale 1), and the centring weight w (1/scale or 1).
+__global__ void stats_finalize_kernel(const unsigned long long* __restrict__ S1,
+                                      const unsigned long long* __restrict__ S2, int64_t n, int64_t d,
+                                      int standardize, double* __restrict__ mean,
+                                      double* __restrict__ var, double* __restrict__ scale,
+                                      double* __restrict__ w) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  const long long s1 = (long long)S1[c], s2 = (long long)S2[c];
+  const double dn = (double)n;
+  const double mu = (double)s1 / dn;
+  const long long num = (long long)n * s2 - s1 * s1;  // exact: n*sum(x^2) - (sum x)^2
+  const double v = (double)num / (dn * dn);
+  const double eps = 2.220446049250313e-16;
+  const double bound = dn * eps * v + (dn * mu * eps) * (dn * mu * eps);
+  const double sc = (v <= bound) ? 1.0 : sqrt(v);
+  mean[c] = mu;
+  var[c] = v;
+  scale[c] = sc;
+  w[c] = standardize ? 1.0 / sc : 1.0;
+}
+
+// ------------------------------------------------------------ generic f64 MFMA GEMM
+// C[M][N] = alpha * sum_k A(m,k) * B(k,n) on v_mfma_f64_16x16x4_f64.  A/B are read
+// through loaders so the centred/scaled pixel matrix ((x - mu) * w) is formed in the
+// operand load and never materialised (K2).  Split-K over gridDim.z writes fp64 slabs
+// that reduce_splitk sums in a fixed order.
+constexpr int GT = 64;          // tile M and N
+constexpr int GK = 16;          // tile K
+constexpr int GS = GT + 16;     // LDS row stride (doubles): conflict-free ds_read_b64
+
+template <class LA, class LB>
+__global__ __launch_bounds__(256) void gemm64_kernel(LA A, LB B, int64_t M, int64_t N, int64_t K,
+                                                     int64_t k_per_split, double alpha,
+                                                     double* __restrict__ C, int64_t ldc,
+                                                     double* __restrict__ part) {
+  __shared__ double sA[GK * GS];
+  __shared__ double sB[GK * GS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * GT, n0 = (int64_t)blockIdx.x * GT;
+  const int64_t kb = (int64_t)blockIdx.z * k_per_split;
+  int64_t ke = kb + k_per_split;
+  if (ke > K) ke = K;
+
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0, 0, 0, 0};
+
+  for (int64_t k0 = kb; k0 < ke; k0 += GK) {
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const int e = tid + 256 * e4;
+      int mm, kk;
+      if (A.kfast) { kk = e % GK; mm = e / GK; } else { mm = e % GT; kk = e / GT; }
+      const int64_t gm = m0 + mm, gk = k0 + kk;
+      sA[kk * GS + mm] = (gm < M && gk < ke) ? A(gm, gk) : 0.0;
+      int nn;
+      if (B.kfast) { kk = e % GK; nn = e / GK; } else { nn = e % GT; kk = e / GT; }
+      const int64_t gn = n0 + nn, gk2 = k0 + kk;
+      sB[kk * GS + nn] = (gn < N && gk2 < ke) ? B(gk2, gn) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < GK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = sA[kr * GS + wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = sB[kr * GS + wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // f64 16x16x4 C/D map: col = lane&15, row = (lane>>4) + 4*r
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        const int64_t col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (row < M && col < N) {
+          if (part)
+            part[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+          else
+            C[row * ldc + col] = alpha * acc[i][j][r];
+        }
+      }
+}
+
+__global__ void reduce_splitk_kernel(const double* __restrict__ part, int nsplit, int64_t M, int64_t N,
+                                     double alpha, double* __restrict__ C, int64_t ldc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  double s = 0.0;
+  for (int z = 0; z < nsplit; ++z) s += part[(int64_t)z * M * N + i];
+  const int64_t r = i / N, c = i - r * N;
+  C[r * ldc + c] = alpha * s;
+}
+
+template <class LA, class LB>
+static hipError_t gemm_t(hipStream_t s, const LA& A, const LB& B, int64_t M, int64_t N, int64_t K,
+                         double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
+  const int64_t mt = (M + GT - 1) / GT, nt = (N + GT - 1) / GT;
+  const int64_t ksteps = (K + GK - 1) / GK;
+  int64_t ns = 1;
+  const int64_t tiles = mt * nt;
+  if (tiles < 512 && work) {
+    ns = (1024 + tiles - 1) / tiles;
+    if (ns > ksteps) ns = ksteps;
+    if (ns > 256) ns = 256;
+    while (ns > 1 && (size_t)(ns * M * N) > work_elems) --ns;
+  }
+  const int64_t kps = ((ksteps + ns - 1) / ns) * GK;
+  ns = (K + kps - 1) / kps;
+  if (ns < 1) ns = 1;
+  const dim3 grid((unsigned)nt, (unsigned)mt, (unsigned)ns);
+  hipLaunchKernelGGL((gemm64_kernel<LA, LB>), grid, dim3(256), 0, s, A, B, M, N, K, kps, alpha, C, ldc,
+                     ns > 1 ? work : nullptr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ns == 1) return e;
+  const int64_t tot = M * N;
+  hipLaunchKernelGGL(reduce_splitk_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, work,
+                     (int)ns, M, N, alpha, C, ldc);
+  return hipGetLastError();
+}
+
+hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
+                  double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
+  if (A.u8) {
+    const U8Ld a{A.x, A.ld, A.trans, A.mu, A.w, A.trans == 0};
+    if (B.u8) {
+      const U8Ld b{B.x, B.ld, B.trans, B.mu, B.w, B.trans != 0};
+      return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+    }
+    const DenseLd b{B.p, B.ld, B.trans, B.trans != 0};
+    return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+  }
+  const DenseLd a{A.p, A.ld, A.trans, A.trans == 0};
+  if (B.u8) {
+    const U8Ld b{B.x, B.ld, B.trans, B.mu, B.w, B.trans != 0};
+    return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+  }
+  const DenseLd b{B.p, B.ld, B.trans, B.trans != 0};
+  return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+}
+
+// ------------------------------------------------------------- K4: Jacobi in LDS
+// Cyclic two-sided Jacobi for a symmetric m x m (m <= kJacobiMax) matrix, fully in LDS
+// (T and the accumulated rotations V, both fp64).  Each round applies m/2 disjoint
+// rotations (round-robin "circle" ordering) in parallel: rows, barrier, columns.
+// Output: eigenvalues descending, eigenvectors as columns of evecs (row-major m x m).
+__global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__ A, int m, int64_t lda,
+                                                      double* __restrict__ evals, double* __restrict__ evecs,
+                                                      int64_t ldv, int max_sweeps, int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) double jsm[];
+  const int mp = m + (m & 1);
+  const int S = mp + 1;
+  const int np = mp / 2;
+  double* T = jsm;
+  double* V = T + mp * S;
+  double* cs = V + mp * S;
+  double* sn = cs + np;
+  int* pp = reinterpret_cast<int*>(sn + np);
+  int* qq = pp + np;
+  int* flag = qq + np;
+  const int tid = threadIdx.x, nth = blockDim.x;
+
+  for (int e = tid; e < mp * mp; e += nth) {
+    const int i = e / mp, j = e - (e / mp) * mp;
+    double v = 0.0;
+    if (i < m && j < m) v = 0.5 * (A[(int64_t)i * lda + j] + A[(int64_t)j * lda + i]);
+    T[i * S + j] = v;
+    V[i * S + j] = (i == j) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+
+  int sweep = 0;
+  bool converged = false;
+  for (; sweep < max_sweeps; ++sweep) {
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    for (int r = 0; r < mp - 1; ++r) {
+      if (tid < np) {
+        auto pos = [&](int j) { return j == 0 ? 0 : 1 + ((j - 1 + r) % (mp - 1)); };
+        int p = pos(tid), q = pos(mp - 1 - tid);
+        if (p > q) { const int t = p; p = q; q = t; }
+        const double apq = T[p * S + q];
+        const double app = T[p * S + p], aqq = T[q * S + q];
+        const double g = 100.0 * fabs(apq);
+        if (apq == 0.0 || (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq))) {
+          pp[tid] = -1;
+        } else {
+          const double theta = (aqq - app) / (2.0 * apq);
+          double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+          if (fabs(theta) > 1e150) t = 0.5 / fabs(theta);
+          if (theta < 0.0) t = -t;
+          const double c = 1.0 / sqrt(t * t + 1.0);
+          cs[tid] = c;
+          sn[tid] = t * c;
+          pp[tid] = p;
+          qq[tid] = q;
+          *flag = 1;
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < np * mp; e += nth) {  // rows p, q  <- J^T T
+        const int i = e / mp, j = e - (e / mp) * mp;
+        const int p = pp[i];
+        if (p < 0) continue;
+        const int q = qq[i];
+        const double c = cs[i], s = sn[i];
+        const double tp = T[p * S + j], tq = T[q * S + j];
+        T[p * S + j] = c * tp - s * tq;
+        T[q * S + j] = s * tp + c * tq;
+      }
+      __syncthreads();
+      for (int e = tid; e < np * mp; e += nth) {  // columns p, q <- T J ; V <- V J
+        const int i = e / mp, rr = e - (e / mp) * mp;
+        const int p = pp[i];
+        if (p < 0) continue;
+        const int q = qq[i];
+        const double c = cs[i], s = sn[i];
+        const double tp = T[rr * S + p], tq = T[rr * S + q];
+        double np_ = c * tp - s * tq, nq_ = s * tp + c * tq;
+        if (rr == p) nq_ = 0.0;
+        if (rr == q) np_ = 0.0;
+        T[rr * S + p] = np_;
+        T[rr * S + q] = nq_;
+        const double vp = V[rr * S + p], vq = V[rr * S + q];
+        V[rr * S + p] = c * vp - s * vq;
+        V[rr * S + q] = s * vp + c * vq;
+      }
+      __syncthreads();
+    }
+    const int f = *flag;
+    __syncthreads();
+    if (f == 0) { converged = true; break; }
+  }
+
+  // descending sort by rank (ties -> lower index first); the padding index goes last
+  if (tid < mp) {
+    const int i = tid;
+    const bool dummy = (i >= m);
+    const double li = T[i * S + i];
+    int rank = mp - 1;
+    if (!dummy) {
+      rank = 0;
+      for (int j = 0; j < m; ++j) {
+        const double lj = T[j * S + j];
+        rank += (lj > li) || (lj == li && j < i);
+      }
+      evals[rank] = li;
+      for (int rr = 0; rr < m; ++rr) evecs[(int64_t)rr * ldv + rank] = V[rr * S + i];
+    }
+  }
+  if (tid == 0) *info = converged ? sweep + 1 : -1;
+}
+
+size_t jacobi_lds_bytes(int m) {
+  const int mp = m + (m & 1);
+  return (size_t)2 * mp * (mp + 1) * sizeof(double) + (size_t)mp * sizeof(double) +
+         (size_t)(mp + 2) * sizeof(int) + 16;
+}
+
+hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,
+                         int64_t ldv, int max_sweeps, int* info) {
+  if (m < 1 || m > kJacobiMax) return hipErrorInvalidValue;
+  const size_t lds = jacobi_lds_bytes(m);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(jacobi_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)jacobi_lds_bytes(kJacobiMax));
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(jacobi_kernel, dim3(1), dim3(1024), lds, s, A, m, lda, evals, evecs, ldv, max_sweeps,
+                     info);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ small helpers
+__global__ void trace_kernel(const double* __restrict__ C, int64_t m, int64_t ldc, double* out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += 256) s += C[i * ldc + i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void rand_init_kernel(double* __restrict__ Q, int64_t count, unsigned long long seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const unsigned long long r = splitmix64(seed ^ (unsigned long long)i * 0xD1B54A32D192ED03ull);
+  Q[i] = ((double)(r >> 11) * (1.0 / 9007199254740992.0)) * 2.0 - 1.0;
+}
+
+// W'[i][j] = W[i][j] / sqrt(max(lam[j], floor))  (Q <- Y W Lambda^{-1/2})
+__global__ void scale_cols_rsqrt_kernel(const double* __restrict__ W, int64_t rows, int cols,
+                                        const double* __restrict__ lam, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int j = (int)(i % cols);
+  double floor_ = lam[0] * 1e-28;
+  if (!(floor_ > 0.0)) floor_ = 1e-300;
+  const double l = lam[j] > floor_ ? lam[j] : floor_;
+  out[i] = W[i] / sqrt(l);
+}
+
+// Per column j of E (rows x cols, row-major, ld): unit-normalise (useless/train.py:94-95)
+// and apply sklearn's svd_flip row rule (largest-|.| entry positive, first on ties;
+// extmath.py:946-952).  Writes comps[j][r] (k x rows) and En[r][j] (rows x k).
+__global__ __launch_bounds__(256) void normalize_sign_kernel(const double* __restrict__ E, int64_t rows,
+                                                             int cols, int64_t ld,
+                                                             double* __restrict__ comps,
+                                                             double* __restrict__ En) {
+  __shared__ double rs[256];
+  __shared__ double rm[256];
+  __shared__ long long ri[256];
+  const int j = blockIdx.x;
+  double ss = 0.0, mx = -1.0;
+  long long mi = LLONG_MAX;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) {
+    const double v = E[r * ld + j];
+    ss += v * v;
+    const double a = fabs(v);
+    if (a > mx) { mx = a; mi = r; }
+  }
+  rs[threadIdx.x] = ss;
+  rm[threadIdx.x] = mx;
+  ri[threadIdx.x] = mi;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      rs[threadIdx.x] += rs[threadIdx.x + w];
+      const double om = rm[threadIdx.x + w];
+      const long long oi = ri[threadIdx.x + w];
+      if (om > rm[threadIdx.x] || (om == rm[threadIdx.x] && oi < ri[threadIdx.x])) {
+        rm[threadIdx.x] = om;
+        ri[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  const double nrm = sqrt(rs[0]);
+  const double piv = ri[0] == LLONG_MAX ? 1.0 : E[ri[0] * ld + j];
+  const double f = (piv < 0.0 ? -1.0 : 1.0) / (nrm > 0.0 ? nrm : 1.0);
+  for (int64_t r = threadIdx.x; r < rows; r += 256) {
+    const double v = E[r * ld + j] * f;
+    comps[(int64_t)j * rows + r] = v;
+    if (En) En[r * cols + j] = v;
+  }
+}
+
+hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
+                           unsigned long long* S1, unsigned long long* S2) {
+  const int64_t cgroups = (d + 255) / 256;
+  int64_t ny = (262144 + d - 1) / d;  // ~256K threads in flight
+  if (ny > n) ny = n;
+  if (ny < 1) ny = 1;
+  if (ny > 65535) ny = 65535;
+  const int64_t rows_per = (n + ny - 1) / ny;
+  ny = (n + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(colstats_kernel, dim3((unsigned)cgroups, (unsigned)ny), dim3(256), 0, s, X, n, d,
+                     rows_per, S1, S2);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,
+                                 int64_t n, int64_t d, int standardize, double* mean, double* var,
+                                 double* scale, double* w) {
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, S2,
+                     n, d, standardize, mean, var, scale, w);
+  return hipGetLastError();
+}
+
+hipError_t launch_trace(hipStream_t s, const double* C, int64_t m, int64_t ldc, double* out) {
+  hipLaunchKernelGGL(trace_kernel, dim3(1), dim3(256), 0, s, C, m, ldc, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rand_init(hipStream_t s, double* Q, int64_t count, unsigned long long seed) {
+  hipLaunchKernelGGL(rand_init_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, Q, count,
+                     seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_cols_rsqrt(hipStream_t s, const double* W, int64_t rows, int cols,
+                                   const double* lam, double* out) {
+  const int64_t tot = rows * cols;
+  hipLaunchKernelGGL(scale_cols_rsqrt_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, W,
+                     rows, cols, lam, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize_sign(hipStream_t s, const double* E, int64_t rows, int cols, int64_t ld,
+                                 double* comps, double* En) {
+  hipLaunchKernelGGL(normalize_sign_kernel, dim3((unsigned)cols), dim3(256), 0, s, E, rows, cols, ld,
+                     comps, En);
+  return hipGetLastError();
+}
+
+}  // namespace ef

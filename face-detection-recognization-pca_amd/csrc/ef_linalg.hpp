@@ -1,0 +1,84 @@
+// Fit-path (float64) kernel interfaces.
+#pragma once
+
+#include "ef_internal.hpp"
+
+namespace ef {
+
+// Loader semantics: L(r, c) = trans ? M[c][r] : M[r][c] for the stored row-major M.
+// A operands are read as A(m, k), B operands as B(k, n).  kfast tells the staging loop
+// which tile index is contiguous in memory so global reads coalesce.
+struct DenseLd {
+  const double* p;
+  int64_t ld;
+  int trans;
+  bool kfast;
+  __device__ __forceinline__ double operator()(int64_t r, int64_t c) const {
+    return trans ? p[c * ld + r] : p[r * ld + c];
+  }
+};
+
+// Stored M = X[sample][pixel] uint8; value = (x - mu[pixel]) * w[pixel] (w may be null).
+struct U8Ld {
+  const uint8_t* x;
+  int64_t ld;
+  int trans;
+  const double* mu;
+  const double* w;
+  bool kfast;
+  __device__ __forceinline__ double operator()(int64_t r, int64_t c) const {
+    const int64_t smp = trans ? c : r;
+    const int64_t px = trans ? r : c;
+    const double v = (double)x[smp * ld + px] - mu[px];
+    return w ? v * w[px] : v;
+  }
+};
+
+// Host-side operand description for gemm64.
+struct Operand {
+  bool u8 = false;
+  const double* p = nullptr;
+  const uint8_t* x = nullptr;
+  int64_t ld = 0;
+  int trans = 0;
+  const double* mu = nullptr;
+  const double* w = nullptr;
+  static Operand dense(const double* p, int64_t ld, bool trans) {
+    Operand o;
+    o.p = p;
+    o.ld = ld;
+    o.trans = trans;
+    return o;
+  }
+  static Operand pixels(const uint8_t* x, int64_t ld, bool trans, const double* mu, const double* w) {
+    Operand o;
+    o.u8 = true;
+    o.x = x;
+    o.ld = ld;
+    o.trans = trans;
+    o.mu = mu;
+    o.w = w;
+    return o;
+  }
+};
+
+// C[M][N] = alpha * A . B (split-K slabs in `work` when it helps; work may be null).
+hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
+                  double alpha, double* C, int64_t ldc, double* work, size_t work_elems);
+
+size_t jacobi_lds_bytes(int m);
+hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,
+                         int64_t ldv, int max_sweeps, int* info);
+hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
+                           unsigned long long* S1, unsigned long long* S2);
+hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,
+                                 int64_t n, int64_t d, int standardize, double* mean, double* var,
+                                 double* scale, double* w);
+hipError_t launch_trace(hipStream_t s, const double* C, int64_t m, int64_t ldc, double* out);
+hipError_t launch_rand_init(hipStream_t s, double* Q, int64_t count, unsigned long long seed);
+hipError_t launch_scale_cols_rsqrt(hipStream_t s, const double* W, int64_t rows, int cols,
+                                   const double* lam, double* out);
+hipError_t launch_normalize_sign(hipStream_t s, const double* E, int64_t rows, int cols, int64_t ld,
+                                 double* comps, double* En);
+
+}  // namespace ef

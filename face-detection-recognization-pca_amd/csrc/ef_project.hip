@@ -1,0 +1,227 @@
+// Probe projection f = (p - mean) . W  (SURVEY.md K6).
+//
+// Replaces project_face_to_eigenspace (useless/scan.py:93-96) and the folded
+// scaler.transform + pca.transform of extract_face_features (scan-template-v4.py:265-266),
+// batched over B probes.  uint8 pixels are converted and mean-subtracted while they are
+// staged into LDS (the centred matrix is never materialised in HBM).
+//
+// GEMM M=B probes, N=KPW (64|128) components, K=d pixels on v_mfma_f32_32x32x2_f32.
+// Workgroup tile 128 probes x KPW, BK=32 pixels per stage, double-buffered LDS with
+// register-staged prefetch.  K is split over gridDim.y into fp32 partial slabs that a
+// second kernel sums in a fixed order (deterministic) straight into the padded probe
+// buffer the search kernel reads.
+#include "ef_internal.hpp"
+
+namespace ef {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = kProjRowTile;  // 128 probes
+constexpr int BK = 32;            // pixels per stage
+constexpr int SA = BK + 4;        // LDS row stride of the pixel tile (conflict-free b128 reads)
+
+template <int KPW, int PDT, bool VEC>
+__global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict__ Pv, int64_t b,
+                                                         int64_t d, const float* __restrict__ mu,
+                                                         const float* __restrict__ W,
+                                                         float* __restrict__ part, int64_t bpad,
+                                                         int64_t pix_per_split) {
+  constexpr int WAVES_M = KPW == 128 ? 2 : 4;
+  constexpr int RW = BM / WAVES_M;            // rows per wave (64 | 32)
+  constexpr int AB = RW / 32;                 // A blocks per wave
+  constexpr int CW = KPW / (4 / WAVES_M);     // cols per wave (64)
+  constexpr int BB = CW / 32;                 // B blocks per wave
+  constexpr int SW = KPW;                     // LDS row stride of the W tile
+  constexpr int W4 = BK * KPW / 4;            // float4s per W tile
+  constexpr int W4_PT = W4 / 256;
+
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * SA];
+  __shared__ __attribute__((aligned(16))) float sW[2][BK * SW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int wm = wave / (4 / WAVES_M), wn = wave % (4 / WAVES_M);
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t k_beg = (int64_t)blockIdx.y * pix_per_split;
+  int64_t k_end = k_beg + pix_per_split;
+  if (k_end > d) k_end = d;
+  const int nsteps = (int)((k_end - k_beg + BK - 1) / BK);
+
+  // pixel staging: thread -> (row, 16-pixel half)
+  const int pr = tid >> 1, ph = (tid & 1) * 16;
+  float pv[16];
+  float4 wv[W4_PT];
+
+  auto load_stage = [&](int step) {
+    const int64_t kb = k_beg + (int64_t)step * BK;
+    const int64_t row = m0 + pr;
+    const int64_t px0 = kb + ph;
+    if constexpr (PDT == EF_U8) {
+      const uint8_t* P = reinterpret_cast<const uint8_t*>(Pv);
+      if (VEC && row < b && px0 + 16 <= k_end) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(P + row * d + px0);
+        const unsigned w4[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pv[j] = (float)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          pv[j] = (row < b && px0 + j < k_end) ? (float)P[row * d + px0 + j] : 0.f;
+      }
+    } else {
+      const float* P = reinterpret_cast<const float*>(Pv);
+      if (VEC && row < b && px0 + 16 <= k_end) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 v = *reinterpret_cast<const float4*>(P + row * d + px0 + 4 * j);
+          pv[4 * j] = v.x; pv[4 * j + 1] = v.y; pv[4 * j + 2] = v.z; pv[4 * j + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pv[j] = (row < b && px0 + j < k_end) ? P[row * d + px0 + j] : 0.f;
+      }
+    }
+    // mean subtraction fused into the operand load (K2); padded rows/pixels stay 0
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t px = px0 + j;
+      if (row < b && px < k_end) pv[j] -= mu[px];
+    }
+#pragma unroll
+    for (int j = 0; j < W4_PT; ++j) {
+      const int idx = tid + 256 * j;
+      const int kr = idx / (KPW / 4), c4 = idx % (KPW / 4);
+      const int64_t px = kb + kr;
+      wv[j] = px < k_end ? reinterpret_cast<const float4*>(W + px * KPW)[c4]
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float* a = &sA[buf][pr * SA + ph];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<float4*>(a + 4 * j) = make_float4(pv[4 * j], pv[4 * j + 1], pv[4 * j + 2], pv[4 * j + 3]);
+#pragma unroll
+    for (int j = 0; j < W4_PT; ++j) {
+      const int idx = tid + 256 * j;
+      const int kr = idx / (KPW / 4), c4 = idx % (KPW / 4);
+      *reinterpret_cast<float4*>(&sW[buf][kr * SW + c4 * 4]) = wv[j];
+    }
+  };
+
+  f32x16 acc[AB][BB];
+#pragma unroll
+  for (int i = 0; i < AB; ++i)
+#pragma unroll
+    for (int j = 0; j < BB; ++j) acc[i][j] = f32x16{};
+
+  if (nsteps > 0) {
+    load_stage(0);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const bool more = st + 1 < nsteps;
+    if (more) load_stage(st + 1);
+    // k permutation inside the stage: lane half h owns pixels [16h, 16h+16)
+#pragma unroll
+    for (int s4 = 0; s4 < 16; s4 += 4) {
+      float4 a[AB];
+#pragma unroll
+      for (int i = 0; i < AB; ++i)
+        a[i] = *reinterpret_cast<const float4*>(&sA[buf][(wm * RW + i * 32 + c32) * SA + 16 * h + s4]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float bv[BB];
+#pragma unroll
+        for (int j = 0; j < BB; ++j) bv[j] = sW[buf][(16 * h + s4 + e) * SW + wn * CW + j * 32 + c32];
+#pragma unroll
+        for (int i = 0; i < AB; ++i) {
+          const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
+#pragma unroll
+          for (int j = 0; j < BB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // partial slab [split][bpad][KPW]; col = lane&31, row = (r&3) + 8(r>>2) + 4h
+  float* out = part + (int64_t)blockIdx.y * bpad * KPW;
+#pragma unroll
+  for (int i = 0; i < AB; ++i)
+#pragma unroll
+    for (int j = 0; j < BB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * RW + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * CW + j * 32 + c32;
+        out[row * KPW + col] = acc[i][j][r];
+      }
+}
+
+// qpad[row][c] = sum_z part[z][row][c] (c < kp, rows < bpad; fixed z order);
+// f_out[row][c] for row < b, c < k when requested.
+__global__ void project_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t b,
+                                      int64_t bpad, int kpw, int k, int kp, float* __restrict__ qpad,
+                                      float* __restrict__ f_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= bpad * kp) return;
+  const int64_t row = i / kp;
+  const int c = (int)(i - row * kp);
+  float s = 0.f;
+  if (row < b && c < k)
+    for (int z = 0; z < nsplit; ++z) s += part[((int64_t)z * bpad + row) * kpw + c];
+  qpad[i] = s;
+  if (f_out && row < b && c < k) f_out[row * k + c] = s;
+}
+
+int project_nsplit(int64_t bpad, int64_t d, int64_t* pix_per_split) {
+  const int64_t mtiles = bpad / BM;
+  int64_t ns = (512 + mtiles - 1) / mtiles;  // ~2 workgroups per CU
+  const int64_t steps = (d + BK - 1) / BK;
+  if (ns > steps) ns = steps;
+  if (ns < 1) ns = 1;
+  if (ns > 64) ns = 64;
+  const int64_t steps_per = (steps + ns - 1) / ns;
+  *pix_per_split = steps_per * BK;
+  return (int)((d + *pix_per_split - 1) / *pix_per_split);
+}
+
+template <int KPW, int PDT>
+static hipError_t proj_t(hipStream_t s, const void* P, int64_t b, int64_t bpad, int64_t d,
+                         const float* mean, const float* W, float* part, int nsplit, int64_t pps) {
+  const dim3 grid((unsigned)(bpad / BM), (unsigned)nsplit);
+  const bool vec = (d % 16 == 0) && ((reinterpret_cast<uintptr_t>(P) & 15) == 0) && (pps % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL((project_kernel<KPW, PDT, true>), grid, dim3(256), 0, s, P, b, d, mean, W, part,
+                       bpad, pps);
+  else
+    hipLaunchKernelGGL((project_kernel<KPW, PDT, false>), grid, dim3(256), 0, s, P, b, d, mean, W,
+                       part, bpad, pps);
+  return hipGetLastError();
+}
+
+hipError_t launch_project(hipStream_t s, int kpw, int p_dtype, const void* P, int64_t b,
+                          int64_t bpad, int64_t d, const float* mean, const float* W, float* part,
+                          int nsplit, int64_t pps) {
+  if (kpw == 64)
+    return p_dtype == EF_U8 ? proj_t<64, EF_U8>(s, P, b, bpad, d, mean, W, part, nsplit, pps)
+                            : proj_t<64, EF_F32>(s, P, b, bpad, d, mean, W, part, nsplit, pps);
+  if (kpw == 128)
+    return p_dtype == EF_U8 ? proj_t<128, EF_U8>(s, P, b, bpad, d, mean, W, part, nsplit, pps)
+                            : proj_t<128, EF_F32>(s, P, b, bpad, d, mean, W, part, nsplit, pps);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, int64_t b,
+                                 int64_t bpad, int kpw, int k, int kp, float* qpad, float* f_out) {
+  const int64_t tot = bpad * kp;
+  hipLaunchKernelGGL(project_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part,
+                     nsplit, b, bpad, kpw, k, kp, qpad, f_out);
+  return hipGetLastError();
+}
+
+}  // namespace ef

@@ -1,0 +1,520 @@
+// Distance GEMM with fused arg-best epilogue.
+//
+// Replaces `cosine_similarity([f], face_features)` + `np.argmax`
+// (scan-template-v4.py:274-275) and the per-row Python loop of useless/scan.py:122-127,
+// batched over B probes, plus the north-star L2 argmin.
+//
+// Layout in HBM:  gallery G[n][KP] fp32 (k zero-padded to KP), gnorm2[n], ginv[n];
+// probe features Qp[bpad][KP] (bpad a multiple of 256).
+//
+// Pass 1 — search_kernel (the hot kernel, v_mfma_f32_32x32x2_f32, exact fp32):
+//   * workgroup = 4 waves = 256 probes; each wave keeps 64 probes (two 32-probe
+//     B-operand blocks, KP/2 fp32 VGPRs each) in registers for the whole sweep;
+//   * the workgroup sweeps one chunk of the gallery in 32-row tiles staged through
+//     double-buffered LDS (register-staged prefetch of tile t+1 under tile t's MFMAs);
+//   * the gallery tile is the MFMA A operand so each lane's 16 accumulators hold 16
+//     gallery rows of ONE probe: the arg-best is an in-lane running (best, index,
+//     runner-up) with no cross-lane traffic until one __shfl_xor(32) at the end;
+//   * K is permuted (lane half h owns k in [h*KP/2, (h+1)*KP/2)) so every A fragment is a
+//     conflict-free ds_read_b128 feeding 4 MFMAs;
+//   * blockIdx is remapped so the workgroups sharing a gallery chunk run on one XCD
+//     (same blockIdx % 8) and hit its L2;
+//   * each workgroup writes its per-probe (best key, runner-up score) for its chunk.
+// Pass 2 — reduce_kernel: per probe, min over chunks -> winner + global runner-up; the
+//   winner is re-scored in fp64 (difference form for L2).  A rigorous fp32 error bound
+//   decides whether the runner-up could beat the winner; if so the probe is queued.
+// Pass 3 (only for queued probes; a no-op launch otherwise) — the search kernel in
+//   COLLECT mode gathers every row whose fp32 score is within the bound, and
+//   resolve_kernel re-scores them in fp64 and keeps the lowest index among exact ties.
+// Result: the argmin/argmax identity equals an fp64 evaluation with lowest-index
+// tie-break (np.argmin / np.argmax semantics), independent of fp32 rounding.
+#include "ef_internal.hpp"
+
+#include <climits>
+#include <cmath>
+
+namespace ef {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ long long pack_key(float v, unsigned idx) {
+  if (v == 0.0f) v = 0.0f;  // canonical +0 so that -0 and +0 tie on index
+  int b = __float_as_int(v);
+  int s = b >= 0 ? b : (b ^ 0x7FFFFFFF);
+  return (long long)(((unsigned long long)(unsigned)s << 32) | (unsigned long long)idx);
+}
+__device__ __forceinline__ float key_value(long long key) {
+  const int s = (int)(key >> 32);
+  return __int_as_float(s >= 0 ? s : (s ^ 0x7FFFFFFF));
+}
+
+constexpr int TG = 32;  // gallery rows per tile
+
+template <int KP, int METRIC, bool COLLECT>
+__global__ __launch_bounds__(256, 2) void search_kernel(
+    const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
+    int n_ptiles, int tiles_per_chunk, int64_t bpad, SearchWs ws) {
+  constexpr int KH = KP / 2;
+  constexpr int LDS_STRIDE = KP + 4;
+  constexpr int F4_ROW = KP / 4;
+  constexpr int F4_TILE = TG * F4_ROW;
+  constexpr int F4_PER_THREAD = (F4_TILE + 255) / 256;
+
+  __shared__ __attribute__((aligned(16))) float sG[2][TG * LDS_STRIDE];
+  __shared__ __attribute__((aligned(16))) float sAux[2][TG];
+
+  // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD a contiguous run of
+  // (chunk, probe-tile) pairs so the probe tiles of one chunk are co-resident on it.
+  const int total = gridDim.x;  // host guarantees total % 8 == 0
+  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+  const int gc = lin / n_ptiles;
+  const int pt = lin - gc * n_ptiles;
+
+  int n_amb = 0;
+  if constexpr (COLLECT) {
+    n_amb = *ws.amb_count;
+    if (pt * 256 >= n_amb) return;  // uniform: nothing queued for this probe tile
+  }
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+
+  const int64_t tiles_total = (n + TG - 1) / TG;
+  const int64_t t0 = (int64_t)gc * tiles_per_chunk;
+  const int64_t t1 = t0 + tiles_per_chunk < tiles_total ? t0 + tiles_per_chunk : tiles_total;
+
+  // probe slots of this lane (two 32-probe blocks)
+  const int64_t s0 = (int64_t)pt * 256 + wave * 64 + c32;
+  const int64_t s1 = s0 + 32;
+
+  if (t0 >= t1) {  // empty chunk: publish "no candidate" so the reducer can skip it
+    if constexpr (!COLLECT) {
+      if (h == 0) {
+        ws.part_key[(int64_t)gc * bpad + s0] = LLONG_MAX;
+        ws.part_key[(int64_t)gc * bpad + s1] = LLONG_MAX;
+        ws.part_b2[(int64_t)gc * bpad + s0] = __builtin_inff();
+        ws.part_b2[(int64_t)gc * bpad + s1] = __builtin_inff();
+      }
+    }
+    return;
+  }
+
+  // Probe fragments (B operand): lane holds probe (c32) of each block, k in [h*KH, h*KH+KH).
+  float qb0[KH], qb1[KH];
+  {
+    int64_t r0 = s0, r1 = s1;
+    bool v0 = true, v1 = true;
+    if constexpr (COLLECT) {
+      v0 = s0 < n_amb;
+      v1 = s1 < n_amb;
+      r0 = v0 ? ws.amb_list[s0] : 0;
+      r1 = v1 ? ws.amb_list[s1] : 0;
+    }
+    const float4* q0 = reinterpret_cast<const float4*>(qpad + r0 * KP + h * KH);
+    const float4* q1 = reinterpret_cast<const float4*>(qpad + r1 * KP + h * KH);
+#pragma unroll
+    for (int j = 0; j < KH / 4; ++j) {
+      float4 a = v0 ? q0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 b = v1 ? q1[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      qb0[4 * j] = a.x; qb0[4 * j + 1] = a.y; qb0[4 * j + 2] = a.z; qb0[4 * j + 3] = a.w;
+      qb1[4 * j] = b.x; qb1[4 * j + 1] = b.y; qb1[4 * j + 2] = b.z; qb1[4 * j + 3] = b.w;
+    }
+  }
+  float thr0 = -__builtin_inff(), thr1 = -__builtin_inff();
+  if constexpr (COLLECT) {
+    if (s0 < n_amb) thr0 = ws.thr[s0];
+    if (s1 < n_amb) thr1 = ws.thr[s1];
+  }
+
+  const float4* G4 = reinterpret_cast<const float4*>(G);
+  float4 stage[F4_PER_THREAD];
+  float stage_aux = 0.f;
+
+  auto load_tile = [&](int64_t t) {
+#pragma unroll
+    for (int j = 0; j < F4_PER_THREAD; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < F4_TILE) {
+        const int row = idx / F4_ROW;
+        const int c4 = idx - row * F4_ROW;
+        const int64_t grow = t * TG + row;
+        stage[j] = grow < n ? G4[grow * F4_ROW + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (tid < TG) {
+      const int64_t grow = t * TG + tid;
+      stage_aux = grow < n ? aux[grow] : 0.f;  // padded rows are masked in the epilogue
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < F4_PER_THREAD; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < F4_TILE) {
+        const int row = idx / F4_ROW;
+        const int c4 = idx - row * F4_ROW;
+        *reinterpret_cast<float4*>(&sG[buf][row * LDS_STRIDE + c4 * 4]) = stage[j];
+      }
+    }
+    if (tid < TG) sAux[buf][tid] = stage_aux;
+  };
+
+  const float INF = __builtin_inff();
+  float b1_0 = INF, b2_0 = INF, b1_1 = INF, b2_1 = INF;
+  int i1_0 = INT_MAX, i1_1 = INT_MAX;
+
+  load_tile(t0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int64_t t = t0; t < t1; ++t) {
+    const int buf = (int)((t - t0) & 1);
+    const bool more = t + 1 < t1;
+    if (more) load_tile(t + 1);
+
+    f32x16 acc0 = {}, acc1 = {};
+    const float* arow = &sG[buf][c32 * LDS_STRIDE + h * KH];
+#pragma unroll
+    for (int s = 0; s < KH; s += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(arow + s);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb1[s], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qb0[s + 1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qb1[s + 1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qb0[s + 2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qb1[s + 2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qb0[s + 3], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qb1[s + 3], acc1, 0, 0, 0);
+    }
+
+    // Epilogue: accumulator register r holds gallery row (r&3) + 8*(r>>2) + 4*h.
+    const int rowbase = (int)(t * TG);
+    const bool tail = (t + 1) * TG > n;  // uniform; only the last tile has padded rows
+    auto epilogue = [&](auto mask_c) {
+      constexpr bool MASK = decltype(mask_c)::value;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 a4 = *reinterpret_cast<const float4*>(&sAux[buf][8 * q + 4 * h]);
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q + e;
+          const int row = rowbase + 8 * q + 4 * h + e;
+          float v0, v1;
+          if constexpr (METRIC == EF_METRIC_L2) {
+            v0 = __builtin_fmaf(-2.f, acc0[r], av[e]);
+            v1 = __builtin_fmaf(-2.f, acc1[r], av[e]);
+          } else {
+            v0 = -(acc0[r] * av[e]);
+            v1 = -(acc1[r] * av[e]);
+          }
+          if constexpr (MASK) {
+            if (row >= n) { v0 = INF; v1 = INF; }
+          }
+          if constexpr (COLLECT) {
+            if (v0 <= thr0) {
+              const int pos = atomicAdd(&ws.cand_cnt[s0], 1);
+              if (pos < kCandMax) ws.cand[s0 * kCandMax + pos] = row;
+            }
+            if (v1 <= thr1) {
+              const int pos = atomicAdd(&ws.cand_cnt[s1], 1);
+              if (pos < kCandMax) ws.cand[s1 * kCandMax + pos] = row;
+            }
+          } else {
+            // running (best, index, runner-up); strict '<' keeps the lowest row on ties
+            b2_0 = fminf(b2_0, fmaxf(b1_0, v0));
+            if (v0 < b1_0) { b1_0 = v0; i1_0 = row; }
+            b2_1 = fminf(b2_1, fmaxf(b1_1, v1));
+            if (v1 < b1_1) { b1_1 = v1; i1_1 = row; }
+          }
+        }
+      }
+    };
+    if (tail)
+      epilogue(std::integral_constant<bool, true>{});
+    else
+      epilogue(std::integral_constant<bool, false>{});
+
+    if (more) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  if constexpr (!COLLECT) {
+    // Merge the two lane halves (same probe, disjoint rows).
+    auto merge = [&](float& b1, int& i1, float& b2) {
+      const float ob1 = __shfl_xor(b1, 32);
+      const int oi1 = __shfl_xor(i1, 32);
+      const float ob2 = __shfl_xor(b2, 32);
+      const bool other = ob1 < b1 || (ob1 == b1 && oi1 < i1);
+      const float lose = other ? b1 : ob1;
+      b2 = fminf(fminf(b2, ob2), lose);
+      if (other) { b1 = ob1; i1 = oi1; }
+    };
+    merge(b1_0, i1_0, b2_0);
+    merge(b1_1, i1_1, b2_1);
+    if (h == 0) {
+      const int64_t o = (int64_t)gc * bpad;
+      ws.part_key[o + s0] = i1_0 == INT_MAX ? LLONG_MAX : pack_key(b1_0, (unsigned)i1_0);
+      ws.part_key[o + s1] = i1_1 == INT_MAX ? LLONG_MAX : pack_key(b1_1, (unsigned)i1_1);
+      ws.part_b2[o + s0] = b2_0;
+      ws.part_b2[o + s1] = b2_1;
+    }
+  }
+}
+
+// fp64 score of gallery row `row` for probe q (L2: squared distance in difference form;
+// cosine: -q.g/(|q||g|), 0 for a zero vector — sklearn normalize semantics).
+template <int KP, int METRIC>
+__device__ __forceinline__ double score64(const float* __restrict__ q, const float* __restrict__ g, int lane) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int c = lane; c < KP; c += 64) {
+    const double qv = q[c], gv = g[c];
+    if constexpr (METRIC == EF_METRIC_L2) {
+      const double dv = qv - gv;
+      s0 = fma(dv, dv, s0);
+    } else {
+      s0 = fma(qv, gv, s0);
+      s1 = fma(qv, qv, s1);
+      s2 = fma(gv, gv, s2);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    if constexpr (METRIC != EF_METRIC_L2) {
+      s1 += __shfl_xor(s1, off);
+      s2 += __shfl_xor(s2, off);
+    }
+  }
+  if constexpr (METRIC == EF_METRIC_L2) {
+    return s0;
+  } else {
+    return (s1 > 0.0 && s2 > 0.0) ? -(s0 / (sqrt(s1) * sqrt(s2))) : 0.0;
+  }
+}
+
+// One wave per probe: winner over chunks, global runner-up, fp64 re-score, ambiguity test.
+template <int KP, int METRIC>
+__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ qpad, int64_t b, int64_t bpad,
+                                                     int nchunks, const float* __restrict__ G, int64_t n,
+                                                     int64_t g_offset, float gmax2, SearchWs ws,
+                                                     long long* __restrict__ keys) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= b) return;
+  long long kmin = LLONG_MAX;
+  for (int c = lane; c < nchunks; c += 64) {
+    const long long k = ws.part_key[(int64_t)c * bpad + p];
+    kmin = k < kmin ? k : kmin;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const long long o = __shfl_xor(kmin, off);
+    kmin = o < kmin ? o : kmin;
+  }
+  if (kmin == LLONG_MAX) {  // empty gallery
+    if (lane == 0) keys[p] = LLONG_MAX;
+    return;
+  }
+  float r2 = __builtin_inff();
+  for (int c = lane; c < nchunks; c += 64) {
+    const long long k = ws.part_key[(int64_t)c * bpad + p];
+    r2 = fminf(r2, ws.part_b2[(int64_t)c * bpad + p]);
+    if (k != kmin && k != LLONG_MAX) r2 = fminf(r2, key_value(k));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) r2 = fminf(r2, __shfl_xor(r2, off));
+
+  const float b1 = key_value(kmin);
+  const unsigned row = (unsigned)(kmin & 0xffffffffll);
+  const float* q = qpad + p * KP;
+  const double v = score64<KP, METRIC>(q, G + (int64_t)row * KP, lane);
+  // rigorous bound on |fp32 score - exact score| (fp32 FMA chain of KP terms,
+  // fp32 ||g||^2 / 1/||g||, final rounding), doubled for the two compared scores
+  float qq = 0.f;
+  for (int c = lane; c < KP; c += 64) qq = __builtin_fmaf(q[c], q[c], qq);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) qq += __shfl_xor(qq, off);
+  const float u = 5.9604645e-08f;  // 2^-24
+  const float qn = sqrtf(qq);
+  float delta;
+  if constexpr (METRIC == EF_METRIC_L2) {
+    const float gm = sqrtf(gmax2);
+    delta = 2.f * ((KP + 4) * u * 1.01f * (2.f * qn * gm + gmax2) + 4.f * u * fabsf(b1));
+  } else {
+    delta = 2.f * ((KP + 8) * u * 1.01f * qn) + 1e-30f;
+  }
+  delta *= 2.f;  // safety factor
+  if (lane == 0) {
+    keys[p] = pack_key((float)v, (unsigned)(row + g_offset));
+    if (r2 - b1 <= delta) {
+      const int slot = atomicAdd(ws.amb_count, 1);
+      ws.amb_list[slot] = (int)p;
+      ws.thr[slot] = b1 + delta;
+      ws.cand_cnt[slot] = 0;
+    }
+  }
+}
+
+// fp64 resolution of queued probes: lowest index among candidates whose fp64 score is
+// within 1e-12 (relative) of the best — exact ties resolve like np.argmin/argmax.
+template <int KP, int METRIC>
+__global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ qpad, const float* __restrict__ G,
+                                                      int64_t n, int64_t g_offset, float gmax2, SearchWs ws,
+                                                      long long* __restrict__ keys) {
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (slot >= *ws.amb_count) return;
+  const int64_t p = ws.amb_list[slot];
+  const float* q = qpad + p * KP;
+  const int cnt = ws.cand_cnt[slot];
+  const bool overflow = cnt > kCandMax;
+  const int64_t m = overflow ? n : cnt;
+  auto row_of = [&](int64_t j) -> int64_t { return overflow ? j : (int64_t)ws.cand[slot * kCandMax + j]; };
+  double vmin = INFINITY;
+  for (int64_t j = 0; j < m; ++j) {
+    const double v = score64<KP, METRIC>(q, G + row_of(j) * KP, lane);
+    vmin = v < vmin ? v : vmin;
+  }
+  double qq = 0.0;
+  for (int c = lane; c < KP; c += 64) qq = fma((double)q[c], (double)q[c], qq);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) qq += __shfl_xor(qq, off);
+  const double scale = METRIC == EF_METRIC_L2 ? qq + (double)gmax2 : 1.0;
+  const double tol = 1e-12 * (fabs(vmin) + scale);
+  int64_t best_row = LLONG_MAX;
+  double best_v = vmin;
+  for (int64_t j = 0; j < m; ++j) {
+    const int64_t r = row_of(j);
+    const double v = score64<KP, METRIC>(q, G + r * KP, lane);
+    if (v <= vmin + tol && r < best_row) { best_row = r; best_v = v; }
+  }
+  if (lane == 0 && best_row != LLONG_MAX) keys[p] = pack_key((float)best_v, (unsigned)(best_row + g_offset));
+}
+
+// dst[rows_pad][kp] <- src[rows][k] with zero padding.
+__global__ void pad_rows_kernel(const float* __restrict__ src, int64_t rows, int k, int64_t rows_pad,
+                                float* __restrict__ dst, int kp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_pad * kp) return;
+  const int64_t r = i / kp;
+  const int c = (int)(i - r * kp);
+  dst[i] = (r < rows && c < k) ? src[r * k + c] : 0.f;
+}
+
+// ||g||^2 and 1/||g|| per gallery row (K7: computed once at enrolment, not per probe as
+// sklearn's cosine_similarity does, pairwise.py:1734), and max ||g||^2 for the bound.
+__global__ void gallery_aux_kernel(const float* __restrict__ G, int64_t n, int kp, float* __restrict__ gnorm2,
+                                   float* __restrict__ ginv, unsigned* __restrict__ gmax2_bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < kp; c += 64) {
+    const float v = G[row * kp + c];
+    s = __builtin_fmaf(v, v, s);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) {
+    gnorm2[row] = s;
+    ginv[row] = s > 0.f ? 1.0f / sqrtf(s) : 0.f;
+    atomicMax(gmax2_bits, __float_as_uint(s));  // non-negative floats order as uints
+  }
+}
+
+// ------------------------------------------------------------------------ launchers
+SearchPlan search_plan(int64_t bpad, int64_t n) {
+  SearchPlan pl;
+  pl.n_ptiles = (int)(bpad / kSearchProbeTile);
+  const int64_t tiles = (n + TG - 1) / TG;
+  // ~2048 workgroups (>= 4 resident waves per SIMD over the launch); the chunk count is a
+  // multiple of 8 so the XCD remap is a bijection.
+  int64_t want = (2048 + pl.n_ptiles - 1) / pl.n_ptiles;
+  if (want > tiles) want = tiles;
+  if (want < 1) want = 1;
+  pl.nchunks = (int)(((want + 7) / 8) * 8);
+  pl.tiles_per_chunk = (int)((tiles + pl.nchunks - 1) / pl.nchunks);
+  if (pl.tiles_per_chunk < 1) pl.tiles_per_chunk = 1;
+  return pl;
+}
+
+template <int KP, int M>
+static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpad, int64_t bpad, int64_t b,
+                           const float* G, const float* aux, int64_t n, int64_t g_offset, float gmax2,
+                           const SearchWs& ws, long long* keys, bool timed_main, TimerEvt* tev, ef_ctx* c) {
+  const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
+  if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
+  hipLaunchKernelGGL((search_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
+                     pl.tiles_per_chunk, bpad, ws);
+  if (timed_main) timer_end(c, tev);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
+  if (e != hipSuccess) return e;
+  const dim3 pgrid((unsigned)((b + 3) / 4));
+  hipLaunchKernelGGL((reduce_kernel<KP, M>), pgrid, block, 0, s, qpad, b, bpad, pl.nchunks, G, n, g_offset,
+                     gmax2, ws, keys);
+  // queued (fp32-ambiguous) probes: collect + fp64 resolve; both exit at once when none
+  hipLaunchKernelGGL((search_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
+                     pl.tiles_per_chunk, bpad, ws);
+  hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, block, 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
+                         int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
+                         float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c) {
+  TimerEvt tev;
+  tev.kernel = -1;
+#define EF_SEARCH_CASE(KPV)                                                                                 \
+  case KPV:                                                                                                 \
+    return metric == EF_METRIC_L2                                                                           \
+               ? search_t<KPV, EF_METRIC_L2>(s, pl, qpad, bpad, b, G, aux, n, g_offset, gmax2, ws, keys, true, \
+                                             &tev, c)                                                       \
+               : search_t<KPV, EF_METRIC_COSINE>(s, pl, qpad, bpad, b, G, aux, n, g_offset, gmax2, ws, keys,  \
+                                                 true, &tev, c);
+  switch (kp) {
+    EF_SEARCH_CASE(16)
+    EF_SEARCH_CASE(32)
+    EF_SEARCH_CASE(64)
+    EF_SEARCH_CASE(96)
+    EF_SEARCH_CASE(128)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef EF_SEARCH_CASE
+}
+
+__global__ void keys_fill_kernel(long long* keys, int64_t b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < b) keys[i] = LLONG_MAX;
+}
+
+hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b) {
+  hipLaunchKernelGGL(keys_fill_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, s, keys, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad, float* dst,
+                           int kp) {
+  const int64_t tot = rows_pad * kp;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, rows, k,
+                     rows_pad, dst, kp);
+  return hipGetLastError();
+}
+
+hipError_t launch_gallery_aux(hipStream_t s, const float* G, int64_t n, int kp, float* gnorm2, float* ginv,
+                              unsigned* gmax2_bits) {
+  hipError_t e = hipMemsetAsync(gmax2_bits, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gallery_aux_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, G, n, kp, gnorm2, ginv,
+                     gmax2_bits);
+  return hipGetLastError();
+}
+
+}  // namespace ef

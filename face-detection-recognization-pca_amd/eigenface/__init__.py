@@ -1,0 +1,21 @@
+"""eigenface — MI355X-native eigenfaces engine (fit + projection + nearest neighbour).
+
+Drop-in for the PCA / recognition hot path of saladbkp/face-detection-recognization-PCA
+(train-v4.py, scan-template-v4.py, useless/train.py, useless/scan.py), executed by
+hand-written gfx950 HIP kernels in ``_lib/libeigenface.so`` (no CPU fallback).
+"""
+from ._native import EigenfaceError, NativeLibraryError, LIB_PATH  # noqa: F401
+from .engine import Engine, FitResult, decode_keys, device_count  # noqa: F401
+from .pca import (  # noqa: F401
+    EigenfacePCA,
+    get_engine,
+    manual_pca,
+    recognize_face,
+    recognize_face_with_model,
+)
+
+__all__ = [
+    "Engine", "FitResult", "decode_keys", "device_count", "EigenfacePCA", "get_engine",
+    "manual_pca", "recognize_face", "recognize_face_with_model", "EigenfaceError",
+    "NativeLibraryError", "LIB_PATH",
+]

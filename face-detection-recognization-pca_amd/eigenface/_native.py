@@ -1,0 +1,93 @@
+"""ctypes binding of libeigenface.so (include/eigenface.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be
+loaded, every entry point raises ``NativeLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libeigenface.so")
+
+EF_OK = 0
+EF_U8, EF_F32, EF_F64 = 0, 1, 2
+EF_METRIC_L2, EF_METRIC_COSINE = 0, 1
+EF_FIT_STANDARDIZE = 0x1
+EF_MEM_DEVICE = 0x100
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT = 0, 1
+EF_KEY_NONE = (1 << 63) - 1
+
+_ERRNAMES = {-1: "EF_E_INVALID", -2: "EF_E_HIP", -3: "EF_E_STATE", -4: "EF_E_NOMEM", -5: "EF_E_NUMERIC"}
+
+
+class NativeLibraryError(RuntimeError):
+    """libeigenface.so is missing or unusable (there is no CPU fallback)."""
+
+
+class EigenfaceError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+vp, i32, i64, u32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32
+
+_SIGS = {
+    "ef_api_version": ([], C.c_int),
+    "ef_device_count": ([C.POINTER(C.c_int)], C.c_int),
+    "ef_create": ([C.c_int, C.POINTER(vp)], C.c_int),
+    "ef_destroy": ([vp], None),
+    "ef_last_error": ([vp], C.c_char_p),
+    "ef_set_stream": ([vp, vp], C.c_int),
+    "ef_synchronize": ([vp], C.c_int),
+    "ef_fit": ([vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+    "ef_model_set": ([vp, vp, vp, i64, i32, u32], C.c_int),
+    "ef_project": ([vp, vp, i32, i64, vp, u32], C.c_int),
+    "ef_gallery_set": ([vp, vp, i64, i32, i64, u32], C.c_int),
+    "ef_search": ([vp, vp, i64, i32, vp, u32], C.c_int),
+    "ef_recognize": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
+    "ef_keys_decode": ([vp, i64, i32, vp, vp], None),
+    "ef_timing_enable": ([vp, C.c_int], C.c_int),
+    "ef_timing_get": ([vp, i32, C.POINTER(C.c_double), C.POINTER(i64)], C.c_int),
+    "ef_timing_reset": ([vp], C.c_int),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise loudly when unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"{LIB_PATH} not found: build it with `make -C face-detection-recognization-pca_amd` "
+                "or __graft_entry__.build() (there is no CPU fallback)")
+        try:
+            h = C.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = res
+        if h.ef_api_version() != 1:
+            raise NativeLibraryError("libeigenface.so API version mismatch")
+        _lib = h
+        return h
+
+
+def check(ctx, rc):
+    if rc != EF_OK:
+        msg = lib().ef_last_error(ctx)
+        raise EigenfaceError(rc, msg.decode() if msg else "")
+    return rc

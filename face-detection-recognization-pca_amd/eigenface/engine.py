@@ -1,0 +1,268 @@
+"""Thin Python layer over the C ABI: one ``Engine`` per GPU.
+
+Arrays may be NumPy (host; the call copies in/out and synchronises) or torch-ROCm
+CUDA tensors (device; zero-copy, stream-ordered, no synchronisation).  One call must
+not mix the two.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+METRICS = {"l2": N.EF_METRIC_L2, "cosine": N.EF_METRIC_COSINE}
+
+
+def _is_dev(x):
+    return x is not None and hasattr(x, "data_ptr") and getattr(x, "is_cuda", False)
+
+
+def _host(x, dtype):
+    a = np.ascontiguousarray(x, dtype=dtype)
+    return a, a.ctypes.data
+
+
+def _dev(x, torch_dtype):
+    if x.dtype != torch_dtype:
+        raise TypeError(f"expected {torch_dtype}, got {x.dtype}")
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return x, x.data_ptr()
+
+
+def _metric(m):
+    if isinstance(m, str):
+        return METRICS[m.lower()]
+    return int(m)
+
+
+@dataclass
+class FitResult:
+    """Outputs of the GPU fit (float64).  ``components`` is k x d (rows =
+    eigenfaces, sklearn ``components_``); manual_pca's ``eigenfaces`` is its
+    transpose."""
+
+    mean: np.ndarray
+    var: np.ndarray
+    scale: np.ndarray
+    components: np.ndarray
+    eigenvalues: np.ndarray
+    projection: np.ndarray | None
+    total_var: float
+    k: int
+    iters: int
+
+
+class Engine:
+    """A libeigenface context bound to one HIP device."""
+
+    def __init__(self, device: int = 0):
+        self._lib = N.lib()
+        h = C.c_void_p()
+        rc = self._lib.ef_create(int(device), C.byref(h))
+        if rc != N.EF_OK:
+            raise N.EigenfaceError(rc, f"ef_create(device={device}) failed (no usable HIP device?)")
+        self._h = h
+        self.device = int(device)
+        self.model_k = None
+        self.model_d = None
+        self.gallery_n = 0
+        self.gallery_k = None
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.ef_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc):
+        return N.check(self._h, rc)
+
+    def set_stream(self, stream_handle):
+        """Run on an external hipStream_t (int handle, e.g. torch stream.cuda_stream)."""
+        self._chk(self._lib.ef_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+
+    def synchronize(self):
+        self._chk(self._lib.ef_synchronize(self._h))
+
+    # ------------------------------------------------------------------------ fit
+    def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
+        """GPU eigenfaces fit of uint8 faces X (n x d); see include/eigenface.h ef_fit."""
+        x, xp = _host(X, np.uint8)
+        if x.ndim != 2:
+            raise ValueError("X must be 2-D (n_samples, n_pixels)")
+        n, d = x.shape
+        k = int(n_components)
+        kk = min(k, n if n < d else d)
+        mean = np.empty(d)
+        var = np.empty(d)
+        scale = np.empty(d)
+        comps = np.empty((kk, d))
+        eig = np.empty(kk)
+        proj = np.empty((n, kk)) if projection else None
+        tv = np.empty(1)
+        k_out = C.c_int32(0)
+        it = C.c_int32(0)
+        flags = N.EF_FIT_STANDARDIZE if standardize else 0
+        self._chk(self._lib.ef_fit(
+            self._h, xp, n, d, k, flags, mean.ctypes.data, var.ctypes.data, scale.ctypes.data,
+            comps.ctypes.data, eig.ctypes.data, proj.ctypes.data if proj is not None else None,
+            tv.ctypes.data, C.byref(k_out), C.byref(it)))
+        return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
+
+    # ----------------------------------------------------------------- projection
+    def set_model(self, mean, W):
+        """Resident recognition model f = (p - mean) . W, W is d x k."""
+        if _is_dev(W):
+            import torch
+            m, mp = _dev(mean, torch.float32)
+            w, wp = _dev(W, torch.float32)
+            flags = N.EF_MEM_DEVICE
+        else:
+            m, mp = _host(mean, np.float32)
+            w, wp = _host(W, np.float32)
+            flags = 0
+        d, k = w.shape
+        if m.shape[0] != d:
+            raise ValueError("mean and W disagree on d")
+        self._chk(self._lib.ef_model_set(self._h, mp, wp, d, k, flags))
+        if flags:
+            self.synchronize()
+        self.model_d, self.model_k = int(d), int(k)
+
+    def project(self, P, out=None):
+        if self.model_k is None:
+            raise RuntimeError("no model: call set_model first")
+        if _is_dev(P):
+            import torch
+            dtype = N.EF_U8 if P.dtype == torch.uint8 else N.EF_F32
+            p, pp = _dev(P, P.dtype if P.dtype in (torch.uint8, torch.float32) else torch.float32)
+            b = p.shape[0]
+            if out is None:
+                out = torch.empty((b, self.model_k), dtype=torch.float32, device=p.device)
+            self._chk(self._lib.ef_project(self._h, pp, dtype, b, out.data_ptr(), N.EF_MEM_DEVICE))
+            return out
+        p = np.asarray(P)
+        dtype = N.EF_U8 if p.dtype == np.uint8 else N.EF_F32
+        p, pp = _host(p, np.uint8 if dtype == N.EF_U8 else np.float32)
+        if p.ndim != 2 or p.shape[1] != self.model_d:
+            raise ValueError("P must be (b, d)")
+        b = p.shape[0]
+        f = np.empty((b, self.model_k), dtype=np.float32)
+        self._chk(self._lib.ef_project(self._h, pp, dtype, b, f.ctypes.data, 0))
+        return f
+
+    # --------------------------------------------------------------------- search
+    def set_gallery(self, G, global_offset: int = 0):
+        if _is_dev(G):
+            import torch
+            g, gp = _dev(G, torch.float32)
+            flags = N.EF_MEM_DEVICE
+        else:
+            g, gp = _host(G, np.float32)
+            flags = 0
+        n, k = g.shape
+        self._chk(self._lib.ef_gallery_set(self._h, gp, n, k, int(global_offset), flags))
+        self.gallery_n, self.gallery_k = int(n), int(k)
+
+    def search_keys(self, Q, metric="l2", keys=None):
+        """Packed keys (int64) of the best gallery row per probe."""
+        mt = _metric(metric)
+        if _is_dev(Q):
+            import torch
+            q, qp = _dev(Q, torch.float32)
+            b = q.shape[0]
+            if keys is None:
+                keys = torch.empty(b, dtype=torch.int64, device=q.device)
+            self._chk(self._lib.ef_search(self._h, qp, b, mt, keys.data_ptr(), N.EF_MEM_DEVICE))
+            return keys
+        q, qp = _host(Q, np.float32)
+        b = q.shape[0]
+        k = np.empty(b, dtype=np.int64)
+        self._chk(self._lib.ef_search(self._h, qp, b, mt, k.ctypes.data, 0))
+        return k
+
+    def search(self, Q, metric="l2"):
+        """Return (idx int64, best float32): L2 -> squared distance, cosine -> similarity."""
+        keys = self.search_keys(Q, metric)
+        if _is_dev(keys):
+            keys = keys.cpu().numpy()
+        return decode_keys(keys, metric)
+
+    def recognize_keys(self, P, metric="l2", keys=None, feats=None):
+        """Fused projection + search (device or host)."""
+        mt = _metric(metric)
+        if _is_dev(P):
+            import torch
+            dtype = N.EF_U8 if P.dtype == torch.uint8 else N.EF_F32
+            p = P if P.is_contiguous() else P.contiguous()
+            b = p.shape[0]
+            if keys is None:
+                keys = torch.empty(b, dtype=torch.int64, device=p.device)
+            fp = feats.data_ptr() if feats is not None else None
+            self._chk(self._lib.ef_recognize(self._h, p.data_ptr(), dtype, b, mt, keys.data_ptr(), fp,
+                                             N.EF_MEM_DEVICE))
+            return keys
+        p = np.asarray(P)
+        dtype = N.EF_U8 if p.dtype == np.uint8 else N.EF_F32
+        p, pp = _host(p, np.uint8 if dtype == N.EF_U8 else np.float32)
+        b = p.shape[0]
+        k = np.empty(b, dtype=np.int64)
+        fp = None
+        if feats is not None:
+            fp = feats.ctypes.data
+        self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, k.ctypes.data, fp, 0))
+        return k
+
+    def recognize(self, P, metric="l2", return_features=False):
+        """Project probes P (uint8/float32 pixels) and return (idx, best[, feats])."""
+        p = np.asarray(P)
+        feats = np.empty((p.shape[0], self.model_k), dtype=np.float32) if return_features else None
+        keys = self.recognize_keys(p, metric, feats=feats)
+        idx, best = decode_keys(keys, metric)
+        return (idx, best, feats) if return_features else (idx, best)
+
+    # --------------------------------------------------------------------- timing
+    def timing(self, on=True):
+        self._chk(self._lib.ef_timing_enable(self._h, 1 if on else 0))
+
+    def timing_reset(self):
+        self._chk(self._lib.ef_timing_reset(self._h))
+
+    def timing_get(self, kernel="search"):
+        kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT}[kernel]
+        ms = C.c_double(0)
+        n = C.c_int64(0)
+        self._chk(self._lib.ef_timing_get(self._h, kid, C.byref(ms), C.byref(n)))
+        return float(ms.value), int(n.value)
+
+
+def decode_keys(keys, metric="l2"):
+    """(idx int64, best float32) from packed keys; EF_KEY_NONE -> (-1, nan)."""
+    k = np.ascontiguousarray(keys, dtype=np.int64)
+    b = k.shape[0]
+    idx = np.empty(b, dtype=np.int64)
+    best = np.empty(b, dtype=np.float32)
+    N.lib().ef_keys_decode(k.ctypes.data, b, _metric(metric), best.ctypes.data, idx.ctypes.data)
+    return idx, best
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    N.lib().ef_device_count(C.byref(n))
+    return int(n.value)

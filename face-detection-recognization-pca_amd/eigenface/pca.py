@@ -1,0 +1,190 @@
+"""Reference-surface mirror: the fit()/transform()/recognize() API and the drop-in
+functions of the reference's hot path, all executed by libeigenface on the GPU.
+
+* ``manual_pca``                 — useless/train.py:56-128
+* ``EigenfacePCA``               — FaceTrainer.train_pca_model's StandardScaler+PCA
+                                   (train-v4.py:110-146) and sklearn's
+                                   fit/transform/fit_transform surface
+* ``recognize_face_with_model``  — scan-template-v4.py:270-287
+* ``recognize_face``             — useless/scan.py:100-132
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from .engine import Engine
+
+_engines: dict[int, Engine] = {}
+_elock = threading.Lock()
+
+
+def get_engine(device: int = 0) -> Engine:
+    """Process-wide Engine for a device (created on first use)."""
+    with _elock:
+        e = _engines.get(device)
+        if e is None:
+            e = Engine(device)
+            _engines[device] = e
+        return e
+
+
+def _as_pixels(X):
+    """The GPU fit consumes uint8 pixels (train-v4.py:68,73); float inputs
+    (useless/train.py:40 flattens to float64) must be integral 0..255."""
+    x = np.asarray(X)
+    if x.dtype == np.uint8:
+        return x
+    xf = np.asarray(x, dtype=np.float64)
+    xu = np.clip(np.rint(xf), 0, 255)
+    if not np.array_equal(xu, xf):
+        raise ValueError("GPU fit expects 8-bit pixel values (integers in 0..255)")
+    return xu.astype(np.uint8)
+
+
+class EigenfacePCA:
+    """Eigenfaces estimator with sklearn-compatible attributes.
+
+    ``standardize=True`` reproduces train-v4.py's ``StandardScaler`` -> ``PCA``
+    (with the deterministic full solver); ``standardize=False`` is manual_pca.
+    After ``fit`` the recognition model (folded into ``(p - mu_f) . W``) and the
+    training features (as gallery) are resident on the GPU.
+    """
+
+    def __init__(self, n_components=50, standardize=False, device=0):
+        self.n_components = n_components
+        self.standardize = standardize
+        self.device = device
+
+    # -------------------------------------------------------------------- fit
+    def fit(self, X, y=None):
+        x = _as_pixels(X)
+        n, d = x.shape
+        eng = get_engine(self.device)
+        r = eng.fit(x, self.n_components, standardize=self.standardize)
+        k = r.k
+        self.n_samples_, self.n_features_in_ = n, d
+        self.n_components_ = k
+        self.mean_face_ = r.mean
+        self.components_ = r.components
+        self.explained_variance_ = r.eigenvalues
+        self.total_var_ = r.total_var
+        self.explained_variance_ratio_ = r.eigenvalues / r.total_var
+        self.singular_values_ = np.sqrt(np.maximum(r.eigenvalues, 0.0) * (n - 1))
+        rank = min(n, d)
+        self.noise_variance_ = float((r.total_var - r.eigenvalues.sum()) / (rank - k)) if k < rank else 0.0
+        if self.standardize:
+            self.scaler_mean_, self.scaler_var_, self.scaler_scale_ = r.mean, r.var, r.scale
+            self.mean_ = np.zeros(d)  # PCA mean of standardised data (exactly 0)
+            w = (r.components / r.scale[None, :]).T
+        else:
+            self.scaler_mean_ = self.scaler_var_ = self.scaler_scale_ = None
+            self.mean_ = r.mean
+            w = r.components.T
+        self.face_features_ = r.projection
+        self.fit_iters_ = r.iters
+        self._W = np.ascontiguousarray(w, dtype=np.float32)
+        self._mu = np.ascontiguousarray(r.mean, dtype=np.float32)
+        self._model_on = None
+        self._gallery_on = None
+        return self
+
+    def fit_transform(self, X, y=None):
+        return self.fit(X).face_features_
+
+    # --------------------------------------------------------------- transform
+    def _ensure_model(self, eng):
+        if self._model_on is not eng:
+            eng.set_model(self._mu, self._W)
+            self._model_on = eng
+
+    def transform(self, X):
+        """(p - mean) . W on the GPU (fp32 MFMA), returned as float64."""
+        eng = get_engine(self.device)
+        self._ensure_model(eng)
+        x = np.asarray(X)
+        if x.dtype != np.uint8:
+            x = np.asarray(x, dtype=np.float32)
+        return eng.project(x).astype(np.float64)
+
+    # --------------------------------------------------------------- recognize
+    def set_gallery(self, features=None):
+        eng = get_engine(self.device)
+        g = self.face_features_ if features is None else features
+        eng.set_gallery(np.asarray(g, dtype=np.float32))
+        self._gallery_on = (eng, id(g))
+        return self
+
+    def recognize(self, P, metric="cosine", threshold=None):
+        """Batched recognise: returns (idx, score); with ``threshold`` (cosine
+        only) idx is -1 where score < threshold (scan-template-v4.py:278)."""
+        eng = get_engine(self.device)
+        self._ensure_model(eng)
+        if self._gallery_on is None or self._gallery_on[0] is not eng:
+            self.set_gallery()
+        idx, best = eng.recognize(P, metric)
+        if threshold is not None:
+            idx = np.where(best >= threshold, idx, -1)
+        return idx, best
+
+
+def manual_pca(data_matrix, n_components=None, device=0):
+    """Drop-in for manual_pca (useless/train.py:56-128), computed on the GPU.
+
+    Returns ``(eigenfaces (d,k), mean_face (d,), projected_data (n,k),
+    eigenvalues (k,))`` float64.  Eigenvector signs follow sklearn's svd_flip
+    rule (the reference's LAPACK signs are arbitrary)."""
+    x = _as_pixels(data_matrix)
+    n, d = x.shape
+    if n_components is None:
+        n_components = min(n - 1, d)
+    r = get_engine(device).fit(x, n_components, standardize=False)
+    return np.ascontiguousarray(r.components.T), r.mean, r.projection, r.eigenvalues
+
+
+# ------------------------------------------------------------------ recognize
+_gallery_cache: dict = {}
+
+
+def _gallery_engine(features, device):
+    eng = get_engine(device)
+    key = (id(features), np.asarray(features).shape, device)
+    if _gallery_cache.get(device) != key:
+        eng.set_gallery(np.asarray(features, dtype=np.float32))
+        _gallery_cache[device] = key
+    return eng
+
+
+def recognize_face_with_model(face_features, model_data, threshold=0.7, device=0):
+    """Drop-in for ``recognize_face_with_model`` (scan-template-v4.py:270-287):
+    cosine vs ``model_data['face_features']`` on the GPU, first argmax,
+    ``>= threshold``, label via ``face_labels`` / ``person_id_map``."""
+    eng = _gallery_engine(model_data["face_features"], device)
+    idx, best = eng.search(np.asarray(face_features, dtype=np.float32).reshape(1, -1), "cosine")
+    i, sim = int(idx[0]), float(best[0])
+    if i >= 0 and sim >= threshold:
+        pid = model_data["face_labels"][i]
+        name = "unknown"
+        for nm, v in model_data["person_id_map"].items():
+            if v == pid:
+                name = nm
+                break
+        return pid, name, sim
+    return -1, "unknown", sim
+
+
+def recognize_face(face_vector, model_data, similarity_threshold=0.7, device=0):
+    """Drop-in for ``recognize_face`` on a ``models/*_pca_model.pkl`` dict
+    (useless/scan.py:100-132): returns ``(person_name, max_similarity,
+    is_recognized)``."""
+    eng = get_engine(device)
+    ef = np.asarray(model_data["eigenfaces"], dtype=np.float32)
+    eng.set_model(np.asarray(model_data["mean_face"], dtype=np.float32), ef)
+    _gallery_cache.pop(device, None)
+    eng.set_gallery(np.asarray(model_data["projected_data"], dtype=np.float32))
+    p = np.asarray(face_vector).reshape(1, -1)
+    p = p if p.dtype == np.uint8 else p.astype(np.float32)
+    _, best = eng.recognize(p, "cosine")
+    sim = float(best[0])
+    return model_data["person_name"], sim, sim >= similarity_threshold

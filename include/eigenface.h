@@ -1,0 +1,135 @@
+/*
+ * eigenface.h — C ABI of libeigenface.so, the MI355X (gfx950) eigenfaces engine.
+ *
+ * The reference (saladbkp/face-detection-recognization-PCA) has no FFI: its hot
+ * path is Python calling NumPy/LAPACK and scikit-learn.  Each entry point below
+ * replaces one of those call sites; the Python host layer
+ * (face-detection-recognization-pca_amd/eigenface) binds them with ctypes and
+ * keeps the reference's Python surface (INTEGRATION.md shows the bindings).
+ *
+ * Conventions
+ *   - Every function returns EF_OK (0) or a negative EF_E_* code; the message is
+ *     available from ef_last_error(ctx) until the next call on that ctx.
+ *   - Sizes are int64_t, matrices are row-major and dense (leading dimension =
+ *     row length) unless stated otherwise.
+ *   - Pointer arguments are HOST pointers unless EF_MEM_DEVICE is set in
+ *     `flags`, in which case they are device pointers on the ctx's device
+ *     (e.g. torch-ROCm data_ptr()).  Host-pointer calls are synchronous on
+ *     return; device-pointer calls are stream-ordered on the ctx's stream and
+ *     return without synchronising.
+ *   - A ctx is not thread-safe.  One process per GPU.
+ */
+#ifndef EIGENFACE_H_
+#define EIGENFACE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EF_API_VERSION 1
+
+/* status codes */
+#define EF_OK 0
+#define EF_E_INVALID (-1) /* bad argument / unsupported shape            */
+#define EF_E_HIP (-2)     /* HIP runtime error                           */
+#define EF_E_STATE (-3)   /* call out of order (no model / no gallery)   */
+#define EF_E_NOMEM (-4)   /* device allocation failed                    */
+#define EF_E_NUMERIC (-5) /* eigensolver did not converge / non-finite   */
+
+/* element types */
+#define EF_U8 0
+#define EF_F32 1
+#define EF_F64 2
+
+/* similarity metrics (ef_search) */
+#define EF_METRIC_L2 0     /* argmin ||q-g||^2, lowest index on ties (north star)           */
+#define EF_METRIC_COSINE 1 /* argmax q.g/(|q||g|), first max wins (scan-template-v4.py:274-275) */
+
+/* flags */
+#define EF_FIT_STANDARDIZE 0x1u /* StandardScaler before PCA (train-v4.py:131)                */
+#define EF_MEM_DEVICE 0x100u    /* pointer args are device pointers, call is asynchronous    */
+
+/* kernels whose device time can be queried with ef_timing_get */
+#define EF_KERNEL_SEARCH 0  /* distance GEMM + fused arg-best   */
+#define EF_KERNEL_PROJECT 1 /* (p - mean).W projection GEMM     */
+
+/* No-result sentinel in a key array (empty gallery). */
+#define EF_KEY_NONE INT64_MAX
+
+typedef struct ef_ctx ef_ctx;
+
+/* ---------------------------------------------------------------- context */
+int ef_api_version(void);
+int ef_device_count(int* out);
+int ef_create(int device, ef_ctx** out);
+void ef_destroy(ef_ctx* ctx);
+const char* ef_last_error(const ef_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the ctx's own stream. */
+int ef_set_stream(ef_ctx* ctx, void* hip_stream);
+int ef_synchronize(ef_ctx* ctx);
+
+/* -------------------------------------------------------------------- fit
+ * Replaces manual_pca (useless/train.py:56-128) and, with EF_FIT_STANDARDIZE,
+ * StandardScaler.fit_transform + PCA(svd_solver='full').fit_transform
+ * (train-v4.py:126-146).  X is n x d uint8 pixels (train-v4.py:68,73).
+ * Computes mean -> centre(+scale) -> covariance (Gram A.A^T/(n-1) when n<d,
+ * A^T.A/(n-1) otherwise) -> symmetric eigensolve -> back-project -> unit
+ * eigenfaces with the sklearn svd_flip sign rule -> training projection.
+ * k is clamped to min(n, d) as manual_pca does (useless/train.py:114).
+ * Outputs (host or device, all float64; NULL skips an optional output):
+ *   mean_out[d]        column mean of X (train-v4.py:127, useless/train.py:70)
+ *   var_out[d]         population variance (StandardScaler.var_)        optional
+ *   scale_out[d]       StandardScaler.scale_ (1 for constant pixels)     optional
+ *   components_out[k*d] eigenfaces as rows (pca.components_; manual_pca's
+ *                      eigenfaces matrix is its transpose)
+ *   eigvals_out[k]     covariance eigenvalues, descending (explained_variance_)
+ *   proj_out[n*k]      training projection (projected_data / face_features) optional
+ *   total_var_out[1]   trace of the covariance                         optional
+ *   k_out[1]           number of components actually produced          optional
+ *   iters_out[1]       eigensolver iterations (0 = direct Jacobi)       optional
+ */
+int ef_fit(ef_ctx* ctx, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint32_t flags,
+           double* mean_out, double* var_out, double* scale_out, double* components_out,
+           double* eigvals_out, double* proj_out, double* total_var_out, int32_t* k_out,
+           int32_t* iters_out);
+
+/* --------------------------------------------------------------- projection
+ * Recognition model f = (p - mean) . W  (useless/scan.py:93-96; sklearn
+ * scaler.transform + pca.transform folded, scan-template-v4.py:265-266).
+ * mean[d], W[d*k] float32, row-major (d rows of k).  Kept resident. */
+int ef_model_set(ef_ctx* ctx, const float* mean, const float* W, int64_t d, int32_t k, uint32_t flags);
+/* P[b*d] pixels (EF_U8 or EF_F32) -> F[b*k] float32. */
+int ef_project(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, float* F, uint32_t flags);
+
+/* ------------------------------------------------------------------ search
+ * Gallery rows G[n*k] float32 (face_features / projected_data), kept resident.
+ * global_offset is added to every returned index (row sharding across ranks). */
+int ef_gallery_set(ef_ctx* ctx, const float* G, int64_t n, int32_t k, int64_t global_offset,
+                   uint32_t flags);
+/* Q[b*k] float32 probe features -> keys[b].  A key packs the exact fp32 score
+ * of the winning row in its high 32 bits (order-preserving) and the global
+ * row index in its low 32 bits, so min over keys == argbest with lowest-index
+ * tie-break; an all-reduce(MIN) over ranks combines sharded galleries. */
+int ef_search(ef_ctx* ctx, const float* Q, int64_t b, int32_t metric, int64_t* keys, uint32_t flags);
+/* Fused pipeline: project P then search; feats (b*k float32) optional. */
+int ef_recognize(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, int32_t metric,
+                 int64_t* keys, float* feats, uint32_t flags);
+/* Host-side key decoding: L2 -> squared distance, COSINE -> similarity;
+ * EF_KEY_NONE -> idx -1, best NaN. */
+void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx);
+
+/* ------------------------------------------------------------------ timing
+ * Device time of each launch of a kernel, measured with hipEvents on the
+ * stream the kernel is launched on. */
+int ef_timing_enable(ef_ctx* ctx, int on);
+int ef_timing_get(ef_ctx* ctx, int32_t kernel_id, double* total_ms, int64_t* launches);
+int ef_timing_reset(ef_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EIGENFACE_H_ */

@@ -1,0 +1,96 @@
+"""GPU fit (mean, covariance, eigensolve, back-projection) against the reference
+goldens and the oracle."""
+import numpy as np
+import pytest
+
+from conftest import golden, local_golden
+from oracle import eigenface_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _align(a, ref, axis=0):
+    s = np.sign((a * ref).sum(axis=axis, keepdims=True))
+    s[s == 0] = 1
+    return a * s
+
+
+def test_manual_pca_light_golden():
+    """Real faces (faces/Light_version, 229 x 10000) through the GPU manual_pca vs the
+    reference's own manual_pca output (useless/train.py:56-128)."""
+    from eigenface import manual_pca
+    g = local_golden("light_manual_pca.npz")
+    eig, mean, proj, lam = manual_pca(g["X"], 50)
+    assert eig.shape == (10000, 50) and proj.shape == (229, 50) and lam.shape == (50,)
+    np.testing.assert_allclose(mean, g["mean_face"], rtol=1e-15)
+    np.testing.assert_allclose(lam, g["eigenvalues"], rtol=1e-9)
+    e10 = _align(eig[:, :10], g["eigenfaces_10"].astype(np.float64))
+    np.testing.assert_allclose(e10, g["eigenfaces_10"], atol=1e-6)
+    p = _align(proj, g["projected"])
+    np.testing.assert_allclose(p, g["projected"], rtol=1e-6, atol=1e-6 * np.abs(g["projected"]).max())
+    np.testing.assert_allclose(orc.manual_model_info_evr(lam), g["evr_json"], atol=1e-10)
+    # all 50 eigenfaces against the oracle, 1e-4 relative (north-star tolerance)
+    o_eig, _, _, _ = orc.manual_pca(g["X"], 50)
+    np.testing.assert_allclose(_align(eig, o_eig), o_eig, atol=1e-4 * np.abs(o_eig).max())
+
+
+def test_sklearn_path_golden():
+    """train-v4.py's StandardScaler + PCA (solver pinned 'full') vs the GPU fit."""
+    from eigenface import EigenfacePCA
+    g = golden("sklearn_path.npz")
+    m = EigenfacePCA(16, standardize=True).fit(g["X"])
+    np.testing.assert_allclose(m.scaler_mean_, g["scaler_mean"], rtol=1e-14)
+    np.testing.assert_allclose(m.scaler_var_, g["scaler_var"], rtol=1e-10)
+    np.testing.assert_allclose(m.scaler_scale_, g["scaler_scale"], rtol=1e-10)
+    np.testing.assert_allclose(m.explained_variance_, g["explained_variance"], rtol=1e-9)
+    np.testing.assert_allclose(m.explained_variance_ratio_, g["explained_variance_ratio"], rtol=1e-9)
+    np.testing.assert_allclose(m.singular_values_, g["singular_values"], rtol=1e-9)
+    np.testing.assert_allclose(m.noise_variance_, g["noise_variance"], rtol=1e-8)
+    # deterministic sign rule == sklearn svd_flip: no alignment needed
+    np.testing.assert_allclose(m.components_, g["components"], atol=1e-8)
+    np.testing.assert_allclose(m.face_features_, g["face_features"], rtol=1e-7, atol=1e-7)
+    np.testing.assert_allclose(m.mean_face_, g["mean_face"], rtol=1e-14)
+    f = m.transform(g["probes"])
+    np.testing.assert_allclose(f, g["probe_features"], rtol=1e-5, atol=1e-4)
+    idx, sim = m.recognize(g["probes"], "cosine", threshold=float(g["threshold"]))
+    pid = np.where(idx >= 0, g["labels"][np.maximum(idx, 0)], -1)
+    np.testing.assert_array_equal(pid, g["probe_person_id"])
+    np.testing.assert_allclose(sim, g["probe_similarity"], atol=1e-5)
+
+
+@pytest.mark.parametrize("n,d,k", [(60, 4096, 20), (87, 1000, 86), (500, 64, 10), (300, 48, 48)])
+def test_fit_shapes_vs_oracle(n, d, k):
+    """Direct-Jacobi (order <= 88), Gram and covariance (n >= d) branches."""
+    from eigenface import manual_pca
+    side = int(np.sqrt(d))
+    if side * side == d:
+        x, _ = orc.synth_faces(n, side, r=min(32, d), seed=n + d)
+    else:
+        x = np.random.default_rng(n).integers(0, 256, (n, d), dtype=np.uint8)
+    eig, mean, proj, lam = manual_pca(x, k)
+    o_eig, o_mean, o_proj, o_lam = orc.manual_pca(x, k)
+    kk = o_lam.shape[0]
+    assert lam.shape == (kk,)
+    np.testing.assert_allclose(mean, o_mean, rtol=1e-14)
+    keep = o_lam > 1e-9 * o_lam[0]
+    np.testing.assert_allclose(lam[keep], o_lam[keep], rtol=1e-8)
+    # compare eigenvectors with a clear gap only
+    gap = np.ones(kk, bool)
+    rel = np.abs(np.diff(o_lam)) / o_lam[0]
+    gap[:-1] &= rel > 1e-6
+    gap[1:] &= rel > 1e-6
+    gap &= keep
+    a = _align(eig, o_eig)
+    np.testing.assert_allclose(a[:, gap], o_eig[:, gap], atol=1e-6)
+
+
+def test_rank_deficient_duplicates():
+    """Duplicate faces make the Gram singular; the fit must stay finite and
+    reproduce the non-zero spectrum."""
+    from eigenface import manual_pca
+    x, _ = orc.synth_faces(40, 32, r=8, seed=2)
+    x = np.concatenate([x, x, x])  # 120 x 1024, rank <= 40
+    eig, mean, proj, lam = manual_pca(x, 20)
+    o_eig, _, _, o_lam = orc.manual_pca(x, 20)
+    assert np.all(np.isfinite(eig)) and np.all(np.isfinite(proj))
+    np.testing.assert_allclose(lam, o_lam, rtol=1e-8)

@@ -1,0 +1,98 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every entry point that
+include/eigenface.h declares, and its host-only helpers behave (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "eigenface.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ef_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    names = _declared()
+    for n in ("ef_create", "ef_destroy", "ef_fit", "ef_model_set", "ef_project", "ef_gallery_set",
+              "ef_search", "ef_recognize", "ef_keys_decode", "ef_timing_get"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from eigenface import _native
+    lib = _native.lib()
+    for n in _declared():
+        assert hasattr(lib, n), n
+    assert set(_native.EXPORTED_SYMBOLS) == set(_declared())
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    for n in _declared():
+        assert re.search(rf"\bT {n}$", out, re.M), n
+
+
+def test_library_is_gfx950_code_object():
+    from eigenface import _native
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle target id
+
+
+def test_api_version_and_no_device_here():
+    from eigenface import _native
+    lib = _native.lib()
+    assert lib.ef_api_version() == 1
+    n = ctypes.c_int(-1)
+    assert lib.ef_device_count(ctypes.byref(n)) == 0
+    if n.value == 0:  # build container: creating a context must fail cleanly, not crash
+        h = ctypes.c_void_p()
+        assert lib.ef_create(0, ctypes.byref(h)) != 0
+        from eigenface import Engine, EigenfaceError
+        with pytest.raises(EigenfaceError):
+            Engine(0)
+
+
+def test_key_decode_roundtrip_order_and_ties():
+    """Packed keys: high 32 bits order-preserving score, low 32 bits index."""
+    from eigenface import decode_keys
+
+    def pack(v, i):
+        b = np.float32(v).view(np.int32).item()
+        if v == 0:
+            b = 0
+        s = b if b >= 0 else b ^ 0x7FFFFFFF
+        return (s << 32) | i
+
+    vals = [-3.5, -1e-30, 0.0, 1e-30, 2.0, 7.25, np.inf]
+    keys = np.array([pack(v, 10 + j) for j, v in enumerate(vals)], dtype=np.int64)
+    assert np.all(np.diff(keys) > 0)  # signed int64 order == score order
+    idx, best = decode_keys(keys, "l2")
+    np.testing.assert_array_equal(idx, 10 + np.arange(len(vals)))
+    np.testing.assert_array_equal(best, np.array(vals, np.float32))
+    # equal scores: lower index is the smaller key (np.argmin tie-break)
+    assert pack(1.5, 3) < pack(1.5, 4)
+    # cosine keys hold -similarity
+    idx, sim = decode_keys(np.array([pack(-0.75, 2)], np.int64), "cosine")
+    assert idx[0] == 2 and sim[0] == np.float32(0.75)
+    idx, best = decode_keys(np.array([(1 << 63) - 1], np.int64), "l2")
+    assert idx[0] == -1 and np.isnan(best[0])
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    from eigenface import _native
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(_native.NativeLibraryError):
+        _native.lib()
+
+
+def test_product_package_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "face-detection-recognization-pca_amd", "eigenface")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            assert "oracle" not in open(os.path.join(pkg, f)).read().replace("no oracle", ""), f
