@@ -67,6 +67,38 @@ def cpu_baseline(P, mean, W, G, targets, budget_s):
     }
 
 
+def fit_bench(eng, with_cpu: bool):
+    """Secondary metric "covariance+SVD fit sec": GPU ef_fit (mean, centre, Gram,
+    eigensolve, back-project, training projection; fp64) on configs[1]'s shape
+    (synthetic 10k faces 128x128, k=64) and on a 2000-face subset that the CPU oracle
+    (NumPy/LAPACK manual_pca restatement) also runs."""
+    from eigenface import synth
+    side, k, n_full, n_sub = 128, 64, 10_000, 2000
+    d = side * side
+    rng = np.random.default_rng(77)
+    B = synth.basis(d, 128, 5)
+    coef = rng.standard_normal((n_full, 128)) * synth.spectrum(128)
+    X = np.clip(np.rint(synth.mean_face(side) + coef @ B.T + 2.0 * rng.standard_normal((n_full, d))),
+                0, 255).astype(np.uint8)
+    out = {"config": f"synthetic faces {side}x{side}, k={k}, manual_pca semantics (Gram path, fp64)"}
+    for n in (n_sub, n_full):
+        eng.fit(X[:256], 16)  # warm the code paths
+        t = time.perf_counter()
+        r = eng.fit(X[:n], k)
+        out[f"gpu_s_n{n}"] = round(time.perf_counter() - t, 4)
+        out[f"gpu_iters_n{n}"] = r.iters
+    if with_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import eigenface_oracle as orc
+        t = time.perf_counter()
+        _, _, _, lam = orc.manual_pca(X[:n_sub], k)
+        out[f"cpu_s_n{n_sub}"] = round(time.perf_counter() - t, 4)
+        r = eng.fit(X[:n_sub], k)
+        out["eig_max_rel_err_vs_cpu"] = float(np.max(np.abs(r.eigenvalues - lam) / lam))
+    out["note"] = "host X (includes the H2D copy of the uint8 faces); CPU = oracle manual_pca, all host cores"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +108,7 @@ def main():
     ap.add_argument("--metric", default="l2", choices=["l2", "cosine"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-fit", action="store_true", help="skip the secondary fit timing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,11 +125,11 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from eigenface import Engine, decode_keys, synth
+    from eigenface.distributed import ShardedGallery, shard_range
 
     n_total, side, k, bsz = CONFIGS[args.config]
     d = side * side
-    lo = n_total * rank // world
-    hi = n_total * (rank + 1) // world
+    lo, hi = shard_range(n_total, rank, world)
 
     t_setup = time.perf_counter()
     B = synth.basis(d, k, 0)
@@ -110,16 +143,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     eng.set_model(mean, W)
-    eng.set_gallery(G, global_offset=lo)
+    shard = ShardedGallery(eng, G, n_total, rank, world)
     P_dev = torch.from_numpy(P).to(dev)
     keys = torch.empty(bsz, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s gallery rows [{lo},{hi})")
 
-    def step():
-        eng.recognize_keys(P_dev, args.metric, keys=keys)
-        if world > 1:
-            dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+    def step():  # project + local search + (N>1) all-reduce(MIN) of the packed keys
+        shard.recognize_keys(P_dev, args.metric, keys=keys)
 
     for _ in range(args.warmup):
         step()
@@ -190,6 +221,8 @@ def main():
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
             "check": {"planted_match": match},
         }
+        if world == 1 and not args.no_fit:
+            rec["fit"] = fit_bench(eng, not args.no_cpu)
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
         else:

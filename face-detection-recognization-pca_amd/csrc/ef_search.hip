@@ -409,7 +409,7 @@ __global__ void pad_rows_kernel(const float* __restrict__ src, int64_t rows, int
 // ||g||^2 and 1/||g|| per gallery row (K7: computed once at enrolment, not per probe as
 // sklearn's cosine_similarity does, pairwise.py:1734), and max ||g||^2 for the bound.
 __global__ void gallery_aux_kernel(const float* __restrict__ G, int64_t n, int kp, float* __restrict__ gnorm2,
-                                   float* __restrict__ ginv, unsigned* __restrict__ gmax2_bits) {
+                                   float* __restrict__ ginv) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
@@ -423,7 +423,21 @@ __global__ void gallery_aux_kernel(const float* __restrict__ G, int64_t n, int k
   if (lane == 0) {
     gnorm2[row] = s;
     ginv[row] = s > 0.f ? 1.0f / sqrtf(s) : 0.f;
-    atomicMax(gmax2_bits, __float_as_uint(s));  // non-negative floats order as uints
+  }
+}
+
+// max ||g||^2 (one atomic per block; non-negative floats order as their bit patterns)
+__global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, x[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(m));
   }
 }
 
@@ -512,8 +526,8 @@ hipError_t launch_gallery_aux(hipStream_t s, const float* G, int64_t n, int kp, 
                               unsigned* gmax2_bits) {
   hipError_t e = hipMemsetAsync(gmax2_bits, 0, sizeof(unsigned), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(gallery_aux_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, G, n, kp, gnorm2, ginv,
-                     gmax2_bits);
+  hipLaunchKernelGGL(gallery_aux_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, G, n, kp, gnorm2, ginv);
+  hipLaunchKernelGGL(max_kernel, dim3(256), dim3(256), 0, s, gnorm2, n, gmax2_bits);
   return hipGetLastError();
 }
 
