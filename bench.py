@@ -67,6 +67,17 @@ def cpu_baseline(P, mean, W, G, targets, budget_s):
     }
 
 
+def pmc_traffic(config):
+    """HBM bytes per search launch from the newest committed rocprofv3 PMC summary of
+    this config (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+        rec = json.load(open(f))
+        if rec.get("config") == config:
+            return rec["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def fit_bench(eng, with_cpu: bool):
     """Secondary metric "covariance+SVD fit sec": GPU ef_fit (mean, centre, Gram,
     eigensolve, back-project, training projection; fp64) on configs[1]'s shape
@@ -180,12 +191,23 @@ def main():
     idx, best = decode_keys(keys.cpu().numpy(), args.metric)
     match = float((idx == targets).mean())
 
+    host_rate = None
+    if world == 1:  # PCIe-inclusive rate of the host-buffer boundary (never `value`)
+        eng.set_stream(0)
+        eng.recognize_keys(P, args.metric)
+        t = time.perf_counter()
+        for _ in range(3):
+            hk = eng.recognize_keys(P, args.metric)
+        host_rate = 3 * bsz / (time.perf_counter() - t)
+        assert np.array_equal(hk, keys.cpu().numpy())
+
     if rank == 0:
         ms_step = el / args.steps * 1e3
         value = bsz * args.steps / el
         search_avg_ms = s_ms / max(s_n, 1)
         flops_launch = 2.0 * bsz * (hi - lo) * k  # algorithmic: 2 k N per face x B faces
         achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
         rec = {
             "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128",
             "value": round(value, 1),
@@ -213,12 +235,14 @@ def main():
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": round(search_avg_ms, 4),
                 "launches": s_n,
                 "flops_per_launch": flops_launch,
             },
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
+            "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
             "check": {"planted_match": match},
         }
         if world == 1 and not args.no_fit:

@@ -101,12 +101,14 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
     EF_HIP(c, hipStreamSynchronize(s), "sync");
     for (auto& t : th) t = std::sqrt(t > 0 ? t : 0.0);
-    double worst = 0.0;
-    for (int i = 0; i < kk; ++i) worst = std::fmax(worst, std::fabs(th[i] - prev[i]));
+    // converged when every kept Ritz value is stable to 1e-13 relative (floor 1e-15 of
+    // the largest, for zero eigenvalues of rank-deficient data) twice in a row
+    bool ok = true;
+    for (int i = 0; i < kk; ++i) ok &= std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * th[i], 1e-15 * th[0]);
     prev = th;
     if (!(std::isfinite(th[0]))) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
-    if (it > 2 && worst <= 1e-15 * th[0]) {
-      if (++stable >= 3) break;
+    if (it > 2 && ok) {
+      if (++stable >= 2) break;
     } else {
       stable = 0;
     }

@@ -208,6 +208,7 @@ __global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__
   int* pp = reinterpret_cast<int*>(sn + np);
   int* qq = pp + np;
   int* flag = qq + np;
+  int* rcnt = flag + 1;
   const int tid = threadIdx.x, nth = blockDim.x;
 
   for (int e = tid; e < mp * mp; e += nth) {
@@ -221,10 +222,13 @@ __global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__
 
   int sweep = 0;
   bool converged = false;
+  if (tid < 2) rcnt[tid] = 0;
+  __syncthreads();
   for (; sweep < max_sweeps; ++sweep) {
     if (tid == 0) *flag = 0;
     __syncthreads();
     for (int r = 0; r < mp - 1; ++r) {
+      int* cnt = &rcnt[r & 1];
       if (tid < np) {
         auto pos = [&](int j) { return j == 0 ? 0 : 1 + ((j - 1 + r) % (mp - 1)); };
         int p = pos(tid), q = pos(mp - 1 - tid);
@@ -244,10 +248,13 @@ __global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__
           sn[tid] = t * c;
           pp[tid] = p;
           qq[tid] = q;
-          *flag = 1;
+          atomicAdd(cnt, 1);
         }
       }
       __syncthreads();
+      if (tid == 0) rcnt[(r + 1) & 1] = 0;  // next round's counter (read >= 1 barrier ago)
+      if (*cnt == 0) continue;              // uniform: nothing to rotate this round
+      if (tid == 0) *flag = 1;
       for (int e = tid; e < np * mp; e += nth) {  // rows p, q  <- J^T T
         const int i = e / mp, j = e - (e / mp) * mp;
         const int p = pp[i];
@@ -277,6 +284,7 @@ __global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__
       }
       __syncthreads();
     }
+    __syncthreads();
     const int f = *flag;
     __syncthreads();
     if (f == 0) { converged = true; break; }
@@ -304,7 +312,7 @@ __global__ __launch_bounds__(1024) void jacobi_kernel(const double* __restrict__
 size_t jacobi_lds_bytes(int m) {
   const int mp = m + (m & 1);
   return (size_t)2 * mp * (mp + 1) * sizeof(double) + (size_t)mp * sizeof(double) +
-         (size_t)(mp + 2) * sizeof(int) + 16;
+         (size_t)(mp + 4) * sizeof(int) + 16;
 }
 
 hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,

@@ -17,6 +17,7 @@ step() {  # name, timeout, command...
 step pytest 600 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step bench 600 python bench.py || exit $?
+[ "$2" = quick ] && { echo done >> $O/steps.log; exit 0; }
 B="bench.py --steps 5 --warmup 2 --no-cpu --no-fit"
 step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B || exit $?
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $B || exit $?

@@ -1,0 +1,68 @@
+"""Summarise rocprofv3 --pmc passes of the search kernel into profiles/<round>/pmc_summary.json.
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
+(KiB) from separate passes; on gfx950 FETCH_SIZE reports half the bytes of a wide
+(16 B/lane) coalesced stream, so it is doubled; WRITE_SIZE is exact for 16-B stores
+(the search kernel's partial-key stores are 8/4-B, uncalibrated: reported as is).
+MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x per-XCD GRBM_GUI_ACTIVE), the
+clock = per-XCD GRBM_GUI_ACTIVE / kernel time.
+
+usage: python tools/pmc_summary.py <fetch.csv> <write.csv> <sq.csv> <kernel_trace_stats.csv> <out.json> [config]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+KERNEL = "search_kernel<128, 0, false>"
+SIMDS = 1024  # 256 CUs x 4
+XCDS = 8
+
+
+def per_launch(path, kernel=KERNEL):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"]:
+            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def avg_ns(stats_path, kernel=KERNEL):
+    for r in csv.DictReader(open(stats_path)):
+        if kernel in r["Name"]:
+            return float(r["AverageNs"]), int(r["Calls"])
+    raise SystemExit("kernel not found in stats")
+
+
+def main():
+    fetch, write, sq, stats, out = sys.argv[1:6]
+    config = sys.argv[6] if len(sys.argv) > 6 else "c3"
+    f, nf = per_launch(fetch)
+    w, _ = per_launch(write)
+    s, _ = per_launch(sq)
+    ns, calls = avg_ns(stats)
+    fetch_b = f["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE counts half of wide reads
+    write_b = w["WRITE_SIZE"] * 1024
+    grbm_xcd = s["GRBM_GUI_ACTIVE"] / XCDS
+    rec = {
+        "config": config,
+        "kernel": KERNEL,
+        "launches_profiled": nf.get("FETCH_SIZE", 0),
+        "fetch_size_kib_raw": f["FETCH_SIZE"],
+        "write_size_kib_raw": w["WRITE_SIZE"],
+        "hbm_read_bytes": fetch_b,
+        "hbm_write_bytes": write_b,
+        "traffic_bytes": fetch_b + write_b,
+        "algorithmic_bytes": 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4,
+        "trace_avg_ns": ns,
+        "trace_calls": calls,
+        "mfma_busy_frac": s["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * grbm_xcd),
+        "clock_ghz": grbm_xcd / ns,
+        "sq_wait_any_frac": s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"],
+    }
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
