@@ -1,0 +1,368 @@
+"""On-disk formats and the trainer/scanner surface of the reference (SURVEY.md
+Appendix A, §8a rows a1/a10/a11), backed by the GPU engine.
+
+* ``FaceTrainer``            — train-v4.py:11-266 (load, label, train, save/load model,
+                               eigenface JPGs + ``{person}_model_info.json``)
+* ``save_pca_model``         — useless/train.py:130-192 (``models/*_pca_model.pkl`` +
+                               ``*_model_info.json``)
+* ``visualize_eigenfaces``   — useless/train.py:194-223
+* ``sklearn_objects``        — real ``StandardScaler`` / ``PCA`` instances populated from the
+                               GPU fit, so pickles load and ``.transform`` anywhere sklearn
+                               is installed (scan-template-v4.py:36-37, :265-266)
+* ``extract_face_features``, ``recognize_face_all_models`` — scan-template-v4.py:253-319
+
+Image decoding (a1) uses OpenCV when importable (the reference's exact path:
+``imread`` -> ``cvtColor(BGR2GRAY)`` -> ``resize(64, 64)``); otherwise Pillow with
+OpenCV's fixed-point BT.601 grey conversion and a bilinear resize restatement — that
+branch is *parity unpinned* (OpenCV is absent where this was built).
+"""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+from datetime import datetime
+
+import numpy as np
+
+from .pca import EigenfacePCA, get_engine
+
+
+# ----------------------------------------------------------------------- images
+def _gray_resize_fallback(path, size):
+    from PIL import Image
+
+    im = Image.open(path)
+    if im.mode == "L":
+        g = np.asarray(im, dtype=np.uint8)
+    else:
+        rgb = np.asarray(im.convert("RGB"), dtype=np.int32)
+        # OpenCV CV_8U RGB->GRAY: (R*4899 + G*9617 + B*1868 + 8192) >> 14
+        g = ((rgb[..., 0] * 4899 + rgb[..., 1] * 9617 + rgb[..., 2] * 1868 + 8192) >> 14).astype(np.uint8)
+    return _resize_bilinear(g, size)
+
+
+def _resize_bilinear(img, size):
+    """cv2.resize(..., INTER_LINEAR) restatement for uint8 (half-pixel centres,
+    edge clamp, 11-bit weights, rounded).  Parity unpinned."""
+    w_out, h_out = size
+    h_in, w_in = img.shape
+    if (h_in, w_in) == (h_out, w_out):
+        return img.copy()
+
+    def axis(n_in, n_out):
+        f = (np.arange(n_out) + 0.5) * (n_in / n_out) - 0.5
+        i0 = np.floor(f).astype(np.int64)
+        a = f - i0
+        a = np.where(i0 < 0, 0.0, a)
+        i0 = np.clip(i0, 0, n_in - 1)
+        i1 = np.clip(i0 + 1, 0, n_in - 1)
+        w1 = np.rint(a * 2048).astype(np.int64)
+        return i0, i1, 2048 - w1, w1
+
+    y0, y1, wy0, wy1 = axis(h_in, h_out)
+    x0, x1, wx0, wx1 = axis(w_in, w_out)
+    src = img.astype(np.int64)
+    rows = src[:, x0] * wx0 + src[:, x1] * wx1              # (h_in, w_out), scale 2^11
+    val = rows[y0] * wy0[:, None] + rows[y1] * wy1[:, None]  # scale 2^22
+    return np.clip((val + (1 << 21)) >> 22, 0, 255).astype(np.uint8)
+
+
+def read_face(path, size=(64, 64)):
+    """Grey, resized, uint8 face (train-v4.py:59-66); None if unreadable."""
+    try:
+        import cv2  # noqa: F401
+    except ImportError:
+        cv2 = None
+    if cv2 is not None:
+        img = cv2.imread(path)
+        if img is None:
+            return None
+        return cv2.resize(cv2.cvtColor(img, cv2.COLOR_BGR2GRAY), size)
+    try:
+        return _gray_resize_fallback(path, size)
+    except (OSError, ValueError):
+        return None
+
+
+def _save_jpg(path, arr2d):
+    """cv2.normalize(NORM_MINMAX, 0..255, CV_8U) + imwrite (train-v4.py:164-177)."""
+    a = np.asarray(arr2d, dtype=np.float64)
+    lo, hi = a.min(), a.max()
+    u8 = np.zeros(a.shape, np.uint8) if hi == lo else np.rint((a - lo) * (255.0 / (hi - lo))).astype(np.uint8)
+    try:
+        import cv2
+        cv2.imwrite(path, u8)
+    except ImportError:
+        from PIL import Image
+        Image.fromarray(u8, mode="L").save(path, quality=95)
+
+
+# ------------------------------------------------------------ sklearn objects
+def sklearn_objects(model: EigenfacePCA):
+    """Fitted ``StandardScaler`` and ``PCA`` carrying the GPU fit's attributes."""
+    from sklearn.decomposition import PCA
+    from sklearn.preprocessing import StandardScaler
+
+    d = model.n_features_in_
+    scaler = StandardScaler()
+    if model.standardize:
+        scaler.mean_, scaler.var_, scaler.scale_ = model.scaler_mean_.copy(), model.scaler_var_.copy(), \
+            model.scaler_scale_.copy()
+    else:  # identity scaling: the PCA is on raw pixels (manual_pca semantics)
+        scaler.mean_, scaler.var_, scaler.scale_ = np.zeros(d), np.ones(d), np.ones(d)
+    scaler.n_samples_seen_ = model.n_samples_
+    scaler.n_features_in_ = d
+    pca = PCA(n_components=model.n_components, svd_solver="full")
+    pca.mean_ = model.mean_.copy()
+    pca.components_ = model.components_.copy()
+    pca.explained_variance_ = model.explained_variance_.copy()
+    pca.explained_variance_ratio_ = model.explained_variance_ratio_.copy()
+    pca.singular_values_ = model.singular_values_.copy()
+    pca.noise_variance_ = model.noise_variance_
+    pca.n_components_ = model.n_components_
+    pca.n_samples_ = model.n_samples_
+    pca.n_features_in_ = d
+    pca._fit_svd_solver = "full"
+    return scaler, pca
+
+
+# ------------------------------------------------------------------ trainer
+class FaceTrainer:
+    """train-v4.py's FaceTrainer (:11-266) with the fit on the GPU."""
+
+    def __init__(self, n_components=50, device=0):
+        self.n_components = n_components
+        self.device = device
+        self.pca = None
+        self.scaler = None
+        self.face_features = []
+        self.face_labels = []
+        self.face_info = []
+        self.face_images = np.zeros((0, 0), np.uint8)
+        self.person_id_map = {}
+        self.is_trained = False
+        self.mean_face = None
+        self.eigenfaces = None
+        self.face_shape = (64, 64)
+        self.model = None
+
+    def load_face_images(self, json_path, face_dir):
+        """JSON order (train-v4.py:44-76).  ``image_path`` as the reference, falling back to
+        ``image_filename`` inside face_dir (train-v5.py:305-306) for Windows-style paths."""
+        with open(json_path, "r", encoding="utf-8") as f:
+            data = json.load(f)
+        images, valid = [], []
+        for info in data["faces"]:
+            path = info.get("image_path", "")
+            if not os.path.exists(path):
+                alt = os.path.join(face_dir, info.get("image_filename", os.path.basename(path.replace("\\", "/"))))
+                if not os.path.exists(alt):
+                    print(f"Warning: Image {path} not found, skipping...")
+                    continue
+                path = alt
+            g = read_face(path, self.face_shape)
+            if g is None:
+                print(f"Warning: Could not read image {path}, skipping...")
+                continue
+            images.append(g.flatten())
+            valid.append(info)
+        self.face_images = np.array(images, dtype=np.uint8).reshape(len(images), -1)
+        self.face_info = valid
+        return len(images)
+
+    def assign_labels_interactive(self, person_name):
+        """All faces labelled as one person, id 0 (train-v4.py:78-108)."""
+        for info in self.face_info:
+            info["person_name"] = person_name
+            info["person_id"] = 0
+        self.face_labels = np.zeros(len(self.face_info), dtype=np.int64)
+        self.person_id_map = {person_name: 0}
+        return list(self.face_labels)
+
+    def train_pca_model(self):
+        """StandardScaler -> PCA on the GPU (train-v4.py:110-146); False on empty input."""
+        if len(self.face_images) == 0:
+            print("Error: No face images loaded!")
+            return False
+        if len(self.face_labels) == 0:
+            print("Error: No face labels assigned!")
+            return False
+        m = EigenfacePCA(self.n_components, standardize=True, device=self.device).fit(self.face_images)
+        self.model = m
+        self.mean_face = m.mean_face_
+        self.scaler, self.pca = sklearn_objects(m)
+        self.eigenfaces = self.pca.components_
+        self.face_features = m.face_features_
+        print(f"PCA explained variance ratio: {self.pca.explained_variance_ratio_.sum():.3f}")
+        self.is_trained = True
+        return True
+
+    def save_eigenfaces(self, output_dir, person_name):
+        """Mean face + top-10 eigenfaces as min-max JPGs and ``{person}_model_info.json``
+        (train-v4.py:148-197)."""
+        if not self.is_trained:
+            print("Error: Model not trained yet!")
+            return False
+        os.makedirs(output_dir, exist_ok=True)
+        _save_jpg(os.path.join(output_dir, f"{person_name}_mean_face.jpg"), self.mean_face.reshape(self.face_shape))
+        n_save = min(10, len(self.eigenfaces))
+        for i in range(n_save):
+            _save_jpg(os.path.join(output_dir, f"{person_name}_eigenface_{i + 1:02d}.jpg"),
+                      self.eigenfaces[i].reshape(self.face_shape))
+        info = {
+            "person_name": person_name,
+            "training_date": datetime.now().isoformat(),
+            "total_faces": len(self.face_images),
+            "n_components": self.n_components,
+            "explained_variance_ratio": float(self.pca.explained_variance_ratio_.sum()),
+            "face_shape": self.face_shape,
+            "eigenfaces_saved": n_save,
+        }
+        with open(os.path.join(output_dir, f"{person_name}_model_info.json"), "w", encoding="utf-8") as f:
+            json.dump(info, f, indent=2, ensure_ascii=False)
+        return True
+
+    def model_dict(self):
+        """The ``face_model.pkl`` dict (train-v4.py:210-222)."""
+        return {
+            "pca": self.pca,
+            "scaler": self.scaler,
+            "face_features": self.face_features,
+            "face_labels": self.face_labels,
+            "face_info": self.face_info,
+            "person_id_map": self.person_id_map,
+            "n_components": self.n_components,
+            "mean_face": self.mean_face,
+            "eigenfaces": self.eigenfaces,
+            "face_shape": self.face_shape,
+            "training_date": datetime.now().isoformat(),
+        }
+
+    def save_model(self, model_path):
+        if not self.is_trained:
+            print("Error: Model not trained yet!")
+            return False
+        with open(model_path, "wb") as f:
+            pickle.dump(self.model_dict(), f)
+        return True
+
+    def load_model(self, model_path):
+        """Load a model this package (or the reference) wrote — trusted files only: a
+        pickle executes code on load."""
+        if not os.path.exists(model_path):
+            print(f"Error: Model file {model_path} not found!")
+            return False
+        with open(model_path, "rb") as f:
+            md = pickle.load(f)
+        self.pca = md["pca"]
+        self.scaler = md["scaler"]
+        self.face_features = md["face_features"]
+        self.face_labels = md["face_labels"]
+        self.face_info = md["face_info"]
+        self.person_id_map = md["person_id_map"]
+        self.n_components = md["n_components"]
+        self.mean_face = md.get("mean_face")
+        self.eigenfaces = md.get("eigenfaces")
+        self.face_shape = md.get("face_shape", (64, 64))
+        self.is_trained = True
+        return True
+
+
+# ----------------------------------------------------------- manual formats
+def save_pca_model(eigenfaces, mean_face, projected_data, eigenvalues, filenames, person_name, model_dir,
+                   version=None):
+    """``models/{person}[_{version}]_pca_model.pkl`` + ``_model_info.json``
+    (useless/train.py:130-192).  The JSON ratio divides by the sum of the *kept*
+    eigenvalues and keeps the first 10 (:182)."""
+    os.makedirs(model_dir, exist_ok=True)
+    stamp = datetime.now().isoformat()
+    md = {
+        "eigenfaces": eigenfaces,
+        "mean_face": mean_face,
+        "projected_data": projected_data,
+        "eigenvalues": eigenvalues,
+        "training_filenames": list(filenames),
+        "person_name": person_name,
+        "version": version,
+        "training_timestamp": stamp,
+        "n_components": int(eigenfaces.shape[1]),
+        "face_dimensions": int(eigenfaces.shape[0]),
+    }
+    stem = f"{person_name}_{version}" if version else person_name
+    model_file = f"{stem}_pca_model.pkl"
+    path = os.path.join(model_dir, model_file)
+    with open(path, "wb") as f:
+        pickle.dump(md, f)
+    lam = np.asarray(eigenvalues, dtype=np.float64)
+    meta = {
+        "person_name": person_name,
+        "version": version,
+        "training_timestamp": stamp,
+        "n_components": md["n_components"],
+        "face_dimensions": md["face_dimensions"],
+        "n_training_images": len(filenames),
+        "explained_variance_ratio": (lam / lam.sum()).tolist()[:10],
+        "model_file": model_file,
+    }
+    with open(os.path.join(model_dir, f"{stem}_model_info.json"), "w", encoding="utf-8") as f:
+        json.dump(meta, f, indent=2, ensure_ascii=False)
+    return path
+
+
+def visualize_eigenfaces(eigenfaces, mean_face, output_dir, person_name, n_display=10):
+    """Mean face + top eigenfaces as min-max JPGs (useless/train.py:194-223)."""
+    side = int(np.sqrt(len(mean_face)))
+    _save_jpg(os.path.join(output_dir, f"{person_name}_mean_face.jpg"), np.asarray(mean_face).reshape(side, side))
+    for i in range(min(n_display, eigenfaces.shape[1])):
+        _save_jpg(os.path.join(output_dir, f"{person_name}_eigenface_{i + 1:02d}.jpg"),
+                  eigenfaces[:, i].reshape(side, side))
+
+
+# ------------------------------------------------------------------ scanner
+def _model_projection(md):
+    """Fold a face_model.pkl's scaler + pca into (mean, W) for the GPU projection."""
+    pca = md.get("pca", md.get("pca_model"))
+    sc = md["scaler"]
+    comp = np.asarray(pca.components_, dtype=np.float64)
+    scale = np.asarray(sc.scale_, dtype=np.float64)
+    w = (comp / scale[None, :]).T
+    mu = np.asarray(sc.mean_, dtype=np.float64) + scale * np.asarray(pca.mean_, dtype=np.float64)
+    return mu.astype(np.float32), np.ascontiguousarray(w, dtype=np.float32)
+
+
+def extract_face_features(face_img, model_data, device=0):
+    """scan-template-v4.py:253-268 on the GPU: grey 64x64 face -> model features."""
+    g = np.asarray(face_img)
+    if g.ndim == 3:
+        g = ((g[..., 2].astype(np.int32) * 4899 + g[..., 1].astype(np.int32) * 9617 +
+              g[..., 0].astype(np.int32) * 1868 + 8192) >> 14).astype(np.uint8)
+    if g.shape != (64, 64):
+        g = _resize_bilinear(g.astype(np.uint8), (64, 64))
+    eng = get_engine(device)
+    mu, w = _model_projection(model_data)
+    eng.set_model(mu, w)
+    return eng.project(g.reshape(1, -1).astype(np.uint8))[0].astype(np.float64)
+
+
+def recognize_face_all_models(face_img, models, threshold=0.8, device=0):
+    """Best match over per-person models (scan-template-v4.py:289-319): strict '>' over
+    models in iteration order, recognised name or the model's person name."""
+    from .pca import recognize_face_with_model
+
+    best = None
+    best_conf = 0.0
+    for person_name, info in models.items():
+        md = info["model_data"] if "model_data" in info else info
+        if md is None:
+            continue
+        try:
+            f = extract_face_features(face_img, md, device)
+            pid, name, conf = recognize_face_with_model(f, md, threshold, device)
+        except Exception as e:  # reference: print and continue (:312-314)
+            print(f"Error recognizing with model {person_name}: {e}")
+            continue
+        if conf > best_conf:
+            best_conf = conf
+            best = (pid, name if name != "unknown" else person_name, conf)
+    return best if best else (-1, "unknown", 0.0)

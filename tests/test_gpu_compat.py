@@ -1,0 +1,82 @@
+"""Drop-in trainer / scanner surface end to end on the GPU (synthetic faces on disk)."""
+import json
+import os
+import pickle
+
+import numpy as np
+import pytest
+
+from oracle import eigenface_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _person_dir(root, person, n, seed):
+    from PIL import Image
+    d = os.path.join(root, "faces", "lock_version", person)
+    os.makedirs(d)
+    x, _ = orc.synth_faces(n, 64, r=32, seed=seed)
+    faces = []
+    for i, row in enumerate(x):
+        fn = f"face_{i:04d}.png"
+        Image.fromarray(row.reshape(64, 64), mode="L").save(os.path.join(d, fn))
+        # Windows-style path as in the committed JSONs: resolved via image_filename
+        faces.append({"face_id": i, "image_path": f"faces\\lock_version\\{person}\\{fn}", "image_filename": fn,
+                      "width": 64, "height": 64})
+    json.dump({"faces": faces}, open(os.path.join(d, f"{person}_faces_detection.json"), "w"))
+    return x
+
+
+def test_train_v4_cli_and_pickle(tmp_path):
+    from eigenface.cli import train_v4
+    from eigenface.compat import FaceTrainer, recognize_face_all_models
+    from eigenface import recognize_face_with_model
+    xa = _person_dir(str(tmp_path), "alice", 120, 1)
+    xb = _person_dir(str(tmp_path), "bob", 90, 2)
+    assert train_v4("alice", str(tmp_path)) == 0
+    assert train_v4("bob", str(tmp_path)) == 0
+    base = tmp_path / "faces" / "lock_version"
+    for p in ("alice", "bob"):
+        assert (base / p / "face_model.pkl").exists()
+        assert (base / p / f"{p}_model_info.json").exists()
+        assert (base / p / f"{p}_eigenface_01.jpg").exists() and (base / p / f"{p}_mean_face.jpg").exists()
+    md = pickle.load(open(base / "alice" / "face_model.pkl", "rb"))  # written by this package
+    assert set(md) >= {"pca", "scaler", "face_features", "face_labels", "face_info", "person_id_map",
+                       "n_components", "mean_face", "eigenfaces", "face_shape", "training_date"}
+    # the pickled sklearn objects reproduce the oracle's sklearn path (train-v4.py:131-134)
+    ref = orc.train_pca_model(xa, 50)
+    f_ref = orc.sklearn_transform(xa[:10], ref["scaler"], ref["pca"])
+    f_pk = md["pca"].transform(md["scaler"].transform(xa[:10].astype(np.float64)))
+    scale = np.abs(f_ref).max()
+    # components agree up to sign only where the spectrum has gaps: compare projections' norms
+    np.testing.assert_allclose(np.linalg.norm(f_pk, axis=1), np.linalg.norm(f_ref, axis=1), rtol=1e-6)
+    np.testing.assert_allclose(md["pca"].explained_variance_, ref["pca"]["explained_variance_"], rtol=1e-8)
+    np.testing.assert_allclose(md["face_features"][:, :10], ref["face_features"][:, :10], atol=1e-6 * scale)
+    # reference-style recognition on the loaded dict (scan-template-v4.py:270-287)
+    pid, name, sim = recognize_face_with_model(f_pk[3], md, 0.8)
+    assert (pid, name) == (0, "alice") and sim > 0.999
+    # multi-model best (scan-template-v4.py:289-319)
+    models = {p: {"model_data": pickle.load(open(base / p / "face_model.pkl", "rb"))} for p in ("alice", "bob")}
+    assert recognize_face_all_models(xa[5].reshape(64, 64), models, 0.8)[1] == "alice"
+    assert recognize_face_all_models(xb[7].reshape(64, 64), models, 0.8)[1] == "bob"
+    tr = FaceTrainer()
+    assert tr.load_model(str(base / "bob" / "face_model.pkl")) and tr.person_id_map == {"bob": 0}
+
+
+def test_train_manual_cli(tmp_path):
+    from PIL import Image
+    from eigenface.cli import train_manual
+    d = tmp_path / "faces_in"
+    d.mkdir()
+    x, _ = orc.synth_faces(150, 40, r=24, seed=8)
+    for i, row in enumerate(x):
+        Image.fromarray(row.reshape(40, 40), mode="L").save(d / f"img_{i:03d}.png")
+    assert train_manual(str(d), "carol", str(tmp_path / "models"), "light", 20) == 0
+    meta = json.load(open(tmp_path / "models" / "carol_light_model_info.json"))
+    _, _, _, lam = orc.manual_pca(x, 20)
+    np.testing.assert_allclose(meta["explained_variance_ratio"], orc.manual_model_info_evr(lam), rtol=1e-9)
+    md = pickle.load(open(tmp_path / "models" / "carol_light_pca_model.pkl", "rb"))
+    assert md["eigenfaces"].shape == (1600, 20) and md["training_filenames"][0] == "img_000.png"
+    from eigenface import recognize_face
+    name, sim, ok = recognize_face(x[11].astype(np.float64), md, 0.7)
+    assert name == "carol" and ok and sim > 0.9999
