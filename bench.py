@@ -193,7 +193,7 @@ def main():
 
     host_rate = None
     if world == 1:  # PCIe-inclusive rate of the host-buffer boundary (never `value`)
-        eng.set_stream(0)
+        eng.use_own_stream()
         eng.recognize_keys(P, args.metric)
         t = time.perf_counter()
         for _ in range(3):

@@ -189,7 +189,13 @@ const char* ef_last_error(const ef_ctx* c) { return c ? c->err.c_str() : "null c
 
 int ef_set_stream(ef_ctx* c, void* s) {
   if (!c) return EF_E_INVALID;
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  c->stream = static_cast<hipStream_t>(s);  // NULL = the default stream
+  return EF_OK;
+}
+
+int ef_use_own_stream(ef_ctx* c) {
+  if (!c) return EF_E_INVALID;
+  c->stream = c->own_stream;
   return EF_OK;
 }
 

@@ -44,6 +44,7 @@ _SIGS = {
     "ef_destroy": ([vp], None),
     "ef_last_error": ([vp], C.c_char_p),
     "ef_set_stream": ([vp, vp], C.c_int),
+    "ef_use_own_stream": ([vp], C.c_int),
     "ef_synchronize": ([vp], C.c_int),
     "ef_fit": ([vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
     "ef_model_set": ([vp, vp, vp, i64, i32, u32], C.c_int),

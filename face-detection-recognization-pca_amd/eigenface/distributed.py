@@ -47,22 +47,30 @@ class ShardedGallery:
             engine.set_gallery(gallery_local, global_offset=self.lo)
         self._local = local_search or (lambda q, m, keys=None: engine.search_keys(q, m, keys=keys))
 
-    def search_keys(self, Q, metric="l2", keys=None):
+    def _allreduce_min(self, k):
         import torch
         import torch.distributed as dist
+
+        if self.world == 1:
+            return k
+        if not isinstance(k, torch.Tensor):
+            k = torch.from_numpy(np.ascontiguousarray(k))
+        if k.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: reduce on host
+            h = k.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MIN, group=self.group)
+            k.copy_(h)
+        else:  # RCCL over xGMI, stream-ordered on torch's current stream
+            dist.all_reduce(k, op=dist.ReduceOp.MIN, group=self.group)
+        return k
+
+    def search_keys(self, Q, metric="l2", keys=None):
+        import torch
 
         k = self._local(Q, metric, keys=keys) if keys is not None else self._local(Q, metric)
         if not isinstance(k, torch.Tensor):
             k = torch.from_numpy(np.ascontiguousarray(k))
-        if self.world > 1:
-            dist.all_reduce(k, op=dist.ReduceOp.MIN, group=self.group)
-        return k
+        return self._allreduce_min(k)
 
     def recognize_keys(self, P, metric="l2", keys=None):
         """Fused projection + local search + all-reduce (engine path)."""
-        import torch.distributed as dist
-
-        k = self.engine.recognize_keys(P, metric, keys=keys)
-        if self.world > 1:
-            dist.all_reduce(k, op=dist.ReduceOp.MIN, group=self.group)
-        return k
+        return self._allreduce_min(self.engine.recognize_keys(P, metric, keys=keys))

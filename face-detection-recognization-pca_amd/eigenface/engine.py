@@ -94,8 +94,13 @@ class Engine:
         return N.check(self._h, rc)
 
     def set_stream(self, stream_handle):
-        """Run on an external hipStream_t (int handle, e.g. torch stream.cuda_stream)."""
-        self._chk(self._lib.ef_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+        """Launch on an external hipStream_t (int handle, e.g. torch's
+        ``current_stream().cuda_stream``; 0 is the default stream)."""
+        self._chk(self._lib.ef_set_stream(self._h, C.c_void_p(int(stream_handle) or None)))
+
+    def use_own_stream(self):
+        """Back to the context's own non-blocking stream."""
+        self._chk(self._lib.ef_use_own_stream(self._h))
 
     def synchronize(self):
         self._chk(self._lib.ef_synchronize(self._h))

@@ -67,9 +67,11 @@ int ef_device_count(int* out);
 int ef_create(int device, ef_ctx** out);
 void ef_destroy(ef_ctx* ctx);
 const char* ef_last_error(const ef_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the ctx's own stream. */
+/* Launch on an external hipStream_t, e.g. torch.cuda.current_stream().cuda_stream;
+ * NULL means the default (null) stream.  ef_use_own_stream restores the ctx's own
+ * non-blocking stream (the default after ef_create). */
 int ef_set_stream(ef_ctx* ctx, void* hip_stream);
+int ef_use_own_stream(ef_ctx* ctx);
 int ef_synchronize(ef_ctx* ctx);
 
 /* -------------------------------------------------------------------- fit
