@@ -13,13 +13,12 @@
 namespace ef {
 
 // ---- padded widths ------------------------------------------------------------------
-// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,96,128}
+// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,128}
 // (zero padding is exact for dot products and distances).
 inline int feature_pad(int k) {
   if (k <= 16) return 16;
   if (k <= 32) return 32;
   if (k <= 64) return 64;
-  if (k <= 96) return 96;
   if (k <= 128) return 128;
   return -1;
 }

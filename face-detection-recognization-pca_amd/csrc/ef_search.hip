@@ -31,6 +31,7 @@
 #include "ef_internal.hpp"
 
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 
 namespace ef {
@@ -48,20 +49,54 @@ __device__ __forceinline__ float key_value(long long key) {
   return __int_as_float(s >= 0 ? s : (s ^ 0x7FFFFFFF));
 }
 
-constexpr int TG = 32;  // gallery rows per tile
+constexpr int TG = 64;  // gallery rows per LDS tile (two 32-row MFMA blocks)
 
-template <int KP, int METRIC, bool COLLECT>
-__global__ __launch_bounds__(256, 2) void search_kernel(
+// LDS-DMA (global_load_lds) in inline asm: hipcc would otherwise treat the pending DMA
+// as an aliasing LDS write and put s_waitcnt vmcnt(0) before every ds_read, serialising the
+// prefetch of tile t+1 with the MFMAs of tile t.  M0 (the wave-uniform LDS destination) is
+// written and restored inside the statement; completion is waited for explicitly with
+// s_waitcnt vmcnt(0) before the barrier that publishes the tile.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {  // wave-uniform by construction
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
+}
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Workgroup = 8 waves x 32 probes = 256 probes (the gallery is swept Bpad/256 times).
+// Each wave keeps its 32 probes as one B block (KP/2 VGPRs, pre-scaled) and runs the
+// tile's two 32-row blocks as two independent accumulator chains; the arg-best epilogue
+// is a branch-free top-2 in row order on registers.  <= 128 VGPRs -> 4 waves per SIMD.
+// ABL (diagnostic builds only, results invalid): bit 1 skips the epilogue, bit 4 skips
+// the per-tile wait + barrier.
+template <int KP, int METRIC, bool COLLECT, int ABL = 0>
+__global__ __launch_bounds__(512, 4) void search_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
     int n_ptiles, int tiles_per_chunk, int64_t bpad, SearchWs ws) {
+  constexpr int NW = 8;
   constexpr int KH = KP / 2;
-  constexpr int LDS_STRIDE = KP + 4;
-  constexpr int F4_ROW = KP / 4;
-  constexpr int F4_TILE = TG * F4_ROW;
-  constexpr int F4_PER_THREAD = (F4_TILE + 255) / 256;
+  constexpr int CPR = KP / 4;                                          // 16-B chunks per row
+  constexpr int SW = (CPR & 15) == 0 ? 16 : ((CPR & 7) == 0 ? 8 : 4);  // XOR swizzle width
+  constexpr int NI = TG * CPR / 64;                                    // 1-KiB LDS-DMA pieces per tile
+  constexpr int PPW = (NI + NW - 1) / NW;                              // pieces per wave
+  constexpr int RP = 64 / CPR;                                         // rows per piece
+  static_assert((NI % NW == 0 || NI < NW) && RP * CPR == 64 && TG == 64, "tile must be whole 1-KiB pieces");
 
-  __shared__ __attribute__((aligned(16))) float sG[2][TG * LDS_STRIDE];
-  __shared__ __attribute__((aligned(16))) float sAux[2][TG];
+  // Unpadded [TG][KP] tiles filled by global_load_lds (lane-linear 1-KiB pieces); the
+  // chunk order inside each row is XOR-swizzled by (row & (SW-1)) on the SOURCE address so
+  // the A-fragment ds_read_b128s (16 lanes = 16 rows, same logical chunk) hit distinct
+  // banks.  All LDS lives in one array (a second __shared__ object can de-pipeline).
+  __shared__ __attribute__((aligned(16))) float smem[2 * TG * KP + 2 * TG];
+  float* const sG0 = smem;
+  float* const sAux0 = smem + 2 * TG * KP;
 
   // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD a contiguous run of
   // (chunk, probe-tile) pairs so the probe tiles of one chunk are co-resident on it.
@@ -78,189 +113,211 @@ __global__ __launch_bounds__(256, 2) void search_kernel(
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5;
   const int c32 = lane & 31;
+  const int lrow = lane / CPR, lc = lane % CPR;  // this lane's (row, chunk) inside a piece
 
   const int64_t tiles_total = (n + TG - 1) / TG;
   const int64_t t0 = (int64_t)gc * tiles_per_chunk;
   const int64_t t1 = t0 + tiles_per_chunk < tiles_total ? t0 + tiles_per_chunk : tiles_total;
-
-  // probe slots of this lane (two 32-probe blocks)
-  const int64_t s0 = (int64_t)pt * 256 + wave * 64 + c32;
-  const int64_t s1 = s0 + 32;
+  const int64_t s0 = (int64_t)pt * 256 + wave * 32 + c32;  // this lane's probe slot
 
   if (t0 >= t1) {  // empty chunk: publish "no candidate" so the reducer can skip it
     if constexpr (!COLLECT) {
       if (h == 0) {
         ws.part_key[(int64_t)gc * bpad + s0] = LLONG_MAX;
-        ws.part_key[(int64_t)gc * bpad + s1] = LLONG_MAX;
         ws.part_b2[(int64_t)gc * bpad + s0] = __builtin_inff();
-        ws.part_b2[(int64_t)gc * bpad + s1] = __builtin_inff();
       }
     }
     return;
   }
 
-  // Probe fragments (B operand): lane holds probe (c32) of each block, k in [h*KH, h*KH+KH).
-  float qb0[KH], qb1[KH];
+  // Issue the LDS-DMA of tile t into buffer buf.  Wave w fills pieces [w*PPW, (w+1)*PPW);
+  // a piece is RP whole rows.  The swizzle splits into a lane constant and a wave-uniform
+  // part: row & (SW-1) == ((j*RP) & (SW-1)) ^ (lrow & (SW-1)) for power-of-two RP, SW.
+  // Rows past n (tail tile only) are clamped to a valid row and masked in the epilogue.
+  const int lcx = lc ^ (lrow & (SW - 1));
+  const unsigned lds_base = lds_addr(smem);
+  auto issue_tile = [&](int64_t t, int buf) {
+    const float* gbase = G + t * TG * KP;  // wave-uniform
+    const int nrem = (int)((n - t * TG) < TG ? (n - t * TG) : TG);
+    int lx = lcx, lr = lrow;
+    asm volatile("" : "+v"(lx), "+v"(lr));  // recompute per tile (no hoisted per-piece VGPRs)
+#pragma unroll
+    for (int jj = 0; jj < PPW; ++jj) {
+      const int j = wave * PPW + jj;
+      if (NI >= NW || wave < NI) {  // uniform
+        const int sj = (j * RP) & (SW - 1);
+        int row = j * RP + lr;
+        if (nrem < TG) row = row < nrem ? row : nrem - 1;
+        glds16(gbase + row * KP + ((lx ^ sj) << 2), lds_base + (unsigned)((buf * TG * KP + j * 256) * 4));
+      }
+    }
+    if (wave == 0) {
+      const int row = lane < nrem ? lane : nrem - 1;
+      glds4(aux + t * TG + row, lds_base + (unsigned)((2 * TG * KP + buf * TG) * 4));  // one 4-B piece per lane
+    }
+  };
+
+  issue_tile(t0, 0);
+
+  // Probe fragments (B operand): lane holds probe c32, k in [h*KH, h*KH+KH), pre-scaled
+  // (exactly) so the chain yields the score: L2 acc = ||g||^2 + sum(-2q)g (the chain
+  // starts from ||g||^2), cosine acc = -q.g (times 1/||g|| after the chain).
+  constexpr float QS = METRIC == EF_METRIC_L2 ? -2.f : -1.f;
+  float qb[KH];
   {
-    int64_t r0 = s0, r1 = s1;
-    bool v0 = true, v1 = true;
+    int64_t r0 = s0;
+    bool v0 = true;
     if constexpr (COLLECT) {
       v0 = s0 < n_amb;
-      v1 = s1 < n_amb;
       r0 = v0 ? ws.amb_list[s0] : 0;
-      r1 = v1 ? ws.amb_list[s1] : 0;
     }
     const float4* q0 = reinterpret_cast<const float4*>(qpad + r0 * KP + h * KH);
-    const float4* q1 = reinterpret_cast<const float4*>(qpad + r1 * KP + h * KH);
 #pragma unroll
     for (int j = 0; j < KH / 4; ++j) {
-      float4 a = v0 ? q0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 b = v1 ? q1[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      qb0[4 * j] = a.x; qb0[4 * j + 1] = a.y; qb0[4 * j + 2] = a.z; qb0[4 * j + 3] = a.w;
-      qb1[4 * j] = b.x; qb1[4 * j + 1] = b.y; qb1[4 * j + 2] = b.z; qb1[4 * j + 3] = b.w;
+      const float4 a = v0 ? q0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      qb[4 * j] = QS * a.x; qb[4 * j + 1] = QS * a.y; qb[4 * j + 2] = QS * a.z; qb[4 * j + 3] = QS * a.w;
     }
   }
-  float thr0 = -__builtin_inff(), thr1 = -__builtin_inff();
+  float thr = -__builtin_inff();
   if constexpr (COLLECT) {
-    if (s0 < n_amb) thr0 = ws.thr[s0];
-    if (s1 < n_amb) thr1 = ws.thr[s1];
+    if (s0 < n_amb) thr = ws.thr[s0];
   }
-
-  const float4* G4 = reinterpret_cast<const float4*>(G);
-  float4 stage[F4_PER_THREAD];
-  float stage_aux = 0.f;
-
-  auto load_tile = [&](int64_t t) {
+  // Consume every probe register here, so hipcc places its waits for these loads before
+  // the loop; otherwise its (loop-merged) wait state puts vmcnt(0) inside the tile loop,
+  // which would also drain the asm LDS-DMA of the next tile.
 #pragma unroll
-    for (int j = 0; j < F4_PER_THREAD; ++j) {
-      const int idx = tid + j * 256;
-      if (idx < F4_TILE) {
-        const int row = idx / F4_ROW;
-        const int c4 = idx - row * F4_ROW;
-        const int64_t grow = t * TG + row;
-        stage[j] = grow < n ? G4[grow * F4_ROW + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    if (tid < TG) {
-      const int64_t grow = t * TG + tid;
-      stage_aux = grow < n ? aux[grow] : 0.f;  // padded rows are masked in the epilogue
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < F4_PER_THREAD; ++j) {
-      const int idx = tid + j * 256;
-      if (idx < F4_TILE) {
-        const int row = idx / F4_ROW;
-        const int c4 = idx - row * F4_ROW;
-        *reinterpret_cast<float4*>(&sG[buf][row * LDS_STRIDE + c4 * 4]) = stage[j];
-      }
-    }
-    if (tid < TG) sAux[buf][tid] = stage_aux;
-  };
+  for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(qb[j]));
+  asm volatile("" ::"v"(thr));
 
   const float INF = __builtin_inff();
-  float b1_0 = INF, b2_0 = INF, b1_1 = INF, b2_1 = INF;
-  int i1_0 = INT_MAX, i1_1 = INT_MAX;
+  float b1 = INF, b2 = INF;
+  int i1 = INT_MAX;
 
-  load_tile(t0);
-  store_tile(0);
-  __syncthreads();
+  // Arg-best epilogue of one finished block of scores v (register r <-> row
+  // rowbase + (r&3) + 8(r>>2) + 4h, increasing with r): branch-free top-2 in row order
+  // (strict '<' keeps the lowest row on ties; v_med3 keeps the runner-up), then merged
+  // into the running (best, index, runner-up).  COLLECT appends rows within thr instead.
+  auto consume = [&](const f32x16& v, int rowbase) {
+    if constexpr (COLLECT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (v[r] <= thr) {
+          const int pos = atomicAdd(&ws.cand_cnt[s0], 1);
+          if (pos < kCandMax) ws.cand[s0 * kCandMax + pos] = rowbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+        }
+      }
+    } else {
+      float m1 = v[0], m2 = INF;
+      int ir = 0;
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        const bool lt = v[r] < m1;
+        m2 = __builtin_amdgcn_fmed3f(m1, v[r], m2);
+        ir = lt ? r : ir;
+        m1 = lt ? v[r] : m1;
+      }
+      const bool lt = m1 < b1;
+      b2 = lt ? fminf(b1, m2) : fminf(b2, m1);
+      i1 = lt ? rowbase + (ir & 3) + 8 * (ir >> 2) + 4 * h : i1;
+      b1 = lt ? m1 : b1;
+    }
+  };
+
+  // Accumulator start value: ||g||^2 of the block's rows for L2 (four float4 reads of the
+  // staged norms match the register <-> row map), 0 for cosine.
+  auto acc_init = [&](const float* tileA_blk) {
+    f32x16 a = {};
+    if constexpr (METRIC == EF_METRIC_L2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(tileA_blk + 8 * q + 4 * h);
+        a[4 * q] = x.x;
+        a[4 * q + 1] = x.y;
+        a[4 * q + 2] = x.z;
+        a[4 * q + 3] = x.w;
+      }
+    }
+    return a;
+  };
+
+  dma_wait_all();
+  __syncthreads();  // tile t0 landed
 
   for (int64_t t = t0; t < t1; ++t) {
     const int buf = (int)((t - t0) & 1);
-    const bool more = t + 1 < t1;
-    if (more) load_tile(t + 1);
+    if (t + 1 < t1) issue_tile(t + 1, buf ^ 1);  // lands under this tile's MFMAs
+    const float* tileG = sG0 + buf * TG * KP;
+    const float* tileA = sAux0 + buf * TG;
+    const bool tail = (t + 1) * TG > n;
+    const int tbase = (int)(t * TG);
+    int swz = c32 & (SW - 1);  // rows c32 and 32 + c32 share (row & (SW-1)), SW <= 16
+    // opaque per tile: stops hipcc hoisting all KH/4 swizzled addresses out of the loop
+    asm volatile("" : "+v"(swz));
+    const float* arow0 = tileG + c32 * KP;
+    const float* arow1 = tileG + (32 + c32) * KP;
 
-    f32x16 acc0 = {}, acc1 = {};
-    const float* arow = &sG[buf][c32 * LDS_STRIDE + h * KH];
+    // both 32-row blocks at once: two independent accumulator chains sharing the B operand
+    f32x16 acc0 = acc_init(tileA), acc1 = acc_init(tileA + 32);
 #pragma unroll
     for (int s = 0; s < KH; s += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(arow + s);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb0[s], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb1[s], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qb0[s + 1], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qb1[s + 1], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qb0[s + 2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qb1[s + 2], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qb0[s + 3], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qb1[s + 3], acc1, 0, 0, 0);
+      const int chunk = (h * (CPR / 2) + s / 4) ^ swz;
+      const float4 a = *reinterpret_cast<const float4*>(arow0 + chunk * 4);
+      const float4 b = *reinterpret_cast<const float4*>(arow1 + chunk * 4);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.x, qb[s], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qb[s + 1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.y, qb[s + 1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qb[s + 2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.z, qb[s + 2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qb[s + 3], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.w, qb[s + 3], acc1, 0, 0, 0);
+      if ((s / 4) % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound the A prefetch depth
     }
-
-    // Epilogue: accumulator register r holds gallery row (r&3) + 8*(r>>2) + 4*h.
-    const int rowbase = (int)(t * TG);
-    const bool tail = (t + 1) * TG > n;  // uniform; only the last tile has padded rows
-    auto epilogue = [&](auto mask_c) {
-      constexpr bool MASK = decltype(mask_c)::value;
+    if constexpr (METRIC != EF_METRIC_L2) {  // cosine: -(q.g) * (1/||g||)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 a4 = *reinterpret_cast<const float4*>(&sAux[buf][8 * q + 4 * h]);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * q + e;
-          const int row = rowbase + 8 * q + 4 * h + e;
-          float v0, v1;
-          if constexpr (METRIC == EF_METRIC_L2) {
-            v0 = __builtin_fmaf(-2.f, acc0[r], av[e]);
-            v1 = __builtin_fmaf(-2.f, acc1[r], av[e]);
-          } else {
-            v0 = -(acc0[r] * av[e]);
-            v1 = -(acc1[r] * av[e]);
-          }
-          if constexpr (MASK) {
-            if (row >= n) { v0 = INF; v1 = INF; }
-          }
-          if constexpr (COLLECT) {
-            if (v0 <= thr0) {
-              const int pos = atomicAdd(&ws.cand_cnt[s0], 1);
-              if (pos < kCandMax) ws.cand[s0 * kCandMax + pos] = row;
-            }
-            if (v1 <= thr1) {
-              const int pos = atomicAdd(&ws.cand_cnt[s1], 1);
-              if (pos < kCandMax) ws.cand[s1 * kCandMax + pos] = row;
-            }
-          } else {
-            // running (best, index, runner-up); strict '<' keeps the lowest row on ties
-            b2_0 = fminf(b2_0, fmaxf(b1_0, v0));
-            if (v0 < b1_0) { b1_0 = v0; i1_0 = row; }
-            b2_1 = fminf(b2_1, fmaxf(b1_1, v1));
-            if (v1 < b1_1) { b1_1 = v1; i1_1 = row; }
-          }
-        }
+        const float4 x = *reinterpret_cast<const float4*>(tileA + 8 * q + 4 * h);
+        const float4 y = *reinterpret_cast<const float4*>(tileA + 32 + 8 * q + 4 * h);
+        acc0[4 * q] *= x.x; acc0[4 * q + 1] *= x.y; acc0[4 * q + 2] *= x.z; acc0[4 * q + 3] *= x.w;
+        acc1[4 * q] *= y.x; acc1[4 * q + 1] *= y.y; acc1[4 * q + 2] *= y.z; acc1[4 * q + 3] *= y.w;
       }
-    };
-    if (tail)
-      epilogue(std::integral_constant<bool, true>{});
-    else
-      epilogue(std::integral_constant<bool, false>{});
-
-    if (more) store_tile(buf ^ 1);
-    __syncthreads();
+    }
+    if (tail) {  // uniform: only the last tile has rows past n
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= n) acc0[r] = INF;
+        if (row + 32 >= n) acc1[r] = INF;
+      }
+    }
+    if constexpr (ABL & 1) {
+      asm volatile("" ::"v"(acc0), "v"(acc1));
+    } else {
+      consume(acc0, tbase);  // rows of block 0 precede block 1 (row-order tie rule)
+      consume(acc1, tbase + 32);
+    }
+    if constexpr (!(ABL & 4)) {
+      dma_wait_all();
+      __syncthreads();  // tile t+1 landed; everyone is done reading buffer buf
+    }
   }
 
   if constexpr (!COLLECT) {
     // Merge the two lane halves (same probe, disjoint rows).
-    auto merge = [&](float& b1, int& i1, float& b2) {
-      const float ob1 = __shfl_xor(b1, 32);
-      const int oi1 = __shfl_xor(i1, 32);
-      const float ob2 = __shfl_xor(b2, 32);
-      const bool other = ob1 < b1 || (ob1 == b1 && oi1 < i1);
-      const float lose = other ? b1 : ob1;
-      b2 = fminf(fminf(b2, ob2), lose);
-      if (other) { b1 = ob1; i1 = oi1; }
-    };
-    merge(b1_0, i1_0, b2_0);
-    merge(b1_1, i1_1, b2_1);
+    const float ob1 = __shfl_xor(b1, 32);
+    const int oi1 = __shfl_xor(i1, 32);
+    const float ob2 = __shfl_xor(b2, 32);
+    const bool other = ob1 < b1 || (ob1 == b1 && oi1 < i1);
+    const float lose = other ? b1 : ob1;
+    b2 = fminf(fminf(b2, ob2), lose);
+    if (other) { b1 = ob1; i1 = oi1; }
     if (h == 0) {
       const int64_t o = (int64_t)gc * bpad;
-      ws.part_key[o + s0] = i1_0 == INT_MAX ? LLONG_MAX : pack_key(b1_0, (unsigned)i1_0);
-      ws.part_key[o + s1] = i1_1 == INT_MAX ? LLONG_MAX : pack_key(b1_1, (unsigned)i1_1);
-      ws.part_b2[o + s0] = b2_0;
-      ws.part_b2[o + s1] = b2_1;
+      ws.part_key[o + s0] = i1 == INT_MAX ? LLONG_MAX : pack_key(b1, (unsigned)i1);
+      ws.part_b2[o + s0] = b2;
     }
   }
 }
@@ -461,22 +518,29 @@ template <int KP, int M>
 static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpad, int64_t bpad, int64_t b,
                            const float* G, const float* aux, int64_t n, int64_t g_offset, float gmax2,
                            const SearchWs& ws, long long* keys, bool timed_main, TimerEvt* tev, ef_ctx* c) {
-  const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
+  const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
-  hipLaunchKernelGGL((search_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                     pl.tiles_per_chunk, bpad, ws);
+  static const int abl = [] { const char* e = getenv("EF_SEARCH_ABL"); return e ? atoi(e) : 0; }();
+  if (KP == 128 && M == EF_METRIC_L2 && abl > 0) {  // diagnostic ablations (timing only)
+    auto k = abl == 1 ? search_kernel<KP, M, false, 1> : abl == 4 ? search_kernel<KP, M, false, 4>
+                                                                   : search_kernel<KP, M, false, 5>;
+    hipLaunchKernelGGL(k, grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles, pl.tiles_per_chunk, bpad, ws);
+  } else {
+    hipLaunchKernelGGL((search_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, bpad, ws);
+  }
   if (timed_main) timer_end(c, tev);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
   if (e != hipSuccess) return e;
   const dim3 pgrid((unsigned)((b + 3) / 4));
-  hipLaunchKernelGGL((reduce_kernel<KP, M>), pgrid, block, 0, s, qpad, b, bpad, pl.nchunks, G, n, g_offset,
+  hipLaunchKernelGGL((reduce_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n, g_offset,
                      gmax2, ws, keys);
   // queued (fp32-ambiguous) probes: collect + fp64 resolve; both exit at once when none
   hipLaunchKernelGGL((search_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                      pl.tiles_per_chunk, bpad, ws);
-  hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, block, 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+  hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
   return hipGetLastError();
 }
 
@@ -496,7 +560,6 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
     EF_SEARCH_CASE(16)
     EF_SEARCH_CASE(32)
     EF_SEARCH_CASE(64)
-    EF_SEARCH_CASE(96)
     EF_SEARCH_CASE(128)
     default:
       return hipErrorInvalidValue;
