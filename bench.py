@@ -27,9 +27,11 @@ sys.path.insert(0, os.path.join(ROOT, "face-detection-recognization-pca_amd"))
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (/opt/skills/guides/MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (gallery rows, face side, k, probe batch)
-    "c3": (1_000_000, 128, 128, 4096),
-    "c2": (10_000, 128, 64, 4096),
+    # name: (gallery rows, face side, k, probe batch, projection precision)
+    "c3": (1_000_000, 128, 128, 4096, "fp32"),
+    "c2": (10_000, 128, 64, 4096, "fp32"),
+    # BASELINE.json configs[4]: 256x256 faces, k=512, bf16 projection, fp32 distances
+    "c5": (1_000_000, 256, 512, 4096, "bf16"),
 }
 
 
@@ -138,7 +140,7 @@ def main():
     from eigenface import Engine, decode_keys, synth
     from eigenface.distributed import ShardedGallery, shard_range
 
-    n_total, side, k, bsz = CONFIGS[args.config]
+    n_total, side, k, bsz, precision = CONFIGS[args.config]
     d = side * side
     lo, hi = shard_range(n_total, rank, world)
 
@@ -153,7 +155,7 @@ def main():
     eng = Engine(local)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
-    eng.set_model(mean, W)
+    eng.set_model(mean, W, precision=precision)
     shard = ShardedGallery(eng, G, n_total, rank, world)
     P_dev = torch.from_numpy(P).to(dev)
     keys = torch.empty(bsz, dtype=torch.int64, device=dev)
@@ -209,7 +211,8 @@ def main():
         achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
         rec = {
-            "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128",
+            "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128" if args.config == "c3"
+                      else f"faces/sec recognized (projection+NN) @{n_total}-gallery k={k}",
             "value": round(value, 1),
             "unit": "faces/s",
             "n_gpus": world,
@@ -219,11 +222,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if precision == "fp32" else "bf16 projection, f32 distance",
             "data": "synthetic (eigenface.synth planted probes; gallery = eigen-coefficients)",
             "config": {
                 "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
-                            f"probe batch {bsz}, metric {args.metric}",
+                            f"probe batch {bsz}, metric {args.metric}, projection {precision}",
                 "gallery": n_total, "face": f"{side}x{side}", "k": k, "batch": bsz,
                 "parallelism": f"gallery row-shard x{world} + RCCL all-reduce(MIN) of packed keys"
                                if world > 1 else "1 GPU",

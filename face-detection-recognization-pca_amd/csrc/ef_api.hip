@@ -73,7 +73,7 @@ static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long
     EF_HIP(c, launch_keys_none(c->stream, keys_dev, b), "keys");
     return EF_OK;
   }
-  const SearchPlan pl = search_plan(bpad, c->n_gallery);
+  const SearchPlan pl = search_plan(bpad, c->n_gallery, c->g_kp);
   // workspace carve-out (16-byte aligned pieces)
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t nkb = al((size_t)pl.nchunks * bpad * 8), nb2 = al((size_t)pl.nchunks * bpad * 4);
@@ -108,18 +108,27 @@ static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long
 static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t bpad, float* f_dev) {
   EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->kp * sizeof(float)));
   int64_t pps = 0;
-  const int ns = project_nsplit(bpad, c->d, &pps);
+  const int ns = c->bf16 ? project_bf16_nsplit(bpad, c->d, c->kpw, &pps) : project_nsplit(bpad, c->d, c->kpw, &pps);
   EF_TRY(ensure(c, c->proj_part, (size_t)ns * bpad * c->kpw * sizeof(float)));
   TimerEvt t;
   timer_begin(c, EF_KERNEL_PROJECT, &t);
-  EF_HIP(c,
-         launch_project(c->stream, c->kpw, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean.p),
-                        static_cast<const float*>(c->W.p), static_cast<float*>(c->proj_part.p), ns, pps),
-         "project kernel");
+  if (c->bf16) {
+    EF_HIP(c,
+           launch_project_bf16(c->stream, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean_r.p),
+                               static_cast<const unsigned short*>(c->W16.p), c->kpw,
+                               static_cast<float*>(c->proj_part.p), ns, pps),
+           "project kernel (bf16)");
+  } else {
+    EF_HIP(c,
+           launch_project(c->stream, c->kpw, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean.p),
+                          static_cast<const float*>(c->W.p), static_cast<float*>(c->proj_part.p), ns, pps),
+           "project kernel");
+  }
   timer_end(c, &t);
   EF_HIP(c,
          launch_project_reduce(c->stream, static_cast<const float*>(c->proj_part.p), ns, b, bpad, c->kpw,
-                               c->k, c->kp, static_cast<float*>(c->q_pad.p), f_dev),
+                               c->k, c->kp, c->bf16 ? static_cast<const float*>(c->corr.p) : nullptr,
+                               static_cast<float*>(c->q_pad.p), f_dev),
          "project reduce");
   return EF_OK;
 }
@@ -178,8 +187,9 @@ void ef_destroy(ef_ctx* c) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
-  DevBuf* bufs[] = {&c->mean, &c->W,     &c->G,         &c->gnorm2,    &c->ginv,      &c->gmax2,
-                    &c->q_pad, &c->keys, &c->search_ws, &c->p_stage, &c->proj_part, &c->feats_dev};
+  DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->corr,      &c->G,
+                    &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
+                    &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -209,9 +219,10 @@ int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_
   if (!c) return EF_E_INVALID;
   if (!mean || !W || d < 1 || k < 1) return set_err(c, EF_E_INVALID, "ef_model_set: bad arguments");
   const int kp = feature_pad(k);
-  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_model_set: k > 128 is not supported by this build");
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_model_set: k > 512 is not supported by this build");
   (void)hipSetDevice(c->device);
-  const int kpw = proj_pad(kp);
+  const bool bf16 = (flags & EF_MODEL_BF16) != 0;
+  const int kpw = bf16 ? (kp + 127) / 128 * 128 : proj_pad(kp);  // bf16 kernel: 128-column tiles
   EF_TRY(ensure(c, c->mean, (size_t)d * sizeof(float)));
   EF_TRY(ensure(c, c->W, (size_t)d * kpw * sizeof(float)));
   const hipMemcpyKind kind = (flags & EF_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
@@ -228,6 +239,22 @@ int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   release(tmp);
   if (e != hipSuccess) return hip_err(c, e, "pad W");
+  if (bf16) {
+    const int ldw = kpw;
+    EF_TRY(ensure(c, c->W16, (size_t)ldw * d * sizeof(unsigned short)));
+    EF_TRY(ensure(c, c->mean_r, (size_t)d * sizeof(float)));
+    EF_TRY(ensure(c, c->corr, (size_t)ldw * sizeof(float)));
+    const int nchunk = 256;
+    DevBuf cp;
+    EF_TRY(ensure(c, cp, (size_t)nchunk * ldw * sizeof(double)));
+    e = launch_bf16_model(c->stream, static_cast<const float*>(c->W.p), static_cast<const float*>(c->mean.p), d, ldw,
+                          static_cast<unsigned short*>(c->W16.p), static_cast<float*>(c->mean_r.p),
+                          static_cast<float*>(c->corr.p), static_cast<double*>(cp.p), nchunk);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    release(cp);
+    if (e != hipSuccess) return hip_err(c, e, "bf16 model");
+  }
+  c->bf16 = bf16;
   c->d = d;
   c->k = k;
   c->kp = kp;
@@ -264,7 +291,7 @@ int ef_gallery_set(ef_ctx* c, const float* G, int64_t n, int32_t k, int64_t offs
   if ((!G && n > 0) || n < 0 || k < 1 || offset < 0 || n + offset > (int64_t)UINT_MAX)
     return set_err(c, EF_E_INVALID, "ef_gallery_set: bad arguments");
   const int kp = feature_pad(k);
-  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 128 is not supported by this build");
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 512 is not supported by this build");
   (void)hipSetDevice(c->device);
   c->n_gallery = 0;
   if (n > 0) {

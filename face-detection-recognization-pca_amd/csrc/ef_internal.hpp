@@ -13,17 +13,20 @@
 namespace ef {
 
 // ---- padded widths ------------------------------------------------------------------
-// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,128}
+// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,128,256,512}
 // (zero padding is exact for dot products and distances).
 inline int feature_pad(int k) {
   if (k <= 16) return 16;
   if (k <= 32) return 32;
   if (k <= 64) return 64;
   if (k <= 128) return 128;
+  if (k <= 256) return 256;
+  if (k <= 512) return 512;
   return -1;
 }
-// The projection GEMM writes KPW = 64 or 128 columns.
-inline int proj_pad(int kp) { return kp <= 64 ? 64 : 128; }
+constexpr int kMaxK = 512;
+// The projection GEMM writes KPW = 64 or a multiple of 128 columns (128-column tiles).
+inline int proj_pad(int kp) { return kp <= 64 ? 64 : (kp + 127) / 128 * 128; }
 
 constexpr int kSearchProbeTile = 256;   // probes per search workgroup (4 waves x 64)
 constexpr int kProjRowTile = 128;       // probes per projection workgroup
@@ -69,6 +72,10 @@ struct ef_ctx {
   int k = 0, kp = 0, kpw = 0;
   ef::DevBuf mean;  // float[d]
   ef::DevBuf W;     // float[d][kpw]
+  bool bf16 = false;   // EF_MODEL_BF16: project with W16 on bf16 MFMA
+  ef::DevBuf W16;      // bf16[kpw][d]
+  ef::DevBuf mean_r;   // float[d] round(mean)
+  ef::DevBuf corr;     // float[kpw] (mean - round(mean)).W
 
   // gallery
   int64_t n_gallery = 0, g_offset = 0;
@@ -103,7 +110,7 @@ void timer_begin(ef_ctx* c, int kernel, TimerEvt* t);
 void timer_end(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
-SearchPlan search_plan(int64_t bpad, int64_t n);
+SearchPlan search_plan(int64_t bpad, int64_t n, int kp);
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
                          int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
                          float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
@@ -116,8 +123,16 @@ hipError_t launch_gallery_aux(hipStream_t s, const float* G, int64_t n, int kp, 
 hipError_t launch_project(hipStream_t s, int kpw, int p_dtype, const void* P, int64_t b,
                           int64_t bpad, int64_t d, const float* mean, const float* W,
                           float* part, int nsplit, int64_t pix_per_split);
-int project_nsplit(int64_t bpad, int64_t d, int64_t* pix_per_split);
+int project_nsplit(int64_t bpad, int64_t d, int kpw, int64_t* pix_per_split);
 hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, int64_t b,
-                                 int64_t bpad, int kpw, int k, int kp, float* qpad, float* f_out);
+                                 int64_t bpad, int kpw, int k, int kp, const float* corr, float* qpad,
+                                 float* f_out);
+// bf16 model (EF_MODEL_BF16): W16 [kpw][d] bf16, round(mean), fp64-derived correction row
+hipError_t launch_bf16_model(hipStream_t s, const float* W, const float* mean, int64_t d, int ldw,
+                             unsigned short* Wt16, float* mean_r, float* corr, double* corr_part, int nchunk);
+int project_bf16_nsplit(int64_t bpad, int64_t d, int ldw, int64_t* pix_per_split);
+hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_t b, int64_t bpad, int64_t d,
+                               const float* mean_r, const unsigned short* Wt16, int ldw, float* part, int nsplit,
+                               int64_t pps);
 
 }  // namespace ef

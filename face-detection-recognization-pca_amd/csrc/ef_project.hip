@@ -20,10 +20,12 @@ constexpr int BM = kProjRowTile;  // 128 probes
 constexpr int BK = 32;            // pixels per stage
 constexpr int SA = BK + 4;        // LDS row stride of the pixel tile (conflict-free b128 reads)
 
+// KPW = columns of this workgroup's tile (64 | 128); ldw = total padded columns of W and of
+// the partial slabs (KPW, or a multiple of 128 with gridDim.z = ldw / 128 column tiles).
 template <int KPW, int PDT, bool VEC>
 __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict__ Pv, int64_t b,
                                                          int64_t d, const float* __restrict__ mu,
-                                                         const float* __restrict__ W,
+                                                         const float* __restrict__ W, int ldw,
                                                          float* __restrict__ part, int64_t bpad,
                                                          int64_t pix_per_split) {
   constexpr int WAVES_M = KPW == 128 ? 2 : 4;
@@ -42,6 +44,7 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
   const int h = lane >> 5, c32 = lane & 31;
   const int wm = wave / (4 / WAVES_M), wn = wave % (4 / WAVES_M);
   const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int col0 = blockIdx.z * KPW;
   const int64_t k_beg = (int64_t)blockIdx.y * pix_per_split;
   int64_t k_end = k_beg + pix_per_split;
   if (k_end > d) k_end = d;
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
       const int idx = tid + 256 * j;
       const int kr = idx / (KPW / 4), c4 = idx % (KPW / 4);
       const int64_t px = kb + kr;
-      wv[j] = px < k_end ? reinterpret_cast<const float4*>(W + px * KPW)[c4]
+      wv[j] = px < k_end ? reinterpret_cast<const float4*>(W + px * ldw + col0)[c4]
                          : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
   }
 
   // partial slab [split][bpad][KPW]; col = lane&31, row = (r&3) + 8(r>>2) + 4h
-  float* out = part + (int64_t)blockIdx.y * bpad * KPW;
+  float* out = part + (int64_t)blockIdx.y * bpad * ldw + col0;
 #pragma unroll
   for (int i = 0; i < AB; ++i)
 #pragma unroll
@@ -158,28 +161,32 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * RW + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = wn * CW + j * 32 + c32;
-        out[row * KPW + col] = acc[i][j][r];
+        out[row * ldw + col] = acc[i][j][r];
       }
 }
 
 // qpad[row][c] = sum_z part[z][row][c] (c < kp, rows < bpad; fixed z order);
 // f_out[row][c] for row < b, c < k when requested.
+// corr (bf16 model only): per-column correction subtracted after the sum.
 __global__ void project_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t b,
-                                      int64_t bpad, int kpw, int k, int kp, float* __restrict__ qpad,
-                                      float* __restrict__ f_out) {
+                                      int64_t bpad, int kpw, int k, int kp, const float* __restrict__ corr,
+                                      float* __restrict__ qpad, float* __restrict__ f_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= bpad * kp) return;
   const int64_t row = i / kp;
   const int c = (int)(i - row * kp);
   float s = 0.f;
   if (row < b && c < k)
+  {
     for (int z = 0; z < nsplit; ++z) s += part[((int64_t)z * bpad + row) * kpw + c];
+    if (corr) s -= corr[c];
+  }
   qpad[i] = s;
   if (f_out && row < b && c < k) f_out[row * k + c] = s;
 }
 
-int project_nsplit(int64_t bpad, int64_t d, int64_t* pix_per_split) {
-  const int64_t mtiles = bpad / BM;
+int project_nsplit(int64_t bpad, int64_t d, int kpw, int64_t* pix_per_split) {
+  const int64_t mtiles = bpad / BM * (kpw > 128 ? kpw / 128 : 1);
   int64_t ns = (512 + mtiles - 1) / mtiles;  // ~2 workgroups per CU
   const int64_t steps = (d + BK - 1) / BK;
   if (ns > steps) ns = steps;
@@ -192,14 +199,14 @@ int project_nsplit(int64_t bpad, int64_t d, int64_t* pix_per_split) {
 
 template <int KPW, int PDT>
 static hipError_t proj_t(hipStream_t s, const void* P, int64_t b, int64_t bpad, int64_t d,
-                         const float* mean, const float* W, float* part, int nsplit, int64_t pps) {
-  const dim3 grid((unsigned)(bpad / BM), (unsigned)nsplit);
+                         const float* mean, const float* W, int ldw, float* part, int nsplit, int64_t pps) {
+  const dim3 grid((unsigned)(bpad / BM), (unsigned)nsplit, (unsigned)(ldw / KPW));
   const bool vec = (d % 16 == 0) && ((reinterpret_cast<uintptr_t>(P) & 15) == 0) && (pps % 16 == 0);
   if (vec)
-    hipLaunchKernelGGL((project_kernel<KPW, PDT, true>), grid, dim3(256), 0, s, P, b, d, mean, W, part,
+    hipLaunchKernelGGL((project_kernel<KPW, PDT, true>), grid, dim3(256), 0, s, P, b, d, mean, W, ldw, part,
                        bpad, pps);
   else
-    hipLaunchKernelGGL((project_kernel<KPW, PDT, false>), grid, dim3(256), 0, s, P, b, d, mean, W,
+    hipLaunchKernelGGL((project_kernel<KPW, PDT, false>), grid, dim3(256), 0, s, P, b, d, mean, W, ldw,
                        part, bpad, pps);
   return hipGetLastError();
 }
@@ -208,19 +215,20 @@ hipError_t launch_project(hipStream_t s, int kpw, int p_dtype, const void* P, in
                           int64_t bpad, int64_t d, const float* mean, const float* W, float* part,
                           int nsplit, int64_t pps) {
   if (kpw == 64)
-    return p_dtype == EF_U8 ? proj_t<64, EF_U8>(s, P, b, bpad, d, mean, W, part, nsplit, pps)
-                            : proj_t<64, EF_F32>(s, P, b, bpad, d, mean, W, part, nsplit, pps);
-  if (kpw == 128)
-    return p_dtype == EF_U8 ? proj_t<128, EF_U8>(s, P, b, bpad, d, mean, W, part, nsplit, pps)
-                            : proj_t<128, EF_F32>(s, P, b, bpad, d, mean, W, part, nsplit, pps);
+    return p_dtype == EF_U8 ? proj_t<64, EF_U8>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps)
+                            : proj_t<64, EF_F32>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps);
+  if (kpw % 128 == 0 && kpw <= kMaxK)
+    return p_dtype == EF_U8 ? proj_t<128, EF_U8>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps)
+                            : proj_t<128, EF_F32>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps);
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, int64_t b,
-                                 int64_t bpad, int kpw, int k, int kp, float* qpad, float* f_out) {
+                                 int64_t bpad, int kpw, int k, int kp, const float* corr, float* qpad,
+                                 float* f_out) {
   const int64_t tot = bpad * kp;
   hipLaunchKernelGGL(project_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part,
-                     nsplit, b, bpad, kpw, k, kp, qpad, f_out);
+                     nsplit, b, bpad, kpw, k, kp, corr, qpad, f_out);
   return hipGetLastError();
 }
 

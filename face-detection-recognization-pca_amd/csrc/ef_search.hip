@@ -28,7 +28,7 @@
 //   resolve_kernel re-scores them in fp64 and keeps the lowest index among exact ties.
 // Result: the argmin/argmax identity equals an fp64 evaluation with lowest-index
 // tie-break (np.argmin / np.argmax semantics), independent of fp32 rounding.
-#include "ef_internal.hpp"
+#include "ef_search_common.hpp"
 
 #include <climits>
 #include <cstdlib>
@@ -36,40 +36,7 @@
 
 namespace ef {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ long long pack_key(float v, unsigned idx) {
-  if (v == 0.0f) v = 0.0f;  // canonical +0 so that -0 and +0 tie on index
-  int b = __float_as_int(v);
-  int s = b >= 0 ? b : (b ^ 0x7FFFFFFF);
-  return (long long)(((unsigned long long)(unsigned)s << 32) | (unsigned long long)idx);
-}
-__device__ __forceinline__ float key_value(long long key) {
-  const int s = (int)(key >> 32);
-  return __int_as_float(s >= 0 ? s : (s ^ 0x7FFFFFFF));
-}
-
 constexpr int TG = 64;  // gallery rows per LDS tile (two 32-row MFMA blocks)
-
-// LDS-DMA (global_load_lds) in inline asm: hipcc would otherwise treat the pending DMA
-// as an aliasing LDS write and put s_waitcnt vmcnt(0) before every ds_read, serialising the
-// prefetch of tile t+1 with the MFMAs of tile t.  M0 (the wave-uniform LDS destination) is
-// written and restored inside the statement; completion is waited for explicitly with
-// s_waitcnt vmcnt(0) before the barrier that publishes the tile.
-__device__ __forceinline__ unsigned lds_addr(const void* p) {  // wave-uniform by construction
-  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
-}
-__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
-}
-__device__ __forceinline__ void glds4(const void* gsrc, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
-}
-__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Workgroup = 8 waves x 32 probes = 256 probes (the gallery is swept Bpad/256 times).
 // Each wave keeps its 32 probes as one B block (KP/2 VGPRs, pre-scaled) and runs the
@@ -322,38 +289,6 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   }
 }
 
-// fp64 score of gallery row `row` for probe q (L2: squared distance in difference form;
-// cosine: -q.g/(|q||g|), 0 for a zero vector — sklearn normalize semantics).
-template <int KP, int METRIC>
-__device__ __forceinline__ double score64(const float* __restrict__ q, const float* __restrict__ g, int lane) {
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll
-  for (int c = lane; c < KP; c += 64) {
-    const double qv = q[c], gv = g[c];
-    if constexpr (METRIC == EF_METRIC_L2) {
-      const double dv = qv - gv;
-      s0 = fma(dv, dv, s0);
-    } else {
-      s0 = fma(qv, gv, s0);
-      s1 = fma(qv, qv, s1);
-      s2 = fma(gv, gv, s2);
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s0 += __shfl_xor(s0, off);
-    if constexpr (METRIC != EF_METRIC_L2) {
-      s1 += __shfl_xor(s1, off);
-      s2 += __shfl_xor(s2, off);
-    }
-  }
-  if constexpr (METRIC == EF_METRIC_L2) {
-    return s0;
-  } else {
-    return (s1 > 0.0 && s2 > 0.0) ? -(s0 / (sqrt(s1) * sqrt(s2))) : 0.0;
-  }
-}
-
 // One wave per probe: winner over chunks, global runner-up, fp64 re-score, ambiguity test.
 template <int KP, int METRIC>
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ qpad, int64_t b, int64_t bpad,
@@ -499,10 +434,12 @@ __global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ x, i
 }
 
 // ------------------------------------------------------------------------ launchers
-SearchPlan search_plan(int64_t bpad, int64_t n) {
+SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
   SearchPlan pl;
-  pl.n_ptiles = (int)(bpad / kSearchProbeTile);
-  const int64_t tiles = (n + TG - 1) / TG;
+  const bool wide = kp > 128;
+  pl.n_ptiles = (int)(bpad / (wide ? kWideProbeTile : kSearchProbeTile));
+  const int64_t rows_per_tile = wide ? kWideRowTile : TG;
+  const int64_t tiles = (n + rows_per_tile - 1) / rows_per_tile;
   // ~2048 workgroups (>= 4 resident waves per SIMD over the launch); the chunk count is a
   // multiple of 8 so the XCD remap is a bijection.
   int64_t want = (2048 + pl.n_ptiles - 1) / pl.n_ptiles;
@@ -518,8 +455,13 @@ template <int KP, int M>
 static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpad, int64_t bpad, int64_t b,
                            const float* G, const float* aux, int64_t n, int64_t g_offset, float gmax2,
                            const SearchWs& ws, long long* keys, bool timed_main, TimerEvt* tev, ef_ctx* c) {
+  constexpr bool wide = KP > 128;
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
+  if constexpr (wide) {
+    const hipError_t e = launch_search_wide(s, KP, M, false, pl, qpad, G, aux, n, bpad, ws);
+    if (e != hipSuccess) return e;
+  } else {
   static const int abl = [] { const char* e = getenv("EF_SEARCH_ABL"); return e ? atoi(e) : 0; }();
   if (KP == 128 && M == EF_METRIC_L2 && abl > 0) {  // diagnostic ablations (timing only)
     auto k = abl == 1 ? search_kernel<KP, M, false, 1> : abl == 4 ? search_kernel<KP, M, false, 4>
@@ -528,6 +470,7 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
   } else {
     hipLaunchKernelGGL((search_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, bpad, ws);
+  }
   }
   if (timed_main) timer_end(c, tev);
   hipError_t e = hipGetLastError();
@@ -538,8 +481,13 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
   hipLaunchKernelGGL((reduce_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n, g_offset,
                      gmax2, ws, keys);
   // queued (fp32-ambiguous) probes: collect + fp64 resolve; both exit at once when none
-  hipLaunchKernelGGL((search_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                     pl.tiles_per_chunk, bpad, ws);
+  if constexpr (wide) {
+    e = launch_search_wide(s, KP, M, true, pl, qpad, G, aux, n, bpad, ws);
+    if (e != hipSuccess) return e;
+  } else {
+    hipLaunchKernelGGL((search_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, bpad, ws);
+  }
   hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
   return hipGetLastError();
 }
@@ -561,6 +509,8 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
     EF_SEARCH_CASE(32)
     EF_SEARCH_CASE(64)
     EF_SEARCH_CASE(128)
+    EF_SEARCH_CASE(256)
+    EF_SEARCH_CASE(512)
     default:
       return hipErrorInvalidValue;
   }

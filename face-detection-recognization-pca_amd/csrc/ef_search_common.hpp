@@ -1,0 +1,80 @@
+// Device helpers shared by the search kernels (ef_search.hip, ef_search_wide.hip).
+#pragma once
+
+#include "ef_internal.hpp"
+
+namespace ef {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ long long pack_key(float v, unsigned idx) {
+  if (v == 0.0f) v = 0.0f;  // canonical +0 so that -0 and +0 tie on index
+  int b = __float_as_int(v);
+  int s = b >= 0 ? b : (b ^ 0x7FFFFFFF);
+  return (long long)(((unsigned long long)(unsigned)s << 32) | (unsigned long long)idx);
+}
+__device__ __forceinline__ float key_value(long long key) {
+  const int s = (int)(key >> 32);
+  return __int_as_float(s >= 0 ? s : (s ^ 0x7FFFFFFF));
+}
+
+// LDS-DMA (global_load_lds) in inline asm: hipcc would otherwise treat the pending DMA
+// as an aliasing LDS write and put s_waitcnt vmcnt(0) before every ds_read, serialising the
+// prefetch of tile t+1 with the MFMAs of tile t.  M0 (the wave-uniform LDS destination) is
+// written and restored inside the statement; completion is waited for explicitly with
+// s_waitcnt vmcnt(0) before the barrier that publishes the tile.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {  // wave-uniform by construction
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) void*)p);
+}
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// fp64 score of gallery row `row` for probe q (L2: squared distance in difference form;
+// cosine: -q.g/(|q||g|), 0 for a zero vector — sklearn normalize semantics).
+template <int KP, int METRIC>
+__device__ __forceinline__ double score64(const float* __restrict__ q, const float* __restrict__ g, int lane) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int c = lane; c < KP; c += 64) {
+    const double qv = q[c], gv = g[c];
+    if constexpr (METRIC == EF_METRIC_L2) {
+      const double dv = qv - gv;
+      s0 = fma(dv, dv, s0);
+    } else {
+      s0 = fma(qv, gv, s0);
+      s1 = fma(qv, qv, s1);
+      s2 = fma(gv, gv, s2);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    if constexpr (METRIC != EF_METRIC_L2) {
+      s1 += __shfl_xor(s1, off);
+      s2 += __shfl_xor(s2, off);
+    }
+  }
+  if constexpr (METRIC == EF_METRIC_L2) {
+    return s0;
+  } else {
+    return (s1 > 0.0 && s2 > 0.0) ? -(s0 / (sqrt(s1) * sqrt(s2))) : 0.0;
+  }
+}
+
+// Wide search (KP in {256, 512}): probes streamed through LDS with the gallery.
+constexpr int kWideRowTile = 128;    // gallery rows per tile
+constexpr int kWideProbeTile = 128;  // probes per workgroup
+hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, const SearchPlan& pl,
+                              const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
+                              const SearchWs& ws);
+
+}  // namespace ef

@@ -15,6 +15,7 @@ EF_OK = 0
 EF_U8, EF_F32, EF_F64 = 0, 1, 2
 EF_METRIC_L2, EF_METRIC_COSINE = 0, 1
 EF_FIT_STANDARDIZE = 0x1
+EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_KERNEL_SEARCH, EF_KERNEL_PROJECT = 0, 1
 EF_KEY_NONE = (1 << 63) - 1

@@ -131,8 +131,14 @@ class Engine:
         return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
 
     # ----------------------------------------------------------------- projection
-    def set_model(self, mean, W):
-        """Resident recognition model f = (p - mean) . W, W is d x k."""
+    def set_model(self, mean, W, precision="fp32"):
+        """Resident recognition model f = (p - mean) . W, W is d x k (k <= 512).
+
+        precision="bf16" projects on bf16 MFMA (BASELINE.json config 5):
+        f = (p - round(mean)).bf16(W) - (mean - round(mean)).W, fp32 accumulation;
+        features, gallery search and arg-best stay fp32 (fp64-resolved)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         if _is_dev(W):
             import torch
             m, mp = _dev(mean, torch.float32)
@@ -145,6 +151,8 @@ class Engine:
         d, k = w.shape
         if m.shape[0] != d:
             raise ValueError("mean and W disagree on d")
+        if precision == "bf16":
+            flags |= N.EF_MODEL_BF16
         self._chk(self._lib.ef_model_set(self._h, mp, wp, d, k, flags))
         if flags:
             self.synchronize()

@@ -50,6 +50,7 @@ extern "C" {
 
 /* flags */
 #define EF_FIT_STANDARDIZE 0x1u /* StandardScaler before PCA (train-v4.py:131)                */
+#define EF_MODEL_BF16 0x2u      /* ef_model_set: project on bf16 MFMA (config 5), fp32 features */
 #define EF_MEM_DEVICE 0x100u    /* pointer args are device pointers, call is asynchronous    */
 
 /* kernels whose device time can be queried with ef_timing_get */
@@ -102,7 +103,9 @@ int ef_fit(ef_ctx* ctx, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint3
 /* --------------------------------------------------------------- projection
  * Recognition model f = (p - mean) . W  (useless/scan.py:93-96; sklearn
  * scaler.transform + pca.transform folded, scan-template-v4.py:265-266).
- * mean[d], W[d*k] float32, row-major (d rows of k).  Kept resident. */
+ * mean[d], W[d*k] float32, row-major (d rows of k), k <= 512.  Kept resident.
+ * EF_MODEL_BF16: f = (p - round(mean)).bf16(W) - (mean - round(mean)).W with
+ * fp32 accumulation (exact bf16 inputs for uint8 pixels; only W is rounded). */
 int ef_model_set(ef_ctx* ctx, const float* mean, const float* W, int64_t d, int32_t k, uint32_t flags);
 /* P[b*d] pixels (EF_U8 or EF_F32) -> F[b*k] float32. */
 int ef_project(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, float* F, uint32_t flags);

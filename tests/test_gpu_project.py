@@ -7,7 +7,8 @@ from oracle import eigenface_oracle as orc
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("d,k", [(4096, 16), (10000, 50), (16384, 128), (1000, 96), (333, 10)])
+@pytest.mark.parametrize("d,k", [(4096, 16), (10000, 50), (16384, 128), (1000, 96), (333, 10),
+                                 (4096, 200), (8192, 512)])
 @pytest.mark.parametrize("b", [1, 300])
 def test_project_u8(eng, d, k, b):
     rng = np.random.default_rng(d + k + b)
@@ -52,3 +53,60 @@ def test_recognize_fused_matches_project_then_search(eng):
     idx2, best2 = eng.search(f2, "l2")
     np.testing.assert_array_equal(idx, idx2)
     np.testing.assert_array_equal(best, best2)
+
+
+def test_recognize_fused_wide_k(eng):
+    """k = 512 (config 5 width): fused projection + wide search == planted identities."""
+    rng = np.random.default_rng(14)
+    d, k = 4096, 512
+    mu = rng.uniform(60, 200, d).astype(np.float32)
+    w = np.linalg.qr(rng.standard_normal((d, k)))[0].astype(np.float32)
+    gal = rng.integers(0, 256, (3000, d), dtype=np.uint8)
+    eng.set_model(mu, w)
+    eng.set_gallery(eng.project(gal))
+    probes = np.clip(gal[::10].astype(np.int32) + rng.integers(-3, 4, (300, d)), 0, 255).astype(np.uint8)
+    for metric in ("l2", "cosine"):
+        idx, _ = eng.recognize(probes, metric)
+        np.testing.assert_array_equal(idx, np.arange(0, 3000, 10))
+
+
+BF16_REL = 2.0 ** -8  # stated tolerance: |f_bf16 - f| <= 2^-8 * sum_px |p - round(mean)| |W| (+ fp32 term)
+
+
+@pytest.mark.parametrize("d,k,b", [(4096, 64, 300), (10000, 200, 129), (65536, 512, 256)])
+def test_project_bf16_tolerance(eng, d, k, b):
+    """Config 5 bf16 projection: uint8 pixels minus round(mean) are exact in bf16, so the
+    error is W's bf16 rounding only (unit roundoff 2^-9), bounded per feature."""
+    rng = np.random.default_rng(d + k)
+    mu = rng.uniform(60, 200, d).astype(np.float32)
+    w = (rng.standard_normal((d, k)) / np.sqrt(d)).astype(np.float32)
+    p = rng.integers(0, 256, (b, d), dtype=np.uint8)
+    eng.set_model(mu, w, precision="bf16")
+    f = eng.project(p)
+    ref = orc.project(p, mu.astype(np.float64), w.astype(np.float64))
+    a = np.abs(p.astype(np.float64) - np.rint(mu))
+    bound = BF16_REL * (a @ np.abs(w.astype(np.float64))) \
+        + 2e-6 * (np.abs(p.astype(np.float64) - mu) @ np.abs(w.astype(np.float64))) + 1e-5
+    err = np.abs(f - ref)
+    assert np.all(err <= bound)
+    # typical error is far below the bound (random-walk of the W roundings)
+    rel = np.linalg.norm(f - ref) / np.linalg.norm(ref)
+    assert rel < 4e-3, rel
+
+
+def test_recognize_bf16_agrees_with_fp32(eng):
+    """bf16 projection + fp32 search: argmin identity agreement with the fp32 path
+    (planted probes, config-5 width k=512)."""
+    rng = np.random.default_rng(21)
+    d, k, n = 16384, 512, 4000
+    mu = rng.uniform(60, 200, d).astype(np.float32)
+    w = np.linalg.qr(rng.standard_normal((d, k)))[0].astype(np.float32)
+    gal = rng.integers(0, 256, (n, d), dtype=np.uint8)
+    eng.set_model(mu, w)
+    eng.set_gallery(eng.project(gal))
+    probes = np.clip(gal[:512].astype(np.int32) + rng.integers(-8, 9, (512, d)), 0, 255).astype(np.uint8)
+    idx32, _ = eng.recognize(probes, "l2")
+    eng.set_model(mu, w, precision="bf16")
+    idx16, _ = eng.recognize(probes, "l2")
+    np.testing.assert_array_equal(idx32, np.arange(512))
+    np.testing.assert_array_equal(idx16, idx32)

@@ -25,7 +25,7 @@ def _check_l2(q, g, idx, best):
     np.testing.assert_allclose(best, d_gpu, rtol=1e-4, atol=1e-4 * np.sqrt(scale).max() * 1e-3)
 
 
-@pytest.mark.parametrize("k", [8, 16, 50, 64, 96, 128])
+@pytest.mark.parametrize("k", [8, 16, 50, 64, 96, 128, 200, 256, 300, 512])
 @pytest.mark.parametrize("n,b", [(1, 3), (33, 257), (3001, 300)])
 def test_l2_random(eng, k, n, b):
     rng = np.random.default_rng(k * 1000 + n)
@@ -36,7 +36,7 @@ def test_l2_random(eng, k, n, b):
     _check_l2(q, g, idx, best)
 
 
-@pytest.mark.parametrize("k", [16, 64, 128])
+@pytest.mark.parametrize("k", [16, 64, 128, 256, 512])
 def test_cosine_random(eng, k):
     rng = np.random.default_rng(k)
     g = rng.standard_normal((4000, k)).astype(np.float32)
@@ -62,9 +62,10 @@ def test_cosine_ties_and_zero_norm_golden(eng):
     np.testing.assert_allclose(sim, t["sim"], atol=1e-6)
 
 
-def test_l2_duplicates_lowest_index(eng):
+@pytest.mark.parametrize("k", [32, 512])
+def test_l2_duplicates_lowest_index(eng, k):
     rng = np.random.default_rng(5)
-    g = rng.standard_normal((1000, 32)).astype(np.float32)
+    g = rng.standard_normal((1000, k)).astype(np.float32)
     g[700] = g[5]
     g[999] = g[5]
     g[300] = g[64]
@@ -82,12 +83,13 @@ def test_empty_gallery(eng):
     assert np.all(np.isnan(best))
 
 
-def test_sharded_keys_min_equals_full(eng):
+@pytest.mark.parametrize("k", [64, 300])
+def test_sharded_keys_min_equals_full(eng, k):
     """Row sharding with global offsets + MIN over keys == unsharded search (the
     multi-GPU all-reduce contract)."""
     rng = np.random.default_rng(9)
-    g = rng.standard_normal((5000, 64)).astype(np.float32)
-    q = rng.standard_normal((700, 64)).astype(np.float32)
+    g = rng.standard_normal((5000, k)).astype(np.float32)
+    q = rng.standard_normal((700, k)).astype(np.float32)
     for metric in ("l2", "cosine"):
         eng.set_gallery(g)
         full = eng.search_keys(q, metric)
@@ -98,10 +100,11 @@ def test_sharded_keys_min_equals_full(eng):
         np.testing.assert_array_equal(np.minimum.reduce(parts), full)
 
 
-def test_planted_nearest_neighbour(eng):
+@pytest.mark.parametrize("n,k", [(200_000, 128), (100_000, 512)])
+def test_planted_nearest_neighbour(eng, n, k):
     """Probes = gallery rows + small noise: the argmin identity is exact."""
     rng = np.random.default_rng(1)
-    n, k, b = 200_000, 128, 4096
+    b = 4096
     g = (rng.standard_normal((n, k)) * orc.synth_spectrum(k)).astype(np.float32)
     t = rng.integers(0, n, b)
     q = (g[t] + rng.standard_normal((b, k)).astype(np.float32) * 2.0).astype(np.float32)
