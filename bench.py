@@ -35,6 +35,15 @@ CONFIGS = {
 }
 
 
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        info = threadpool_info()
+        return max(int(i.get("num_threads", 1)) for i in info) if info else os.cpu_count()
+    except Exception:  # pragma: no cover
+        return os.cpu_count()
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -43,11 +52,7 @@ def cpu_baseline(P, mean, W, G, targets, budget_s):
     """Oracle fp32 BLAS restatement on the host cores, bounded sample."""
     sys.path.insert(0, ROOT)
     from oracle import eigenface_oracle as orc
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max(int(i.get("num_threads", 1)) for i in threadpool_info()) if threadpool_info() else os.cpu_count()
-    except Exception:  # pragma: no cover
-        cores = os.cpu_count()
+    cores = _blas_threads()
     gn = np.einsum("ij,ij->i", G, G)
     # calibrate on 32 probes, then size the sample for ~budget_s
     t = time.perf_counter()
@@ -80,11 +85,72 @@ def pmc_traffic(config):
     return None, None
 
 
+def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu=20_000):
+    """Headline secondary metric "covariance+SVD fit sec" on config 3's shape: train-v4.py's
+    train_pca_model semantics (StandardScaler + PCA, k=128) on 1M synthetic 128x128 uint8
+    faces resident in HBM (generated on the GPU with torch: mean face + 256-component
+    spectrum + pixel noise).  GPU: ef_fit (exact int8 covariance, fp64
+    subspace eigensolve, eigenfaces) with and without the 1M x 128 training projection.
+    CPU: the solver the reference's PCA(auto) selects at this shape (scikit-learn
+    randomized PCA after StandardScaler) on an n_cpu-face sample, scaled linearly to n."""
+    import torch
+    from eigenface import synth
+    d = side * side
+    dev = torch.device("cuda", torch.cuda.current_device())
+    B = torch.from_numpy(synth.basis(d, r, 5)).to(dev, torch.float32)
+    sp = torch.from_numpy(synth.spectrum(r)).to(dev, torch.float32)
+    mu = torch.from_numpy(synth.mean_face(side)).to(dev, torch.float32)
+    X = torch.empty((n, d), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    for a in range(0, n, 32768):
+        e = min(n, a + 32768)
+        z = torch.randn((e - a, r), generator=g, device=dev) * sp
+        pix = mu + z @ B.T + 2.0 * torch.randn((e - a, d), generator=g, device=dev)
+        X[a:e] = pix.round_().clamp_(0, 255).to(torch.uint8)
+        del z, pix
+    torch.cuda.synchronize(dev)
+    eng.fit(X[:20_000], k, standardize=True, projection=False)  # warm the code paths
+    t = time.perf_counter()
+    r1 = eng.fit(X, k, standardize=True, projection=False)
+    t_fit = time.perf_counter() - t
+    t = time.perf_counter()
+    r2 = eng.fit(X, k, standardize=True, projection=True)
+    t_fit_tr = time.perf_counter() - t
+    ev = r1.eigenvalues.cpu().numpy()
+    out = {
+        "config": f"C3 fit: {n} synthetic {side}x{side} uint8 faces in HBM, k={k}, StandardScaler+PCA "
+                  "(train-v4.py:126-146), exact int8 covariance + fp64 eigensolve",
+        "gpu_fit_s": round(t_fit, 4),
+        "gpu_fit_transform_s": round(t_fit_tr, 4),
+        "eigensolver_iters": r1.iters,
+        "explained_variance_top3": [float(v) for v in ev[:3]],
+        "repeat_identical": bool(torch.equal(r1.components, r2.components)),
+    }
+    del r1, r2
+    if with_cpu:
+        xs = X[:n_cpu].cpu().numpy()
+        del X
+        torch.cuda.empty_cache()
+        try:
+            from sklearn.decomposition import PCA
+            from sklearn.preprocessing import StandardScaler
+            t = time.perf_counter()
+            z = StandardScaler().fit_transform(xs)
+            PCA(n_components=k, svd_solver="randomized", random_state=0).fit_transform(z)
+            tc = time.perf_counter() - t
+            out["cpu"] = {"kind": "reference", "impl": "scikit-learn StandardScaler + PCA(randomized)",
+                          "sample_faces": n_cpu, "sample_s": round(tc, 3),
+                          "extrapolated_s_at_n": round(tc * n / n_cpu, 2), "cores": _blas_threads()}
+        except ImportError:  # pragma: no cover
+            out["cpu"] = None
+    return out
+
+
 def fit_bench(eng, with_cpu: bool):
-    """Secondary metric "covariance+SVD fit sec": GPU ef_fit (mean, centre, Gram,
-    eigensolve, back-project, training projection; fp64) on configs[1]'s shape
-    (synthetic 10k faces 128x128, k=64) and on a 2000-face subset that the CPU oracle
-    (NumPy/LAPACK manual_pca restatement) also runs."""
+    """Fit on configs[1]'s shape (synthetic 10k faces 128x128, k=64; manual_pca semantics,
+    Gram path) and on a 2000-face subset that the CPU oracle (NumPy/LAPACK manual_pca
+    restatement) also runs."""
     from eigenface import synth
     side, k, n_full, n_sub = 128, 64, 10_000, 2000
     d = side * side
@@ -93,7 +159,7 @@ def fit_bench(eng, with_cpu: bool):
     coef = rng.standard_normal((n_full, 128)) * synth.spectrum(128)
     X = np.clip(np.rint(synth.mean_face(side) + coef @ B.T + 2.0 * rng.standard_normal((n_full, d))),
                 0, 255).astype(np.uint8)
-    out = {"config": f"synthetic faces {side}x{side}, k={k}, manual_pca semantics (Gram path, fp64)"}
+    out = {"config": f"C2 fit: synthetic faces {side}x{side}, k={k}, manual_pca semantics (Gram path)"}
     for n in (n_sub, n_full):
         eng.fit(X[:256], 16)  # warm the code paths
         t = time.perf_counter()
@@ -249,7 +315,7 @@ def main():
             "check": {"planted_match": match},
         }
         if world == 1 and not args.no_fit:
-            rec["fit"] = fit_bench(eng, not args.no_cpu)
+            rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu), "c2": fit_bench(eng, not args.no_cpu)}
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
         else:

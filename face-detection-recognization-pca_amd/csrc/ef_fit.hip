@@ -4,10 +4,13 @@
 // Restates manual_pca (useless/train.py:56-128) and, with EF_FIT_STANDARDIZE, the
 // StandardScaler + PCA(svd_solver='full') fit of train-v4.py:126-146:
 //   * covariance: Gram A.A^T/(n-1) when n < d (useless/train.py:82-85), else the d x d
-//     A^T.A/(n-1) (np.cov branch, :97-99), formed by the f64 MFMA GEMM with the centring
-//     (and 1/scale) applied in the operand loads;
-//   * eigensolve: orders <= kJacobiMax go straight to the LDS Jacobi kernel; larger ones
-//     run block subspace iteration (Y = C.Q; G = Y^T.Y; G = W.L.W^T by Jacobi in LDS;
+//     A^T.A/(n-1) (np.cov branch, :97-99).  Exact integer products on the int8 matrix
+//     cores (ef_cov_i8.hip) whenever the StandardScaler weights commute with them
+//     (covariance path, and the Gram path without scaling); the standardised Gram runs
+//     the f64 MFMA GEMM with centring and 1/scale applied in the operand loads;
+//   * eigensolve: orders <= kJacobiMax go straight to the LDS Jacobi kernel, k > 80 on
+//     orders <= 1024 to the grid-parallel Jacobi (ef_jacobi_big.hip); larger problems
+//     run block subspace iteration (Y = C.Q; G = Y^T.Y; G = W.L.W^T by Jacobi;
 //     Q = Y.W.L^-1/2) to convergence, then a Rayleigh-Ritz step (T = Q^T.C.Q, Jacobi)
 //     — the top-k pairs are all manual_pca keeps (:114-116) and all sklearn reports
 //     (explained_variance_ratio_ uses trace(C) as the total, _pca.py:644-646);
@@ -25,6 +28,14 @@ struct Bufs {
   std::vector<DevBuf> v;
   ~Bufs() {
     for (auto& b : v) release(b);
+  }
+  template <class T>
+  void drop(hipStream_t s, T* p) {  // release one buffer early (after the stream drains)
+    for (auto& b : v)
+      if (b.p == static_cast<void*>(p)) {
+        (void)hipStreamSynchronize(s);
+        release(b);
+      }
   }
   template <class T>
   int get(ef_ctx* c, size_t count, T** out) {
@@ -48,33 +59,72 @@ struct Bufs {
 
 constexpr int kMaxSweeps = 60;
 constexpr int kMaxIters = 500;
+constexpr int kDirectMax = 1024;                 // direct grid-Jacobi up to this order
 constexpr size_t kWorkElems = size_t(1) << 24;  // split-K slab budget (128 MiB)
+
+// Small symmetric eigenproblem G (m x m) -> descending eigenvalues + eigenvectors:
+// the LDS Jacobi up to kJacobiMax, the grid-parallel Jacobi beyond.
+struct SmallEig {
+  int m = 0;
+  int* info = nullptr;
+  double* jwork = nullptr;
+  int init(ef_ctx* c, Bufs& B, int m_) {
+    m = m_;
+    EF_TRY(B.get(c, 4, &info));
+    if (m > kJacobiMax) EF_TRY(B.get(c, jacobi_big_work_elems(m), &jwork));
+    return EF_OK;
+  }
+  int solve(ef_ctx* c, const double* G, int64_t ldg, double* lam, double* V, int64_t ldv, const char* what) {
+    hipStream_t s = c->stream;
+    if (m <= kJacobiMax) {
+      EF_HIP(c, launch_jacobi(s, G, m, ldg, lam, V, ldv, kMaxSweeps, info), what);
+      int hinfo = 0;
+      EF_HIP(c, hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
+      EF_HIP(c, hipStreamSynchronize(s), "sync");
+      if (hinfo < 0) return set_err(c, EF_E_NUMERIC, std::string(what) + ": Jacobi did not converge");
+      return EF_OK;
+    }
+    hipError_t e = hipSuccess;
+    const int rc = jacobi_big(s, G, m, ldg, lam, V, ldv, kMaxSweeps, jwork, info, nullptr, &e);
+    if (rc < 0) return hip_err(c, e, what);
+    if (rc > 0) return set_err(c, EF_E_NUMERIC, std::string(what) + ": Jacobi did not converge");
+    return EF_OK;
+  }
+};
 
 // Top-kk eigenpairs of the symmetric dim x dim matrix C (device, ld = dim).
 // U_out: dim x kk (row-major, ld kk), lam_out: kk (device).  iters: host.
 int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* work, double* U_out,
              double* lam_out, int* iters) {
   hipStream_t s = c->stream;
-  int* info = nullptr;
-  EF_TRY(B.get(c, 4, &info));
-  int hinfo = 0;
-  if (dim <= kJacobiMax) {
+  if (dim <= kJacobiMax || (kk > kJacobiMax - 8 && dim <= kDirectMax)) {  // direct
+    SmallEig se;
+    EF_TRY(se.init(c, B, (int)dim));
     double *ev, *V;
     EF_TRY(B.get(c, (size_t)dim, &ev));
     EF_TRY(B.get(c, (size_t)dim * dim, &V));
-    EF_HIP(c, launch_jacobi(s, C, (int)dim, dim, ev, V, dim, kMaxSweeps, info), "jacobi");
-    EF_HIP(c, hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
+    EF_TRY(se.solve(c, C, dim, ev, V, dim, "eigensolve"));
     EF_HIP(c, hipMemcpy2DAsync(U_out, kk * sizeof(double), V, dim * sizeof(double), kk * sizeof(double), dim,
                                hipMemcpyDeviceToDevice, s),
            "copy U");
     EF_HIP(c, hipMemcpyAsync(lam_out, ev, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
     EF_HIP(c, hipStreamSynchronize(s), "sync");
-    if (hinfo < 0) return set_err(c, EF_E_NUMERIC, "Jacobi eigensolver did not converge");
     *iters = 0;
     return EF_OK;
   }
 
-  const int m = kJacobiMax;  // subspace width (even)
+  // Block subspace iteration of width m: Y = C.Q; G = Y^T.Y = W.L.W^T; Q = Y.W.L^-1/2
+  // (orthonormal, Ritz-ordered); k <= 80 keeps the historical m = kJacobiMax (LDS Jacobi),
+  // wider k uses m = k + max(k/2, 16) (even, <= dim) on the grid Jacobi.
+  int m = kJacobiMax;
+  if (kk > kJacobiMax - 8) {
+    int64_t mm = kk + (kk / 2 > 16 ? kk / 2 : 16);
+    mm = (mm + 7) / 8 * 8;
+    if (mm > dim) mm = dim & ~int64_t(1);
+    m = (int)mm;
+  }
+  SmallEig se;
+  EF_TRY(se.init(c, B, m));
   double *Q, *Y, *G, *Wm, *W2, *lam;
   EF_TRY(B.get(c, (size_t)dim * m, &Q));
   EF_TRY(B.get(c, (size_t)dim * m, &Y));
@@ -93,7 +143,7 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     EF_HIP(c, gemm64(s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
                      kWorkElems),
            "G = Y^T.Y");
-    EF_HIP(c, launch_jacobi(s, G, m, m, lam, Wm, m, kMaxSweeps, info), "jacobi(G)");
+    EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(G)"));
     EF_HIP(c, launch_scale_cols_rsqrt(s, Wm, m, m, lam, W2), "W.L^-1/2");
     EF_HIP(c, gemm64(s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
                      kWorkElems),
@@ -121,14 +171,12 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
   EF_HIP(c, gemm64(s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
                    kWorkElems),
          "T = Q^T.Y");
-  EF_HIP(c, launch_jacobi(s, G, m, m, lam, Wm, m, kMaxSweeps, info), "jacobi(T)");
+  EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(T)"));
   EF_HIP(c, gemm64(s, Operand::dense(Q, m, false), Operand::dense(Wm, m, false), dim, kk, m, 1.0, U_out, kk, work,
                    kWorkElems),
          "U = Q.V");
   EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
-  EF_HIP(c, hipMemcpyAsync(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
   EF_HIP(c, hipStreamSynchronize(s), "sync");
-  if (hinfo < 0) return set_err(c, EF_E_NUMERIC, "Jacobi (Rayleigh-Ritz) did not converge");
   *iters = it;
   return EF_OK;
 }
@@ -148,8 +196,6 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   const bool gram = n < d;
   const int64_t dim = gram ? n : d;
   const int kk = (int)(k < dim ? k : dim);
-  if (dim > kJacobiMax && kk > kJacobiMax - 8)
-    return set_err(c, EF_E_INVALID, "ef_fit: k too large for the LDS subspace eigensolver (max 80)");
 
   Bufs B;
   const uint8_t* Xd = X;
@@ -182,9 +228,25 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
   const double* wp = stdz ? w : nullptr;
 
-  // K2+K3: covariance with the centring fused into the operand loads
+  // K2+K3: covariance.  Exact integer product on the int8 matrix cores whenever the
+  // pixel scaling commutes with it (covariance path; Gram path without StandardScaler),
+  // else the fp64 GEMM with the centring/scaling fused into the operand loads.
   const double inv = 1.0 / (double)(n - 1);
-  if (gram)
+  const bool int8_path = !gram || !stdz;
+  if (int8_path) {
+    const int64_t kpad = cov_i8_kpad(gram ? d : n);
+    uint8_t* At;
+    long long *S64, *cvec, *R;
+    unsigned long long* Q2;
+    EF_TRY(B.get(c, (size_t)dim * kpad, &At));
+    EF_TRY(B.get(c, (size_t)dim * dim, &S64));
+    EF_TRY(B.get(c, (size_t)d, &cvec));
+    EF_TRY(B.get(c, (size_t)(gram ? n : 1), &R));
+    EF_TRY(B.get(c, 2, &Q2));
+    EF_HIP(c, launch_cov_i8(s, Xd, n, d, gram, S1, stdz ? w : nullptr, At, S64, cvec, R, Q2, C), "covariance (int8)");
+    B.drop(s, At);
+    B.drop(s, S64);
+  } else if (gram)
     EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::pixels(Xd, d, true, mean, wp), n, n, d,
                      inv, C, n, work, kWorkElems),
            "Gram");

@@ -69,6 +69,17 @@ hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, 
 size_t jacobi_lds_bytes(int m);
 hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,
                          int64_t ldv, int max_sweeps, int* info);
+// Grid-parallel Jacobi for any order (ef_jacobi_big.hip).  work: jacobi_big_work_elems(m)
+// doubles; returns 0 converged, 1 not converged, -1 HIP error (*err).
+size_t jacobi_big_work_elems(int m);
+int jacobi_big(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs, int64_t ldv,
+               int max_sweeps, double* work, int* flag_dev, int* sweeps_out, hipError_t* err);
+// Exact integer covariance / Gram on int8 MFMA (ef_cov_i8.hip).  At: dim x cov_i8_kpad(K)
+// bytes, S64: dim*dim int64, cvec: d int64, R: n int64 (Gram), Q2: 2 uint64 (Gram).
+int64_t cov_i8_kpad(int64_t K);
+hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
+                         const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
+                         long long* cvec, long long* R, unsigned long long* Q2, double* C);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,

@@ -107,27 +107,45 @@ class Engine:
 
     # ------------------------------------------------------------------------ fit
     def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
-        """GPU eigenfaces fit of uint8 faces X (n x d); see include/eigenface.h ef_fit."""
-        x, xp = _host(X, np.uint8)
+        """GPU eigenfaces fit of uint8 faces X (n x d); see include/eigenface.h ef_fit.
+
+        X may be a host array or a device (torch uint8) tensor; for a device X the
+        outputs stay on the device (float64 torch tensors, EF_MEM_DEVICE)."""
+        dev = _is_dev(X)
+        if dev:
+            import torch
+            x, xp = _dev(X, torch.uint8)
+        else:
+            x, xp = _host(X, np.uint8)
         if x.ndim != 2:
             raise ValueError("X must be 2-D (n_samples, n_pixels)")
-        n, d = x.shape
+        n, d = (int(v) for v in x.shape)
         k = int(n_components)
         kk = min(k, n if n < d else d)
-        mean = np.empty(d)
-        var = np.empty(d)
-        scale = np.empty(d)
-        comps = np.empty((kk, d))
-        eig = np.empty(kk)
-        proj = np.empty((n, kk)) if projection else None
-        tv = np.empty(1)
+        if dev:
+            def alloc(*shape):
+                return torch.empty(shape, dtype=torch.float64, device=x.device)
+
+            def ptr(a):
+                return a.data_ptr()
+        else:
+            def alloc(*shape):
+                return np.empty(shape)
+
+            def ptr(a):
+                return a.ctypes.data
+        mean, var, scale = alloc(d), alloc(d), alloc(d)
+        comps, eig = alloc(kk, d), alloc(kk)
+        proj = alloc(n, kk) if projection else None
+        tv = alloc(1)
         k_out = C.c_int32(0)
         it = C.c_int32(0)
-        flags = N.EF_FIT_STANDARDIZE if standardize else 0
+        flags = (N.EF_FIT_STANDARDIZE if standardize else 0) | (N.EF_MEM_DEVICE if dev else 0)
         self._chk(self._lib.ef_fit(
-            self._h, xp, n, d, k, flags, mean.ctypes.data, var.ctypes.data, scale.ctypes.data,
-            comps.ctypes.data, eig.ctypes.data, proj.ctypes.data if proj is not None else None,
-            tv.ctypes.data, C.byref(k_out), C.byref(it)))
+            self._h, xp, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
+            ptr(proj) if proj is not None else None, ptr(tv), C.byref(k_out), C.byref(it)))
+        if dev:
+            self.synchronize()
         return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
 
     # ----------------------------------------------------------------- projection

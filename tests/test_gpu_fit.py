@@ -59,13 +59,19 @@ def test_sklearn_path_golden():
     np.testing.assert_allclose(sim, g["probe_similarity"], atol=1e-5)
 
 
-@pytest.mark.parametrize("n,d,k", [(60, 4096, 20), (87, 1000, 86), (500, 64, 10), (300, 48, 48)])
-def test_fit_shapes_vs_oracle(n, d, k):
-    """Direct-Jacobi (order <= 88), Gram and covariance (n >= d) branches."""
+@pytest.mark.parametrize("n,d,k,r", [
+    (60, 4096, 20, 32), (87, 1000, 86, 32), (500, 64, 10, 32), (300, 48, 48, 32),
+    # k > 80: direct grid-Jacobi (order <= 1024) and subspace iteration + grid Jacobi
+    (600, 4096, 128, 256), (1500, 4096, 100, 256), (3000, 1024, 130, 256),
+    # covariance path with n > 65536: the int8 product's int32 -> int64 flush
+    (70000, 256, 12, 64)])
+def test_fit_shapes_vs_oracle(n, d, k, r):
+    """Direct-Jacobi (order <= 88), Gram and covariance (n >= d) branches, exact int8
+    covariance, wide k."""
     from eigenface import manual_pca
     side = int(np.sqrt(d))
     if side * side == d:
-        x, _ = orc.synth_faces(n, side, r=min(32, d), seed=n + d)
+        x, _ = orc.synth_faces(n, side, r=min(r, d), seed=n + d)
     else:
         x = np.random.default_rng(n).integers(0, 256, (n, d), dtype=np.uint8)
     eig, mean, proj, lam = manual_pca(x, k)
@@ -95,3 +101,17 @@ def test_rank_deficient_duplicates():
     o_eig, _, _, o_lam = orc.manual_pca(x, 20)
     assert np.all(np.isfinite(eig)) and np.all(np.isfinite(proj))
     np.testing.assert_allclose(lam, o_lam, rtol=1e-8)
+
+
+def test_standardized_covariance_path_vs_oracle():
+    """StandardScaler + PCA with n >= d: the int8 covariance scaled by 1/scale_i 1/scale_j
+    (train-v4.py:131-134) vs the oracle's sklearn 'full' restatement."""
+    from eigenface import EigenfacePCA
+    x, _ = orc.synth_faces(3000, 16, r=64, seed=11)
+    x[:, 0] = 7  # a constant pixel: StandardScaler scale 1
+    m = EigenfacePCA(12, standardize=True).fit(x)
+    o = orc.train_pca_model(x, 12)
+    np.testing.assert_allclose(m.explained_variance_, o["pca"]["explained_variance_"], rtol=1e-9)
+    np.testing.assert_allclose(m.components_, o["pca"]["components_"], atol=1e-8)
+    np.testing.assert_allclose(m.face_features_, o["face_features"], rtol=1e-6,
+                               atol=1e-7 * np.abs(o["face_features"]).max())
