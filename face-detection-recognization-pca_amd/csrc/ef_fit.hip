@@ -68,10 +68,14 @@ struct SmallEig {
   int m = 0;
   int* info = nullptr;
   double* jwork = nullptr;
+  JacobiBig big;
   int init(ef_ctx* c, Bufs& B, int m_) {
     m = m_;
     EF_TRY(B.get(c, 4, &info));
-    if (m > kJacobiMax) EF_TRY(B.get(c, jacobi_big_work_elems(m), &jwork));
+    if (m > kJacobiMax) {
+      EF_TRY(B.get(c, jacobi_big_work_elems(m), &jwork));
+      EF_HIP(c, big.init(m, jwork, info, c->own_stream), "jacobi graph");
+    }
     return EF_OK;
   }
   int solve(ef_ctx* c, const double* G, int64_t ldg, double* lam, double* V, int64_t ldv, const char* what) {
@@ -85,7 +89,7 @@ struct SmallEig {
       return EF_OK;
     }
     hipError_t e = hipSuccess;
-    const int rc = jacobi_big(s, G, m, ldg, lam, V, ldv, kMaxSweeps, jwork, info, nullptr, &e);
+    const int rc = big.solve(s, G, ldg, lam, V, ldv, kMaxSweeps, nullptr, &e);
     if (rc < 0) return hip_err(c, e, what);
     if (rc > 0) return set_err(c, EF_E_NUMERIC, std::string(what) + ": Jacobi did not converge");
     return EF_OK;
@@ -115,10 +119,10 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
 
   // Block subspace iteration of width m: Y = C.Q; G = Y^T.Y = W.L.W^T; Q = Y.W.L^-1/2
   // (orthonormal, Ritz-ordered); k <= 80 keeps the historical m = kJacobiMax (LDS Jacobi),
-  // wider k uses m = k + max(k/2, 16) (even, <= dim) on the grid Jacobi.
+  // wider k uses m = 2k (even, <= dim) on the grid Jacobi.
   int m = kJacobiMax;
   if (kk > kJacobiMax - 8) {
-    int64_t mm = kk + (kk / 2 > 16 ? kk / 2 : 16);
+    int64_t mm = 2 * (int64_t)kk;  // Ritz values converge as (lambda_{m+1} / lambda_k)^2
     mm = (mm + 7) / 8 * 8;
     if (mm > dim) mm = dim & ~int64_t(1);
     m = (int)mm;

@@ -79,7 +79,9 @@ __global__ __launch_bounds__(256) void jbig_round_kernel(const double* __restric
     if (t == u && a.on) {
       z01 = 0.0;
       z10 = 0.0;
-      *flag = 1;
+      // quadratic convergence: once every rotation of a sweep has |tan| <= 1e-9 the
+      // next sweep's would be ~1e-18 (below fp64 resolution), so such a sweep ends it
+      if (fabs(a.s) > 1e-9 * a.c) *flag = 1;
     }
     Gout[(int64_t)a.p * mp + b.p] = z00;
     Gout[(int64_t)a.p * mp + b.q] = z01;
@@ -122,32 +124,59 @@ size_t jacobi_big_work_elems(int m) {
   return (size_t)(3 * mp * mp) + 64;
 }
 
-int jacobi_big(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs, int64_t ldv,
-               int max_sweeps, double* work, int* flag_dev, int* sweeps_out, hipError_t* err) {
-  const int mp = m + (m & 1);
-  double* G0 = work;
-  double* G1 = G0 + (int64_t)mp * mp;
-  double* V = G1 + (int64_t)mp * mp;
-  const int64_t tot = (int64_t)mp * mp;
-  hipLaunchKernelGGL(jbig_init_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G0, V);
+// One sweep (mp - 1 rounds) per graph; two graphs for the two ping-pong parities.
+void JacobiBig::destroy() {
+  for (auto& g : exec)
+    if (g) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
+  exec[0] = exec[1] = nullptr;
+}
+
+hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t capture) {
+  destroy();
+  m = m_;
+  mp = m + (m & 1);
+  work = work_;
+  flag = flag_;
+  double* G[2] = {work, work + (int64_t)mp * mp};
+  double* V = work + 2 * (int64_t)mp * mp;
   const int np = mp / 2;
   const int64_t threads = (int64_t)np * np + (int64_t)mp * np;
   const dim3 grid((unsigned)((threads + 255) / 256));
-  double* cur = G0;
-  double* nxt = G1;
-  int sweep = 0;
+  for (int par = 0; par < 2; ++par) {
+    hipError_t e = hipStreamBeginCapture(capture, hipStreamCaptureModeRelaxed);
+    if (e != hipSuccess) return e;
+    (void)hipMemsetAsync(flag, 0, sizeof(int), capture);
+    int cur = par;
+    for (int r = 0; r < mp - 1; ++r) {
+      hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, capture, G[cur], G[cur ^ 1], V, mp, r, flag);
+      cur ^= 1;
+    }
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(capture, &g);
+    if (e != hipSuccess) return e;
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return e;
+    exec[par] = x;
+  }
+  return hipSuccess;
+}
+
+int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv,
+                     int max_sweeps, int* sweeps_out, hipError_t* err) {
+  double* G[2] = {work, work + (int64_t)mp * mp};
+  double* V = work + 2 * (int64_t)mp * mp;
+  const int64_t tot = (int64_t)mp * mp;
+  hipLaunchKernelGGL(jbig_init_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G[0], V);
+  int cur = 0, sweep = 0;
   bool converged = false;
   for (; sweep < max_sweeps; ++sweep) {
-    *err = hipMemsetAsync(flag_dev, 0, sizeof(int), s);
+    *err = hipGraphLaunch(static_cast<hipGraphExec_t>(exec[cur]), s);
     if (*err != hipSuccess) return -1;
-    for (int r = 0; r < mp - 1; ++r) {
-      hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, s, cur, nxt, V, mp, r, flag_dev);
-      double* x = cur;
-      cur = nxt;
-      nxt = x;
-    }
+    cur ^= (mp - 1) & 1;  // an odd number of rounds swaps the buffers
     int hflag = 0;
-    *err = hipMemcpyAsync(&hflag, flag_dev, sizeof(int), hipMemcpyDeviceToHost, s);
+    *err = hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
     if (*err == hipSuccess) *err = hipStreamSynchronize(s);
     if (*err != hipSuccess) return -1;
     if (hflag == 0) {
@@ -155,7 +184,7 @@ int jacobi_big(hipStream_t s, const double* A, int m, int64_t lda, double* evals
       break;
     }
   }
-  hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, cur, V, m, mp, evals, evecs, ldv);
+  hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, G[cur], V, m, mp, evals, evecs, ldv);
   *err = hipGetLastError();
   if (*err != hipSuccess) return -1;
   if (sweeps_out) *sweeps_out = sweep + 1;

@@ -69,11 +69,21 @@ hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, 
 size_t jacobi_lds_bytes(int m);
 hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,
                          int64_t ldv, int max_sweeps, int* info);
-// Grid-parallel Jacobi for any order (ef_jacobi_big.hip).  work: jacobi_big_work_elems(m)
-// doubles; returns 0 converged, 1 not converged, -1 HIP error (*err).
+// Grid-parallel Jacobi for any order (ef_jacobi_big.hip): one hipGraph per sweep, built
+// once per (order, workspace).  work: jacobi_big_work_elems(m) doubles.  solve returns 0
+// converged, 1 not converged, -1 HIP error (*err).
 size_t jacobi_big_work_elems(int m);
-int jacobi_big(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs, int64_t ldv,
-               int max_sweeps, double* work, int* flag_dev, int* sweeps_out, hipError_t* err);
+struct JacobiBig {
+  int m = 0, mp = 0;
+  double* work = nullptr;
+  int* flag = nullptr;
+  void* exec[2] = {nullptr, nullptr};
+  hipError_t init(int m, double* work, int* flag, hipStream_t capture);
+  int solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv, int max_sweeps,
+            int* sweeps_out, hipError_t* err);
+  void destroy();
+  ~JacobiBig() { destroy(); }
+};
 // Exact integer covariance / Gram on int8 MFMA (ef_cov_i8.hip).  At: dim x cov_i8_kpad(K)
 // bytes, S64: dim*dim int64, cvec: d int64, R: n int64 (Gram), Q2: 2 uint64 (Gram).
 int64_t cov_i8_kpad(int64_t K);
