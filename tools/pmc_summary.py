@@ -14,7 +14,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNEL = "search_kernel<128, 0, false>"
+KERNEL = "search_kernel<128, 0, false, 0>"
 SIMDS = 1024  # 256 CUs x 4
 XCDS = 8
 
