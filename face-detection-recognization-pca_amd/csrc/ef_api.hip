@@ -191,6 +191,7 @@ void ef_destroy(ef_ctx* c) {
                     &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
+  blas_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }

@@ -15,10 +15,21 @@
 //     — the top-k pairs are all manual_pca keeps (:114-116) and all sklearn reports
 //     (explained_variance_ratio_ uses trace(C) as the total, _pca.py:644-646);
 //   * eigenfaces: E = A^T.U (:91), unit columns (:94-95), sklearn svd_flip sign rule.
+#include <rocblas/rocblas.h>
+
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "ef_linalg.hpp"
+
+namespace ef {
+void blas_release(ef_ctx* c) {
+  if (c->blas) (void)rocblas_destroy_handle(static_cast<rocblas_handle>(c->blas));
+  c->blas = nullptr;
+}
+}  // namespace ef
 
 namespace {
 
@@ -57,6 +68,38 @@ struct Bufs {
     if (_e != hipSuccess) return hip_err(ctx, _e, what); \
   } while (0)
 
+// Plain dense fp64 products of the subspace iteration (C.Q, Y^T.Y, Y.W: no operand
+// transformation to fuse) go to rocBLAS dgemm; the pixel-operand products keep gemm64.
+// EF_FIT_GEMM=own forces gemm64 everywhere (A/B comparisons).
+hipError_t dense_gemm(ef_ctx* c, hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
+                      double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
+  static const bool own = [] {
+    const char* e = getenv("EF_FIT_GEMM");
+    return e && std::string(e) == "own";
+  }();
+  // rocBLAS for large outputs; small outputs over long K (Y^T.Y, Q^T.Y) keep gemm64's
+  // split-K (a 256 x 256 output is only 4 rocBLAS tiles)
+  const bool small_out = M * N <= (int64_t)512 * 512 && K >= 4096;
+  if (!own && !A.u8 && !B.u8 && !small_out) {
+    if (!c->blas) {
+      rocblas_handle h = nullptr;
+      if (rocblas_create_handle(&h) == rocblas_status_success) c->blas = h;
+    }
+    if (c->blas) {
+      rocblas_handle h = static_cast<rocblas_handle>(c->blas);
+      const double beta = 0.0;
+      // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
+      if (rocblas_set_stream(h, s) == rocblas_status_success &&
+          rocblas_dgemm(h, B.trans ? rocblas_operation_transpose : rocblas_operation_none,
+                        A.trans ? rocblas_operation_transpose : rocblas_operation_none, (rocblas_int)N,
+                        (rocblas_int)M, (rocblas_int)K, &alpha, B.p, (rocblas_int)B.ld, A.p, (rocblas_int)A.ld, &beta,
+                        C, (rocblas_int)ldc) == rocblas_status_success)
+        return hipGetLastError();
+    }
+  }
+  return gemm64(s, A, B, M, N, K, alpha, C, ldc, work, work_elems);
+}
+
 constexpr int kMaxSweeps = 60;
 constexpr int kMaxIters = 500;
 constexpr int kDirectMax = 1024;                 // direct grid-Jacobi up to this order
@@ -69,6 +112,7 @@ struct SmallEig {
   int* info = nullptr;
   double* jwork = nullptr;
   JacobiBig big;
+  long sweeps = 0, calls = 0;  // grid-Jacobi statistics (EF_FIT_DEBUG)
   int init(ef_ctx* c, Bufs& B, int m_) {
     m = m_;
     EF_TRY(B.get(c, 4, &info));
@@ -89,12 +133,147 @@ struct SmallEig {
       return EF_OK;
     }
     hipError_t e = hipSuccess;
-    const int rc = big.solve(s, G, ldg, lam, V, ldv, kMaxSweeps, nullptr, &e);
+    int sw = 0;
+    const int rc = big.solve(s, G, ldg, lam, V, ldv, kMaxSweeps, &sw, &e);
+    sweeps += sw;
+    ++calls;
     if (rc < 0) return hip_err(c, e, what);
     if (rc > 0) return set_err(c, EF_E_NUMERIC, std::string(what) + ": Jacobi did not converge");
     return EF_OK;
   }
 };
+
+// Y[r][:] <- Y[r][:] L^-T (forward substitution per row; used only without rocBLAS).
+__global__ void trsm_rows_kernel(double* __restrict__ Y, int64_t rows, int m, const double* __restrict__ L) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  double* y = Y + r * m;
+  for (int j = 0; j < m; ++j) {
+    double v = y[j];
+    for (int l = 0; l < j; ++l) v -= y[l] * L[(int64_t)j * m + l];
+    y[j] = v / L[(int64_t)j * m + j];
+  }
+}
+
+// Q <- Y L^-T in place (row-major Y: dim x m; L row-major lower m x m).
+hipError_t tri_solve_right(ef_ctx* c, hipStream_t s, double* Y, int64_t dim, int m, const double* L) {
+  if (c->blas) {
+    rocblas_handle h = static_cast<rocblas_handle>(c->blas);
+    const double one = 1.0;
+    // column-major view: Y^T (m x dim); L row-major lower == column-major upper L^T
+    if (rocblas_set_stream(h, s) == rocblas_status_success &&
+        rocblas_dtrsm(h, rocblas_side_left, rocblas_fill_upper, rocblas_operation_transpose,
+                      rocblas_diagonal_non_unit, (rocblas_int)m, (rocblas_int)dim, &one, L, (rocblas_int)m, Y,
+                      (rocblas_int)m) == rocblas_status_success)
+      return hipGetLastError();
+  }
+  hipLaunchKernelGGL(trsm_rows_kernel, dim3((unsigned)((dim + 255) / 256)), dim3(256), 0, s, Y, dim, m, L);
+  return hipGetLastError();
+}
+
+// Wide-block subspace iteration (m > kJacobiMax): orthonormalise by CholQR every
+// iteration (G = Y^T.Y = L.L^T, Q = Y.L^-T — one small Cholesky instead of an m x m
+// eigensolve), Rayleigh-Ritz (H = Q^T.C.Q, grid Jacobi) at iterations 1, 2, 4 and every
+// kRRPeriod after: its Ritz values give the convergence test, its vectors re-order the
+// block (Y <- Y.V), and the converged RR is the final one.  A numerically rank-deficient
+// block (Cholesky pivot <= 1e-13 of the largest) falls back to the eigen-orthonormalisation
+// Q = Y.W.L^-1/2 for that iteration.
+constexpr int kRRPeriod = 8;
+constexpr int kCholeskyMax = 512;  // launch_cholesky's LDS panel limit (wider: eigen-orthonormalise)
+
+int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int m, double* work, double* U_out,
+                  double* lam_out, int* iters) {
+  hipStream_t s = c->stream;
+  SmallEig se;
+  EF_TRY(se.init(c, B, m));
+  double *Q, *Y, *Y2, *G, *V, *W2, *lam;
+  int* cinfo;
+  EF_TRY(B.get(c, (size_t)dim * m, &Q));
+  EF_TRY(B.get(c, (size_t)dim * m, &Y));
+  EF_TRY(B.get(c, (size_t)dim * m, &Y2));
+  EF_TRY(B.get(c, (size_t)m * m, &G));
+  EF_TRY(B.get(c, (size_t)m * m, &V));
+  EF_TRY(B.get(c, (size_t)m * m, &W2));
+  EF_TRY(B.get(c, (size_t)m, &lam));
+  EF_TRY(B.get(c, 4, &cinfo));
+  EF_HIP(c, launch_rand_init(s, Y, dim * m, 0x5eedULL), "rand init");
+
+  // Q <- orthonormal basis of span(Y) (Y is overwritten)
+  auto orthonormalise = [&]() -> int {
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+                         kWorkElems),
+           "G = Y^T.Y");
+    int hinfo = -1;
+    if (m <= kCholeskyMax) {
+      EF_HIP(c, launch_cholesky(s, G, m, m, 1e-13, cinfo), "cholesky");
+      EF_HIP(c, hipMemcpyAsync(&hinfo, cinfo, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
+      EF_HIP(c, hipStreamSynchronize(s), "sync");
+    }
+    if (hinfo == 0) {
+      EF_HIP(c, tri_solve_right(c, s, Y, dim, m, G), "Q = Y.L^-T");
+      std::swap(Q, Y);
+      return EF_OK;
+    }
+    // rank-deficient block: eigen-orthonormalisation with a floored spectrum
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+                         kWorkElems),
+           "G = Y^T.Y");
+    EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(G)"));
+    EF_HIP(c, launch_scale_cols_rsqrt(s, V, m, m, lam, W2), "W.L^-1/2");
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
+                         kWorkElems),
+           "Q = Y.W");
+    return EF_OK;
+  };
+  EF_TRY(orthonormalise());
+
+  std::vector<double> th(m), prev(m, 0.0);
+  bool have_prev = false;
+  int it = 0;
+  for (it = 1; it <= kMaxIters; ++it) {
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
+                         work, kWorkElems),
+           "Y = C.Q");
+    // Rayleigh-Ritz at iterations 1, 2, 4, then every kRRPeriod
+    const bool rr = it <= 2 || it == 4 || it % kRRPeriod == 0 || it == kMaxIters;
+    if (rr) {
+      EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
+                           work, kWorkElems),
+             "H = Q^T.C.Q");
+      EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(H)"));
+      EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
+      EF_HIP(c, hipStreamSynchronize(s), "sync");
+      if (!std::isfinite(th[0])) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
+      // converged when every kept Ritz value moved by <= 1e-13 relative (floor 1e-15 of
+      // the largest) since the previous Rayleigh-Ritz step
+      bool ok = have_prev;
+      for (int i = 0; i < kk && ok; ++i)
+        ok = std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * std::fabs(th[i]), 1e-15 * std::fabs(th[0]));
+      prev = th;
+      have_prev = true;
+      if (ok || it == kMaxIters) {
+        EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
+                             kk, work, kWorkElems),
+               "U = Q.V");
+        EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
+        EF_HIP(c, hipStreamSynchronize(s), "sync");
+        break;
+      }
+      // continue from the Ritz basis: C.(Q.V) = Y.V
+      EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(V, m, false), dim, m, m, 1.0, Y2, m,
+                           work, kWorkElems),
+             "Y.V");
+      std::swap(Y, Y2);
+    }
+    EF_TRY(orthonormalise());
+  }
+  if (it > kMaxIters) it = kMaxIters;
+  if (getenv("EF_FIT_DEBUG"))
+    fprintf(stderr, "[ef_fit] wide dim=%lld k=%d m=%d iters=%d jacobi calls=%ld sweeps=%ld\n", (long long)dim, kk, m,
+            it, se.calls, se.sweeps);
+  *iters = it;
+  return EF_OK;
+}
 
 // Top-kk eigenpairs of the symmetric dim x dim matrix C (device, ld = dim).
 // U_out: dim x kk (row-major, ld kk), lam_out: kk (device).  iters: host.
@@ -127,6 +306,7 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     if (mm > dim) mm = dim & ~int64_t(1);
     m = (int)mm;
   }
+  if (m > kJacobiMax) return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
   SmallEig se;
   EF_TRY(se.init(c, B, m));
   double *Q, *Y, *G, *Wm, *W2, *lam;
@@ -141,15 +321,15 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
   std::vector<double> th(m), prev(m, 0.0);
   int stable = 0, it = 0;
   for (it = 1; it <= kMaxIters; ++it) {
-    EF_HIP(c, gemm64(s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
                      work, kWorkElems),
            "Y = C.Q");
-    EF_HIP(c, gemm64(s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
                      kWorkElems),
            "G = Y^T.Y");
     EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(G)"));
     EF_HIP(c, launch_scale_cols_rsqrt(s, Wm, m, m, lam, W2), "W.L^-1/2");
-    EF_HIP(c, gemm64(s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
+    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
                      kWorkElems),
            "Q = Y.W");
     EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
@@ -168,15 +348,18 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     }
   }
   if (it > kMaxIters) it = kMaxIters;
+  if (getenv("EF_FIT_DEBUG"))
+    fprintf(stderr, "[ef_fit] dim=%lld k=%d m=%d iters=%d jacobi calls=%ld sweeps=%ld\n", (long long)dim, kk, m, it,
+            se.calls, se.sweeps);
   // Rayleigh-Ritz on C itself: T = Q^T.C.Q, T = V.L.V^T, U = Q.V[:, :kk]
-  EF_HIP(c, gemm64(s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
+  EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
                    kWorkElems),
          "Y = C.Q");
-  EF_HIP(c, gemm64(s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
+  EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
                    kWorkElems),
          "T = Q^T.Y");
   EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(T)"));
-  EF_HIP(c, gemm64(s, Operand::dense(Q, m, false), Operand::dense(Wm, m, false), dim, kk, m, 1.0, U_out, kk, work,
+  EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(Wm, m, false), dim, kk, m, 1.0, U_out, kk, work,
                    kWorkElems),
          "U = Q.V");
   EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");

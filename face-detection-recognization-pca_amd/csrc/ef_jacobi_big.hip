@@ -8,7 +8,8 @@
 //   * the rotation of each pair is recomputed by every thread that needs it from the
 //     round's input matrix, which is therefore ping-ponged (in-place would race on the
 //     pivots); V <- V J is in place (thread (i, u) owns V[i][p_u], V[i][q_u]);
-//   * a sweep with no rotation ends the solve (one host read of a flag per sweep).
+//   * a sweep whose pivots are all below 1e-12 of their diagonal scale ends the solve
+//     (one host read of a flag per sweep).
 // Used for the Rayleigh-Ritz / orthonormalisation problems of the subspace iteration at
 // k > 80 (BASELINE.json config 3: k = 128; config 5: k = 512) and for direct solves of
 // moderate orders.  Quadratic convergence: a nearly diagonal input (warm subspace) needs
@@ -79,9 +80,10 @@ __global__ __launch_bounds__(256) void jbig_round_kernel(const double* __restric
     if (t == u && a.on) {
       z01 = 0.0;
       z10 = 0.0;
-      // quadratic convergence: once every rotation of a sweep has |tan| <= 1e-9 the
-      // next sweep's would be ~1e-18 (below fp64 resolution), so such a sweep ends it
-      if (fabs(a.s) > 1e-9 * a.c) *flag = 1;
+      // a sweep whose rotated pivots were all below 1e-12 of their diagonal scale ends
+      // the solve: the matrix is then diagonal to ~1e-12 relative (near-degenerate pairs
+      // may still rotate by large angles without extending the sweep count)
+      if (fabs(x01) > 1e-12 * sqrt(fabs(x00 * x11))) *flag = 1;
     }
     Gout[(int64_t)a.p * mp + b.p] = z00;
     Gout[(int64_t)a.p * mp + b.q] = z01;

@@ -332,6 +332,102 @@ hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, dou
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------ Cholesky (one workgroup)
+// In-place lower Cholesky of the symmetric positive definite m x m matrix A (row-major,
+// lda): A[i][j] (j <= i) <- L, upper triangle zeroed.  A pivot <= tol_rel * max diagonal
+// stops with *info = -(j+1) (numerically rank-deficient block: the caller falls back to
+// the Jacobi orthonormalisation); *info = 0 on success.  Used by the CholQR
+// orthonormalisation of the subspace iteration (m <= 1024, L2-resident).
+// Right-looking, 32-column panels: the panel (rows jb.., 32 columns) is factored in LDS
+// with LDS-only barriers, then the trailing lower triangle takes one rank-32 update.
+constexpr int kCholNB = 32;
+constexpr int kCholPS = kCholNB + 1;  // LDS panel row stride (odd: rows spread over banks)
+constexpr int kCholMaxM = 512;        // panel rows held in LDS: 512 x 33 doubles = 132 KiB
+
+__global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int m, int64_t lda, double tol_rel,
+                                                    int* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) double P[];  // [m - jb][kCholPS]
+  __shared__ double red[1024];
+  __shared__ double piv;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  double mx = 0.0;
+  for (int i = tid; i < m; i += nth) mx = fmax(mx, A[(int64_t)i * lda + i]);
+  red[tid] = mx;
+  __syncthreads();
+  for (int o = nth / 2; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmax(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  const double tol = tol_rel * red[0];
+  for (int jb = 0; jb < m; jb += kCholNB) {
+    const int nb = m - jb < kCholNB ? m - jb : kCholNB;
+    const int rows = m - jb;
+    for (int e = tid; e < rows * kCholNB; e += nth) {  // load the panel
+      const int i = e / kCholNB, t = e % kCholNB;
+      P[i * kCholPS + t] = t < nb ? A[(int64_t)(jb + i) * lda + jb + t] : 0.0;
+    }
+    __syncthreads();
+    for (int t = 0; t < nb; ++t) {  // unblocked factorisation of the panel
+      if (tid == 0) {
+        const double dj = P[t * kCholPS + t];
+        piv = (dj > tol) ? sqrt(dj) : -1.0;
+        if (piv > 0.0) P[t * kCholPS + t] = piv;
+      }
+      __syncthreads();
+      const double p = piv;
+      if (p < 0.0) {
+        if (tid == 0) *info = -(jb + t + 1);
+        return;
+      }
+      for (int i = t + 1 + tid; i < rows; i += nth) P[i * kCholPS + t] /= p;
+      __syncthreads();
+      const int w = nb - t - 1;  // update the panel's remaining columns
+      for (int e = tid; e < (rows - t - 1) * w; e += nth) {
+        const int i = t + 1 + e / w, l = t + 1 + e % w;
+        if (l <= i) P[i * kCholPS + l] -= P[i * kCholPS + t] * P[l * kCholPS + t];
+      }
+      __syncthreads();
+    }
+    for (int e = tid; e < rows * kCholNB; e += nth) {  // store the panel
+      const int i = e / kCholNB, t = e % kCholNB;
+      if (t < nb && t <= i) A[(int64_t)(jb + i) * lda + jb + t] = P[i * kCholPS + t];
+    }
+    // trailing lower triangle: A[i][l] -= P[i] . P[l]  (jb + nb <= l <= i)
+    const int w = rows - nb;
+    for (int e = tid; e < w * w; e += nth) {
+      const int i = e / w, l = e % w;
+      if (l > i) continue;
+      const double* pi = P + (nb + i) * kCholPS;
+      const double* pl = P + (nb + l) * kCholPS;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int t = 0; t < kCholNB; ++t) acc = fma(pi[t], pl[t], acc);
+      A[(int64_t)(jb + nb + i) * lda + jb + nb + l] -= acc;
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < m * m; e += nth) {
+    const int i = e / m, l = e % m;
+    if (l > i) A[(int64_t)i * lda + l] = 0.0;
+  }
+  if (tid == 0) *info = 0;
+}
+
+hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info) {
+  if (m < 1 || m > kCholMaxM) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  const size_t lds = (size_t)kCholMaxM * kCholPS * sizeof(double);
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chol_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), (size_t)m * kCholPS * sizeof(double), s, A, m, lda, tol_rel,
+                     info);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ small helpers
 __global__ void trace_kernel(const double* __restrict__ C, int64_t m, int64_t ldc, double* out) {
   __shared__ double red[256];

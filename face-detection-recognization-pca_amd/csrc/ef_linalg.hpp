@@ -90,6 +90,7 @@ int64_t cov_i8_kpad(int64_t K);
 hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
                          const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
                          long long* cvec, long long* R, unsigned long long* Q2, double* C);
+hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,
