@@ -14,10 +14,12 @@
 // (train-v4.py:131) is applied afterwards as C_ij / (scale_i scale_j).
 //
 // SYRK kernel: 256 x 256 output tile per workgroup (upper triangle of tiles only), 8 waves
-// of 128 x 64, K-slices of 64 samples staged by global_load_lds into double-buffered LDS
-// (2 x 32 KiB), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the ds_read_b128 fragment
-// reads are conflict-free.  Operands come from a K-contiguous int8 copy At (dim x Kpad):
+// of 128 x 64, K-slices of 64 samples staged by global_load_lds into a 4-stage LDS ring
+// (4 x 32 KiB, three stages in flight), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the
+// ds_read_b128 fragment reads are conflict-free.  Operands come from a K-contiguous int8 copy At (dim x Kpad):
 // X' itself for the Gram path, its transpose for the covariance path.
+#include <vector>
+
 #include "ef_dma.hpp"
 #include "ef_linalg.hpp"
 
@@ -29,6 +31,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int YT = 256;                 // output tile (rows and columns)
 constexpr int YK = 64;                  // samples per stage
 constexpr int YSL = YT * YK;            // bytes per operand stage
+constexpr int YNB = 4;                  // LDS stages in the ring (prefetch distance YNB - 1)
 constexpr int64_t kFlushK = 65536;      // int32-safe accumulation length
 
 // At[r][k] = X[r][k] - 128 (Gram path: rows = samples), zero for k >= d.
@@ -58,16 +61,17 @@ __global__ void shift_transpose_kernel(const uint8_t* __restrict__ X, int64_t n,
 
 // S64[i][j] = sum_k At[i][k] At[j][k] for the upper triangle of 256-tiles (i-tile <= j-tile).
 __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim, int64_t ldk,
-                                                         int64_t kpad, int ntile, long long* __restrict__ S64) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * YSL];  // [buf][A | B]
+                                                         int64_t kpad, int ntiles, const int2* __restrict__ order,
+                                                         long long* __restrict__ S64) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[YNB * 2 * YSL];  // [stage][A | B], 128 KiB
   const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
+  // consecutive list entries run on one XCD (blocks b and b+8 share an XCD), and the
+  // host orders the list in 4 x 8 blocks of tiles, so the ~32 workgroups an XCD runs at
+  // once read 4 row panels and 8 column panels: most panel bytes hit its L2
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  const int ntiles = ntile * (ntile + 1) / 2;
   if (lin >= ntiles) return;
-  // lin -> (ti, tj), ti <= tj, row-major over the upper triangle
-  int ti = 0, rem = lin;
-  while (rem >= ntile - ti) { rem -= ntile - ti; ++ti; }
-  const int tj = ti + rem;
+  const int2 tt = order[lin];
+  const int ti = tt.x, tj = tt.y;
   const int64_t i0 = (int64_t)ti * YT, j0 = (int64_t)tj * YT;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -118,12 +122,19 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
 
   const int sw = (c32 >> 2) & 3;  // swizzle key of every row this lane reads
   const int64_t nst = kpad / YK;
-  issue(0, 0);
-  dma_wait_all();
-  __syncthreads();
+  // ring of YNB stages, YNB - 1 in flight ahead of the one being consumed (an HBM miss is
+  // several stages of MFMA time); each stage is 4 DMA instructions per wave, so "stage st
+  // landed" is vmcnt <= 4 x (stages issued after it).  Tail stages past nst are issued as
+  // harmless re-reads of stage 0 so the count stays uniform.
+  for (int j = 0; j < YNB - 1; ++j) issue((j < nst ? j : 0) * YK, j);
   for (int64_t st = 0; st < nst; ++st) {
-    const int buf = (int)(st & 1);
-    if (st + 1 < nst) issue((st + 1) * YK, buf ^ 1);
+    const int buf = (int)(st % YNB);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage st landed (2 newer stages pending)
+    __syncthreads();                                   // ... for every wave; stage st-1 consumed
+    {
+      const int64_t nx = st + YNB - 1;
+      issue((nx < nst ? nx : 0) * YK, (int)(nx % YNB));
+    }
     const uint8_t* sa = smem + buf * 2 * YSL;
     const uint8_t* sb = sa + YSL;
 #pragma unroll
@@ -140,9 +151,8 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     if (((st + 1) * YK) % kFlushK == 0 && st + 1 < nst) flush();
-    dma_wait_all();
-    __syncthreads();
   }
+  dma_wait_all();
   flush();
 }
 
@@ -214,9 +224,14 @@ __global__ void cov_finalize_kernel(const long long* __restrict__ S64, int64_t d
 
 int64_t cov_i8_kpad(int64_t K) { return (K + YK - 1) / YK * YK; }
 
+int64_t cov_i8_order_bytes(int64_t dim) {
+  const int64_t t = (dim + YT - 1) / YT;
+  return t * (t + 1) / 2 * (int64_t)sizeof(int2) + 64;
+}
+
 hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
                          const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
-                         long long* cvec, long long* R, unsigned long long* Q2, double* C) {
+                         long long* cvec, long long* R, unsigned long long* Q2, void* order_dev, double* C) {
   const int64_t dim = gram ? n : d;
   const int64_t K = gram ? d : n;
   const int64_t kpad = cov_i8_kpad(K);
@@ -231,9 +246,21 @@ hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, 
   hipError_t e = hipMemsetAsync(S64, 0, (size_t)dim * dim * sizeof(long long), s);
   if (e != hipSuccess) return e;
   const int ntile = (int)((dim + YT - 1) / YT);
-  const int ntiles = ntile * (ntile + 1) / 2;
+  // upper-triangle tiles in 4 x 8 blocks (L2 reuse within an XCD), one H2D of the list
+  std::vector<int2> order;
+  for (int bi = 0; bi < ntile; bi += 4)
+    for (int bj = bi / 8 * 8; bj < ntile; bj += 8)
+      for (int ti = bi; ti < bi + 4 && ti < ntile; ++ti)
+        for (int tj = bj; tj < bj + 8 && tj < ntile; ++tj)
+          if (ti <= tj) order.push_back(make_int2(ti, tj));
+  const int ntiles = (int)order.size();
   const int grid = (ntiles + 7) / 8 * 8;
-  hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, kpad, kpad, ntile, S64);
+  e = hipMemcpyAsync(order_dev, order.data(), order.size() * sizeof(int2), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, kpad, kpad, ntiles,
+                     static_cast<const int2*>(order_dev), S64);
+  e = hipStreamSynchronize(s);  // the host list must outlive the copy
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(shifted_sums_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, n, d, cvec);
   if (gram) {
     hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)n), dim3(256), 0, s, At, n, kpad, d, cvec, R);

@@ -430,7 +430,10 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
     EF_TRY(B.get(c, (size_t)d, &cvec));
     EF_TRY(B.get(c, (size_t)(gram ? n : 1), &R));
     EF_TRY(B.get(c, 2, &Q2));
-    EF_HIP(c, launch_cov_i8(s, Xd, n, d, gram, S1, stdz ? w : nullptr, At, S64, cvec, R, Q2, C), "covariance (int8)");
+    uint8_t* order;
+    EF_TRY(B.get(c, (size_t)cov_i8_order_bytes(dim), &order));
+    EF_HIP(c, launch_cov_i8(s, Xd, n, d, gram, S1, stdz ? w : nullptr, At, S64, cvec, R, Q2, order, C),
+           "covariance (int8)");
     B.drop(s, At);
     B.drop(s, S64);
   } else if (gram)

@@ -87,9 +87,10 @@ struct JacobiBig {
 // Exact integer covariance / Gram on int8 MFMA (ef_cov_i8.hip).  At: dim x cov_i8_kpad(K)
 // bytes, S64: dim*dim int64, cvec: d int64, R: n int64 (Gram), Q2: 2 uint64 (Gram).
 int64_t cov_i8_kpad(int64_t K);
+int64_t cov_i8_order_bytes(int64_t dim);  // device scratch for the tile order list
 hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
                          const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
-                         long long* cvec, long long* R, unsigned long long* Q2, double* C);
+                         long long* cvec, long long* R, unsigned long long* Q2, void* order_dev, double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
