@@ -56,14 +56,23 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   constexpr int PPW = (NI + NW - 1) / NW;                              // pieces per wave
   constexpr int RP = 64 / CPR;                                         // rows per piece
   static_assert((NI % NW == 0 || NI < NW) && RP * CPR == 64 && TG == 64, "tile must be whole 1-KiB pieces");
+  // KP = 128 (the k = 128 headline shape): no swizzle.  LDS piece p (1 KiB + 16 B pad)
+  // holds row p of the tile's first 32-row block and row 32 + p of the second, so the
+  // lane reading row c32 of either block uses one base (c32 * 1040 B) plus immediate
+  // offsets — no per-read VALU address math, which costs MFMA issue cycles
+  // (tools/micro/mfma_valu_probe.cpp) — and the 1040-B stride (260 = 4 mod 64 banks)
+  // keeps every ds_read_b128 lane group conflict-free.  One full-wave DMA per piece.
+  constexpr bool PAD = KP == 128;
+  constexpr int PS = 2 * KP + 4;          // PAD: floats per piece (two rows + 16 B)
+  constexpr int TGS = PAD ? 32 * PS : TG * KP;  // floats per tile buffer
 
   // Unpadded [TG][KP] tiles filled by global_load_lds (lane-linear 1-KiB pieces); the
   // chunk order inside each row is XOR-swizzled by (row & (SW-1)) on the SOURCE address so
   // the A-fragment ds_read_b128s (16 lanes = 16 rows, same logical chunk) hit distinct
   // banks.  All LDS lives in one array (a second __shared__ object can de-pipeline).
-  __shared__ __attribute__((aligned(16))) float smem[2 * TG * KP + 2 * TG];
+  __shared__ __attribute__((aligned(16))) float smem[2 * TGS + 2 * TG];
   float* const sG0 = smem;
-  float* const sAux0 = smem + 2 * TG * KP;
+  float* const sAux0 = smem + 2 * TGS;
 
   // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD a contiguous run of
   // (chunk, probe-tile) pairs so the probe tiles of one chunk are co-resident on it.
@@ -106,24 +115,70 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   // Rows past n (tail tile only) are clamped to a valid row and masked in the epilogue.
   const int lcx = lc ^ (lrow & (SW - 1));
   const unsigned lds_base = lds_addr(smem);
+  // Full tiles use the SGPR-base DMA form: per piece one v_xor + one v_lshl_add (every VALU
+  // instruction in this loop costs MFMA issue time); the tail tile clamps rows instead.
   auto issue_tile = [&](int64_t t, int buf) {
-    const float* gbase = G + t * TG * KP;  // wave-uniform
     const int nrem = (int)((n - t * TG) < TG ? (n - t * TG) : TG);
+    if constexpr (PAD) {  // piece p = rows p (lanes 0-31) and 32 + p (lanes 32-63)
+      const unsigned m0 = lds_base + (unsigned)(buf * TGS * 4);
+      unsigned lid;  // re-derived in place (a loop-long VGPR would be spilled by hipcc)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+      if (nrem == TG) {
+        const unsigned long long gb = uniform_ptr(G + t * TG * KP);
+        if (wave == 0) glds4s(lid * 4u, uniform_ptr(aux + t * TG), lds_base + (unsigned)((2 * TGS + buf * TG) * 4));
+        const unsigned voff = ((lid >> 5) * 32 * KP + (lid & 31) * 4) * 4;
+#pragma unroll
+        for (int jj = 0; jj < PPW; ++jj) {
+          const int p = wave * PPW + jj;
+          glds16s(voff, gb + (unsigned long long)(p * KP * 4), m0 + (unsigned)(p * PS * 4));
+        }
+      } else {
+        const float* gbase = G + t * TG * KP;
+#pragma unroll
+        for (int jj = 0; jj < PPW; ++jj) {
+          const int p = wave * PPW + jj;
+          int row = p + (int)(lid >> 5) * 32;
+          row = row < nrem ? row : nrem - 1;
+          glds16(gbase + row * KP + (lid & 31) * 4, m0 + (unsigned)(p * PS * 4));
+        }
+        if (wave == 0) {
+          const int row = (int)lid < nrem ? (int)lid : nrem - 1;
+          glds4(aux + t * TG + row, lds_base + (unsigned)((2 * TGS + buf * TG) * 4));
+        }
+      }
+      return;
+    }
     int lx = lcx, lr = lrow;
     asm volatile("" : "+v"(lx), "+v"(lr));  // recompute per tile (no hoisted per-piece VGPRs)
+    if (nrem == TG) {
+      const unsigned long long gb = uniform_ptr(G + t * TG * KP);
+      const unsigned lro = (unsigned)(lr * KP * 4);
 #pragma unroll
-    for (int jj = 0; jj < PPW; ++jj) {
-      const int j = wave * PPW + jj;
-      if (NI >= NW || wave < NI) {  // uniform
-        const int sj = (j * RP) & (SW - 1);
-        int row = j * RP + lr;
-        if (nrem < TG) row = row < nrem ? row : nrem - 1;
-        glds16(gbase + row * KP + ((lx ^ sj) << 2), lds_base + (unsigned)((buf * TG * KP + j * 256) * 4));
+      for (int jj = 0; jj < PPW; ++jj) {
+        const int j = wave * PPW + jj;
+        if (NI >= NW || wave < NI) {  // uniform
+          const int sj = (j * RP) & (SW - 1);
+          glds16s(lro + ((unsigned)(lx ^ sj) << 4), gb + (unsigned long long)(j * RP * KP * 4),
+                  lds_base + (unsigned)((buf * TGS + j * 256) * 4));
+        }
       }
-    }
-    if (wave == 0) {
-      const int row = lane < nrem ? lane : nrem - 1;
-      glds4(aux + t * TG + row, lds_base + (unsigned)((2 * TG * KP + buf * TG) * 4));  // one 4-B piece per lane
+      if (wave == 0) glds4s((unsigned)lane * 4u, uniform_ptr(aux + t * TG), lds_base + (unsigned)((2 * TGS + buf * TG) * 4));
+    } else {
+      const float* gbase = G + t * TG * KP;  // wave-uniform
+#pragma unroll
+      for (int jj = 0; jj < PPW; ++jj) {
+        const int j = wave * PPW + jj;
+        if (NI >= NW || wave < NI) {  // uniform
+          const int sj = (j * RP) & (SW - 1);
+          int row = j * RP + lr;
+          row = row < nrem ? row : nrem - 1;
+          glds16(gbase + row * KP + ((lx ^ sj) << 2), lds_base + (unsigned)((buf * TGS + j * 256) * 4));
+        }
+      }
+      if (wave == 0) {
+        const int row = lane < nrem ? lane : nrem - 1;
+        glds4(aux + t * TG + row, lds_base + (unsigned)((2 * TGS + buf * TG) * 4));  // one 4-B piece per lane
+      }
     }
   };
 
@@ -216,21 +271,21 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   for (int64_t t = t0; t < t1; ++t) {
     const int buf = (int)((t - t0) & 1);
     if (t + 1 < t1) issue_tile(t + 1, buf ^ 1);  // lands under this tile's MFMAs
-    const float* tileG = sG0 + buf * TG * KP;
+    const float* tileG = sG0 + buf * TGS;
     const float* tileA = sAux0 + buf * TG;
     const bool tail = (t + 1) * TG > n;
     const int tbase = (int)(t * TG);
-    int swz = c32 & (SW - 1);  // rows c32 and 32 + c32 share (row & (SW-1)), SW <= 16
+    int swz = PAD ? 0 : c32 & (SW - 1);  // rows c32 and 32 + c32 share (row & (SW-1)), SW <= 16
     // opaque per tile: stops hipcc hoisting all KH/4 swizzled addresses out of the loop
-    asm volatile("" : "+v"(swz));
-    const float* arow0 = tileG + c32 * KP;
-    const float* arow1 = tileG + (32 + c32) * KP;
+    if constexpr (!PAD) asm volatile("" : "+v"(swz));
+    const float* arow0 = tileG + (PAD ? c32 * PS : c32 * KP);
+    const float* arow1 = PAD ? arow0 + KP : tileG + (32 + c32) * KP;
 
     // both 32-row blocks at once: two independent accumulator chains sharing the B operand
     f32x16 acc0 = acc_init(tileA), acc1 = acc_init(tileA + 32);
 #pragma unroll
     for (int s = 0; s < KH; s += 4) {
-      const int chunk = (h * (CPR / 2) + s / 4) ^ swz;
+      const int chunk = PAD ? h * (CPR / 2) + s / 4 : (h * (CPR / 2) + s / 4) ^ swz;
       const float4 a = *reinterpret_cast<const float4*>(arow0 + chunk * 4);
       const float4 b = *reinterpret_cast<const float4*>(arow1 + chunk * 4);
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qb[s], acc0, 0, 0, 0);
