@@ -105,3 +105,60 @@ def test_pack_keys_matches_library_decoder():
     np.testing.assert_array_equal(idx, i)
     np.testing.assert_array_equal(best, np.where(v == 0, 0.0, v).astype(np.float32))
     assert np.all(np.diff(k[[0, 2, 3, 4, 5]]) > 0)
+
+
+def _proj_worker(rank, world, port, g, P, mean, W, metric, out):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eigenface.distributed import ShardedGallery, shard_range
+    from oracle import eigenface_oracle as orc
+    lo, hi = shard_range(len(g), rank, world)
+    seen = []
+
+    def proj(p, out=None):  # records which probe rows this rank projected
+        seen.append(len(p))
+        return torch.from_numpy(orc.project(p.numpy(), mean, W).astype(np.float32))
+
+    sg = ShardedGallery(None, g[lo:hi], len(g), rank, world, local_project=proj,
+                        local_search=lambda qq, m, keys=None: _oracle_keys(qq.numpy(), g[lo:hi], lo, m))
+    keys = sg.recognize_keys(torch.from_numpy(P), metric)
+    out[rank] = (keys.numpy().copy(), sum(seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,b", [(2, 64), (3, 67), (4, 5)])
+def test_sharded_projection_allgather_matches_unsharded(world, b):
+    """world > 1: each rank projects ceil(B/world) probe rows, the features are
+    all-gathered, then the sharded search + all-reduce(MIN) equals the unsharded result."""
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import eigenface_oracle as orc
+    rng = np.random.default_rng(b)
+    d, k = 64, 12
+    W = np.linalg.qr(rng.standard_normal((d, k)))[0].astype(np.float32)
+    mean = rng.uniform(60, 200, d).astype(np.float32)
+    g = rng.standard_normal((301, k)).astype(np.float32) * 30
+    P = rng.integers(0, 256, (b, d)).astype(np.uint8)
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_proj_worker, args=(r, world, port, g, P, mean, W, "l2", out))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    q = orc.project(P, mean, W).astype(np.float32)
+    full = _oracle_keys(q, g, 0, "l2")
+    c = (b + world - 1) // world
+    for r in range(world):
+        np.testing.assert_array_equal(out[r][0], full)
+        assert out[r][1] == max(0, min(b, (r + 1) * c) - min(b, r * c))
