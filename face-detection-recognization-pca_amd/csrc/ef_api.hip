@@ -192,6 +192,7 @@ void ef_destroy(ef_ctx* c) {
                     &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
   blas_release(c);
+  tm_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }

@@ -1,0 +1,639 @@
+// Image side of the hot path.
+//
+// Ingest — train-v4.py:59-68 / scan-template-v4.py:257-263:
+//     gray = cv2.cvtColor(img, COLOR_BGR2GRAY); face = cv2.resize(gray, (64, 64))
+//   `resize_kernel` turns a ragged batch of decoded images (1 or 3 channels, any size)
+//   into uint8 rows of any output size in one launch, with OpenCV 4.x's CV_8U arithmetic:
+//   BT.601 fixed point Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14, and INTER_LINEAR as
+//   resizeGeneric_ computes it for 8U (11-bit coefficients from float32 offsets, horizontal
+//   int sums, vertical ((b0*(D0>>4))>>16) + ((b1*(D1>>4))>>16) + 2) >> 2), plus its
+//   identity copy and exact-2x INTER_AREA shortcuts.  Parity against OpenCV is unpinned
+//   (OpenCV is absent here); the restatement is oracle/image_oracle.py.
+//   Work per output pixel: 4 gathered source pixels (12 bytes for colour) + 1 byte out —
+//   an L2/HBM-bound byte kernel, no GEMM.
+//
+// Template localiser — scan-template-v4.py:127-200:
+//     cv2.matchTemplate(frame, resize(template, s), TM_CCOEFF_NORMED); cv2.minMaxLoc
+//   for every (template, scale) problem of every model, against one grey frame.
+//   The numerator is an exact integer correlation on the int8 matrix cores: with
+//   I' = I - 128 and T' = T - 128 (exact int8), N = h*w,
+//       N*sum(T I) - sum T * sum I  ==  N*sum(T' I') - sum T' * sum I'
+//   (covariance is shift-invariant), so
+//       P(y, x) = sum_{y'} sum_{x'} T'[y'][x'] I'[y+y'][x+x']
+//   runs on v_mfma_i32_32x32x32_i8 and the window sums come from exact int64 integral
+//   images.  Each template row y' contributes a Toeplitz product: for a 32-column block
+//   of outputs starting at x0, P[y][x0+c] += sum_j I'[y+y'][x0+j] * B0[j][c] with
+//   B0[j][c] = T'[y'][j-c] (0 outside [0, w)) — the frame rows are the plain A operand
+//   and the banded template (precomputed once per template, "band") is the B operand.
+//   Shift invariance of B0 means output block n uses B0's k-block kb-n at step kb, so a
+//   wave carries four output blocks (128 columns) with ONE new B fragment per step.
+//   Template rows are split in chunks of <= 128 (int32-exact: 128 * w * 2^14 < 2^31 for
+//   w <= 1024) and templates wider than 352 in column pieces; the int32 partial slabs are
+//   summed in int64 by `tm_score_kernel`, which applies OpenCV's TM_CCOEFF_NORMED
+//   normalisation rule in float64 and reduces the first raster-order maximum with one
+//   packed-key atomicMin per wave.
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ef_internal.hpp"
+
+namespace ef {
+
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+#define EF_TRY(expr)              \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != EF_OK) return _rc; \
+  } while (0)
+#define EF_HIP(ctx, expr, what)                          \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return hip_err(ctx, _e, what); \
+  } while (0)
+
+// ------------------------------------------------------------------------ ingest
+struct ImgDesc {
+  int64_t src_off;  // byte offset of the source image (rows of w * c bytes)
+  int64_t dst_off;  // byte offset of the output image (oh rows of ow bytes)
+  int h, w, c, oh, ow, pad;
+};
+
+// One axis of OpenCV's INTER_LINEAR setup (resizeGeneric_): source pair and 11-bit
+// weights.  Horizontal: borders clamp the index AND zero the fraction; vertical: only
+// the source rows clamp.  Separate roundings as in the reference (no FMA contraction).
+__device__ __forceinline__ void lin_axis(int dpos, int n_in, int n_out, bool zero_borders, int& i0, int& i1,
+                                         int& c0, int& c1) {
+  const double scale = __ddiv_rn(1.0, __ddiv_rn((double)n_out, (double)n_in));  // 1 / inv_scale
+  float f = __double2float_rn(__dadd_rn(__dmul_rn(__dadd_rn((double)dpos, 0.5), scale), -0.5));
+  int s = (int)floorf(f);
+  f = __fsub_rn(f, (float)s);
+  if (zero_borders) {
+    if (s < 0) { f = 0.f; s = 0; }
+    if (s >= n_in - 1) { f = 0.f; s = n_in - 1; }
+  }
+  c0 = __float2int_rn(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
+  c1 = __float2int_rn(__fmul_rn(f, 2048.f));
+  i0 = s < 0 ? 0 : (s > n_in - 1 ? n_in - 1 : s);
+  i1 = s + 1 < 0 ? 0 : (s + 1 > n_in - 1 ? n_in - 1 : s + 1);
+}
+
+template <bool RGB>
+__device__ __forceinline__ int gray_at(const uint8_t* __restrict__ src, int w, int c, int y, int x) {
+  const uint8_t* p = src + ((int64_t)y * w + x) * c;
+  if (c == 1) return p[0];
+  const int b = RGB ? p[2] : p[0], g = p[1], r = RGB ? p[0] : p[2];
+  return (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14;
+}
+
+// grid (ceil(max_out_pixels / 256), count); thread = one output pixel.
+template <bool RGB>
+__global__ __launch_bounds__(256) void resize_kernel(const uint8_t* __restrict__ src, const ImgDesc* __restrict__ desc,
+                                                     uint8_t* __restrict__ dst) {
+  const ImgDesc dd = desc[blockIdx.y];
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= dd.oh * dd.ow) return;
+  const int dy = o / dd.ow, dx = o - (o / dd.ow) * dd.ow;
+  const uint8_t* s = src + dd.src_off;
+  int v;
+  if (dd.oh == dd.h && dd.ow == dd.w) {  // dsize == ssize: copy
+    v = gray_at<RGB>(s, dd.w, dd.c, dy, dx);
+  } else if (dd.h == 2 * dd.oh && dd.w == 2 * dd.ow) {  // INTER_AREA fast path (exact 2x)
+    const int y = 2 * dy, x = 2 * dx;
+    v = (gray_at<RGB>(s, dd.w, dd.c, y, x) + gray_at<RGB>(s, dd.w, dd.c, y, x + 1) +
+         gray_at<RGB>(s, dd.w, dd.c, y + 1, x) + gray_at<RGB>(s, dd.w, dd.c, y + 1, x + 1) + 2) >> 2;
+  } else {
+    int x0, x1, a0, a1, y0, y1, b0, b1;
+    lin_axis(dx, dd.w, dd.ow, true, x0, x1, a0, a1);
+    lin_axis(dy, dd.h, dd.oh, false, y0, y1, b0, b1);
+    const int d0 = gray_at<RGB>(s, dd.w, dd.c, y0, x0) * a0 + gray_at<RGB>(s, dd.w, dd.c, y0, x1) * a1;
+    const int d1 = gray_at<RGB>(s, dd.w, dd.c, y1, x0) * a0 + gray_at<RGB>(s, dd.w, dd.c, y1, x1) * a1;
+    v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+  }
+  dst[dd.dst_off + o] = (uint8_t)v;
+}
+
+static hipError_t launch_resize(hipStream_t s, const uint8_t* src, const ImgDesc* desc_dev, int count,
+                                int64_t max_out, bool rgb, uint8_t* dst) {
+  if (count == 0 || max_out == 0) return hipSuccess;
+  const dim3 grid((unsigned)((max_out + 255) / 256), (unsigned)count);
+  if (rgb)
+    hipLaunchKernelGGL(resize_kernel<true>, grid, dim3(256), 0, s, src, desc_dev, dst);
+  else
+    hipLaunchKernelGGL(resize_kernel<false>, grid, dim3(256), 0, s, src, desc_dev, dst);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- template localiser
+constexpr int kTmChunk = 128;   // template rows per int32 partial
+constexpr int kTmPiece = 352;   // template columns per piece (nkb <= 12)
+constexpr int kTmTile = 128;    // output tile (rows = 4 waves x 32, cols = 4 blocks x 32)
+
+struct TmProblem {
+  int th, tw, hr, wr;
+  int64_t tmpl_off;  // scaled template (uint8, th x tw) in the scaled buffer
+  int64_t part_off;  // int32 offset of this problem's partial slabs [nparts][hr][wr]
+  int64_t map_off;   // float offset of this problem's map (optional output)
+  int nparts, pad;
+};
+struct TmPiece {
+  int prob, px, wp, nkb;
+  int64_t band_off;  // bytes: [th][nkb][64 lanes][16]
+};
+struct TmWork {
+  int piece, part, ya, yb, y0, x0;
+};
+struct TmStat {
+  long long sT, varT;  // sum(T'), N*sum(T'^2) - sum(T')^2
+};
+
+// frame8 = I - 128 (int8) in a zero-padded [rows][pitch] image; integral images of I'
+// and I'^2 (int64, (H+1) x (W+1)).
+__global__ void tm_frame_kernel(const uint8_t* __restrict__ f, int H, int W, int64_t ld, int8_t* __restrict__ f8,
+                                int64_t pitch) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)H * W) return;
+  const int64_t y = i / W, x = i - (i / W) * W;
+  f8[y * pitch + x] = (int8_t)((int)f[y * ld + x] - 128);
+}
+
+__global__ void tm_rowscan_kernel(const int8_t* __restrict__ f8, int H, int W, int64_t pitch,
+                                  long long* __restrict__ ii1, long long* __restrict__ ii2) {
+  const int y = blockIdx.x * blockDim.x + threadIdx.x;
+  if (y > H) return;
+  long long* r1 = ii1 + (int64_t)y * (W + 1);
+  long long* r2 = ii2 + (int64_t)y * (W + 1);
+  r1[0] = 0;
+  r2[0] = 0;
+  long long s1 = 0, s2 = 0;
+  for (int x = 0; x < W; ++x) {
+    const long long v = y == 0 ? 0 : f8[(int64_t)(y - 1) * pitch + x];
+    s1 += v;
+    s2 += v * v;
+    r1[x + 1] = s1;
+    r2[x + 1] = s2;
+  }
+}
+
+__global__ void tm_colscan_kernel(int H, int W, long long* __restrict__ ii1, long long* __restrict__ ii2) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x > W) return;
+  long long s1 = 0, s2 = 0;
+  for (int y = 0; y <= H; ++y) {
+    s1 += ii1[(int64_t)y * (W + 1) + x];
+    s2 += ii2[(int64_t)y * (W + 1) + x];
+    ii1[(int64_t)y * (W + 1) + x] = s1;
+    ii2[(int64_t)y * (W + 1) + x] = s2;
+  }
+}
+
+// Per problem: sum(T'), sum(T'^2) -> varT (exact int64).  One block per problem.
+__global__ __launch_bounds__(256) void tm_stat_kernel(const uint8_t* __restrict__ scaled,
+                                                      const TmProblem* __restrict__ probs, TmStat* __restrict__ st) {
+  const TmProblem pb = probs[blockIdx.x];
+  const int64_t n = (int64_t)pb.th * pb.tw;
+  long long s1 = 0, s2 = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const long long v = (long long)scaled[pb.tmpl_off + i] - 128;
+    s1 += v;
+    s2 += v * v;
+  }
+  __shared__ long long r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    st[blockIdx.x].sT = r1[0];
+    st[blockIdx.x].varT = n * r2[0] - r1[0] * r1[0];
+  }
+}
+
+// band[y'][kb][lane][j] = T'[y'][px + 32 kb + 16 (lane >> 5) + j - (lane & 31)] inside the
+// piece's columns [0, wp), else 0 — the B-operand fragment (lane (c, h) holds
+// B[16h + j][c]) of k-block kb.  grid (th, npieces), block 64 x nkb <= 1024 threads.
+__global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProblem* __restrict__ probs,
+                               const TmPiece* __restrict__ pieces, uint8_t* __restrict__ bands) {
+  const TmPiece pc = pieces[blockIdx.y];
+  const TmProblem pb = probs[pc.prob];
+  const int yy = blockIdx.x;
+  if (yy >= pb.th) return;
+  for (int t = threadIdx.x; t < 64 * pc.nkb; t += blockDim.x) {
+    const int kb = t >> 6, lane = t & 63;
+    const int c = lane & 31, hh = lane >> 5;
+    union {
+      int8_t b[16];
+      i32x4 v;
+    } u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int q = 32 * kb + 16 * hh + j - c;  // template column inside the piece
+      u.b[j] = (q >= 0 && q < pc.wp) ? (int8_t)((int)scaled[pb.tmpl_off + (int64_t)yy * pb.tw + pc.px + q] - 128)
+                                     : (int8_t)0;
+    }
+    *reinterpret_cast<i32x4*>(bands + pc.band_off + ((int64_t)yy * pc.nkb + kb) * 1024 + lane * 16) = u.v;
+  }
+}
+
+// One workgroup = one work item: a 128 x 128 output tile of one problem, template rows
+// [ya, yb) of one column piece.  Wave w owns output rows y0 + 32w + [0, 32) and all four
+// 32-column blocks; A (frame rows, 16 contiguous int8 per lane) and the band fragment are
+// 16-byte global loads (the frame and the bands stay L2-resident).
+__global__ __launch_bounds__(256) void tm_corr_kernel(const int8_t* __restrict__ f8, int64_t pitch,
+                                                      const uint8_t* __restrict__ bands,
+                                                      const TmPiece* __restrict__ pieces,
+                                                      const TmWork* __restrict__ works,
+                                                      const TmProblem* __restrict__ probs, int* __restrict__ parts) {
+  const TmWork wk = works[blockIdx.x];
+  const TmPiece pc = pieces[wk.piece];
+  const TmProblem pb = probs[pc.prob];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int nkb = pc.nkb;
+  i32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
+  const int8_t* abase = f8 + (int64_t)(wk.y0 + 32 * wave + r) * pitch + wk.x0 + pc.px + 16 * h;
+  const uint8_t* bbase = bands + pc.band_off + lane * 16;
+  for (int yy = wk.ya; yy < wk.yb; ++yy) {
+    const int8_t* arow = abase + (int64_t)yy * pitch;
+    const uint8_t* brow = bbase + (int64_t)yy * nkb * 1024;
+    i32x4 b1 = {}, b2 = {}, b3 = {};
+    for (int kb = 0; kb < nkb + 3; ++kb) {
+      const i32x4 a = *reinterpret_cast<const i32x4*>(arow + 32 * kb);
+      const i32x4 b0 = kb < nkb ? *reinterpret_cast<const i32x4*>(brow + kb * 1024) : i32x4{};
+      acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1, acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b2, acc2, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b3, acc3, 0, 0, 0);
+      b3 = b2;
+      b2 = b1;
+      b1 = b0;
+    }
+  }
+  int* out = parts + pb.part_off + (int64_t)wk.part * pb.hr * pb.wr;
+  auto store = [&](const i32x16& v, int n) {
+    const int x = wk.x0 + 32 * n + r;
+    if (x >= pb.wr) return;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int y = wk.y0 + 32 * wave + (g & 3) + 8 * (g >> 2) + 4 * h;
+      if (y < pb.hr) out[(int64_t)y * pb.wr + x] = v[g];
+    }
+  };
+  store(acc0, 0);
+  store(acc1, 1);
+  store(acc2, 2);
+  store(acc3, 3);
+}
+
+// OpenCV's TM_CCOEFF_NORMED rule (templmatch.cpp common_matchTemplate) on exact integers.
+__device__ __forceinline__ float tm_score(long long numN, long long varI, long long varT) {
+  if (varT == 0) return 1.f;  // flat template: all ones
+  const double t = __dmul_rn(sqrt((double)varI), sqrt((double)varT));
+  const double num = (double)numN;
+  const double an = fabs(num);
+  double rr;
+  if (an < t)
+    rr = __ddiv_rn(num, t);
+  else if (an < __dmul_rn(t, 1.125))
+    rr = num > 0 ? 1.0 : (num < 0 ? -1.0 : 0.0);
+  else
+    rr = 0.0;
+  return __double2float_rn(rr);
+}
+
+// Max-first, then lowest raster index: min over ~orderable(score) << 32 | index.
+__device__ __forceinline__ unsigned long long tm_key(float v, unsigned idx) {
+  const unsigned b = __float_as_uint(v == 0.f ? 0.f : v);
+  const unsigned o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);  // ascending order
+  return ((unsigned long long)(~o) << 32) | idx;
+}
+
+// grid (ceil(max positions / 256), nprob): score every position, optional map, arg-max.
+__global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restrict__ probs,
+                                                       const TmStat* __restrict__ st, const int* __restrict__ parts,
+                                                       const long long* __restrict__ ii1,
+                                                       const long long* __restrict__ ii2, int W,
+                                                       float* __restrict__ maps,
+                                                       unsigned long long* __restrict__ keys) {
+  const TmProblem pb = probs[blockIdx.y];
+  const int64_t npos = (int64_t)pb.hr * pb.wr;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long key = ~0ull;
+  if (i < npos) {
+    const int y = (int)(i / pb.wr), x = (int)(i - (i / pb.wr) * pb.wr);
+    long long P = 0;
+    const int* pp = parts + pb.part_off + i;
+    for (int q = 0; q < pb.nparts; ++q) P += pp[(int64_t)q * npos];
+    const int64_t W1 = W + 1;
+    auto box = [&](const long long* ii) {
+      return ii[(int64_t)(y + pb.th) * W1 + x + pb.tw] - ii[(int64_t)y * W1 + x + pb.tw] -
+             ii[(int64_t)(y + pb.th) * W1 + x] + ii[(int64_t)y * W1 + x];
+    };
+    const long long sI = box(ii1), sI2 = box(ii2);
+    const long long n = (long long)pb.th * pb.tw;
+    const TmStat ts = st[blockIdx.y];
+    const float v = tm_score(n * P - ts.sT * sI, n * sI2 - sI * sI, ts.varT);
+    if (maps) maps[pb.map_off + i] = v;
+    key = tm_key(v, (unsigned)i);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(key, off);
+    key = o < key ? o : key;
+  }
+  if ((threadIdx.x & 63) == 0 && key != ~0ull) atomicMin(keys + blockIdx.y, key);
+}
+
+__global__ void fill_u64_kernel(unsigned long long* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = ~0ull;
+}
+
+// ------------------------------------------------------------------ ctx state
+struct TmState {
+  int H = 0, W = 0, nprob = 0, nwork = 0;
+  int64_t pitch = 0, max_pos = 0, map_total = 0;
+  std::vector<TmProblem> probs;
+  DevBuf raw, scaled, bands, d_probs, d_pieces, d_works, d_stat, parts, f8, ii1, ii2, keys, frame_stage, maps;
+};
+
+void tm_release(ef_ctx* c) {
+  if (!c || !c->tm) return;
+  TmState* t = static_cast<TmState*>(c->tm);
+  DevBuf* bufs[] = {&t->raw,   &t->scaled, &t->bands, &t->d_probs, &t->d_pieces, &t->d_works, &t->d_stat,
+                    &t->parts, &t->f8,     &t->ii1,   &t->ii2,     &t->keys,     &t->frame_stage, &t->maps};
+  for (DevBuf* b : bufs) release(*b);
+  delete t;
+  c->tm = nullptr;
+}
+
+static int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+}  // namespace ef
+
+using namespace ef;
+
+extern "C" {
+
+int ef_preprocess(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const int32_t* heights,
+                  const int32_t* widths, const int32_t* channels, int64_t count, int32_t out_h, int32_t out_w,
+                  uint8_t* out, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (count < 0 || out_h <= 0 || out_w <= 0 || (count > 0 && (!data || !offsets || !heights || !widths || !out)))
+    return set_err(c, EF_E_INVALID, "ef_preprocess: bad arguments");
+  if (count == 0) return EF_OK;
+  if (count > 65535) return set_err(c, EF_E_INVALID, "ef_preprocess: at most 65535 images per call");
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  const bool dev = flags & EF_MEM_DEVICE;
+  std::vector<ImgDesc> desc((size_t)count);
+  int64_t src_bytes = 0;
+  for (int64_t i = 0; i < count; ++i) {
+    const int ch = channels ? channels[i] : 1;
+    if (heights[i] <= 0 || widths[i] <= 0 || (ch != 1 && ch != 3 && ch != 4) || offsets[i] < 0)
+      return set_err(c, EF_E_INVALID, "ef_preprocess: image " + std::to_string(i) + " has a bad shape");
+    desc[i] = ImgDesc{offsets[i], i * (int64_t)out_h * out_w, heights[i], widths[i], ch, out_h, out_w, 0};
+    const int64_t end = offsets[i] + (int64_t)heights[i] * widths[i] * ch;
+    src_bytes = end > src_bytes ? end : src_bytes;
+  }
+  // metadata + (host) pixels staged in one scratch buffer
+  const size_t dbytes = rup((int64_t)desc.size() * sizeof(ImgDesc), 256);
+  const size_t obytes = (size_t)count * out_h * out_w;
+  const size_t need = dbytes + (dev ? 0 : rup(src_bytes, 256) + rup(obytes, 256));
+  EF_TRY(ensure(c, c->p_stage, need));
+  char* base = static_cast<char*>(c->p_stage.p);
+  ImgDesc* ddesc = reinterpret_cast<ImgDesc*>(base);
+  const uint8_t* src = data;
+  uint8_t* dst = out;
+  EF_HIP(c, hipMemcpyAsync(ddesc, desc.data(), desc.size() * sizeof(ImgDesc), hipMemcpyHostToDevice, c->stream),
+         "H2D descriptors");
+  if (!dev) {
+    uint8_t* s = reinterpret_cast<uint8_t*>(base + dbytes);
+    EF_HIP(c, hipMemcpyAsync(s, data, src_bytes, hipMemcpyHostToDevice, c->stream), "H2D images");
+    src = s;
+    dst = reinterpret_cast<uint8_t*>(base + dbytes + rup(src_bytes, 256));
+  }
+  EF_HIP(c, launch_resize(c->stream, src, ddesc, (int)count, (int64_t)out_h * out_w, flags & EF_IMG_RGB, dst),
+         "resize kernel");
+  if (!dev) {
+    EF_HIP(c, hipMemcpyAsync(out, dst, obytes, hipMemcpyDeviceToHost, c->stream), "D2H faces");
+  }
+  // descriptors live in scratch that the next call may overwrite: always wait
+  EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+  return EF_OK;
+}
+
+int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_offsets, const int32_t* templ_h,
+                  const int32_t* templ_w, int32_t n_templates, const int32_t* prob_templ, const int32_t* prob_h,
+                  const int32_t* prob_w, int32_t n_problems, int32_t frame_h, int32_t frame_w, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if (n_templates < 0 || n_problems < 0 || frame_h <= 0 || frame_w <= 0 ||
+      (n_templates > 0 && (!templ_data || !templ_offsets || !templ_h || !templ_w)) ||
+      (n_problems > 0 && (!prob_templ || !prob_h || !prob_w)))
+    return set_err(c, EF_E_INVALID, "ef_tm_prepare: bad arguments");
+  if (n_problems > 65535) return set_err(c, EF_E_INVALID, "ef_tm_prepare: at most 65535 problems");
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  tm_release(c);
+  TmState* t = new TmState();
+  c->tm = t;
+  t->H = frame_h;
+  t->W = frame_w;
+  t->nprob = n_problems;
+  t->pitch = rup((int64_t)frame_w + 256, 64);
+  const bool dev = flags & EF_MEM_DEVICE;
+
+  int64_t raw_bytes = 0;
+  for (int i = 0; i < n_templates; ++i) {
+    if (templ_h[i] <= 0 || templ_w[i] <= 0 || templ_offsets[i] < 0)
+      return set_err(c, EF_E_INVALID, "ef_tm_prepare: template " + std::to_string(i) + " has a bad shape");
+    const int64_t e = templ_offsets[i] + (int64_t)templ_h[i] * templ_w[i];
+    raw_bytes = e > raw_bytes ? e : raw_bytes;
+  }
+  std::vector<ImgDesc> rd;
+  std::vector<TmPiece> pieces;
+  std::vector<TmWork> works;
+  int64_t scaled_bytes = 0, part_elems = 0, band_bytes = 0, map_total = 0, max_pos = 0;
+  int max_h = 0;
+  for (int p = 0; p < n_problems; ++p) {
+    const int ti = prob_templ[p], th = prob_h[p], tw = prob_w[p];
+    if (ti < 0 || ti >= n_templates || th <= 0 || tw <= 0 || th > frame_h || tw > frame_w || tw > 4096)
+      return set_err(c, EF_E_INVALID, "ef_tm_prepare: problem " + std::to_string(p) + " is invalid");
+    TmProblem pb{};
+    pb.th = th;
+    pb.tw = tw;
+    pb.hr = frame_h - th + 1;
+    pb.wr = frame_w - tw + 1;
+    pb.tmpl_off = scaled_bytes;
+    rd.push_back(ImgDesc{templ_offsets[ti], scaled_bytes, templ_h[ti], templ_w[ti], 1, th, tw, 0});
+    scaled_bytes += rup((int64_t)th * tw, 16);
+    const int npiece = (tw + kTmPiece - 1) / kTmPiece;
+    const int nchunk = (th + kTmChunk - 1) / kTmChunk;
+    pb.nparts = npiece * nchunk;
+    pb.part_off = part_elems;
+    part_elems += (int64_t)pb.nparts * pb.hr * pb.wr;
+    pb.map_off = map_total;
+    map_total += (int64_t)pb.hr * pb.wr;
+    max_pos = std::max<int64_t>(max_pos, (int64_t)pb.hr * pb.wr);
+    max_h = std::max(max_h, th);
+    for (int q = 0; q < npiece; ++q) {
+      TmPiece pc{};
+      pc.prob = p;
+      pc.px = q * kTmPiece;
+      pc.wp = std::min(kTmPiece, tw - pc.px);
+      pc.nkb = (pc.wp + 31 + 31) / 32;
+      pc.band_off = band_bytes;
+      band_bytes += (int64_t)th * pc.nkb * 1024;
+      const int pi = (int)pieces.size();
+      pieces.push_back(pc);
+      for (int ch = 0; ch < nchunk; ++ch)
+        for (int y0 = 0; y0 < pb.hr; y0 += kTmTile)
+          for (int x0 = 0; x0 < pb.wr; x0 += kTmTile)
+            works.push_back(TmWork{pi, ch * npiece + q, ch * kTmChunk, std::min(th, (ch + 1) * kTmChunk), y0, x0});
+    }
+    t->probs.push_back(pb);
+  }
+  t->nwork = (int)works.size();
+  t->max_pos = max_pos;
+  t->map_total = map_total;
+  hipStream_t s = c->stream;
+  EF_TRY(ensure(c, t->raw, std::max<int64_t>(raw_bytes, 16)));
+  EF_TRY(ensure(c, t->scaled, std::max<int64_t>(scaled_bytes, 16)));
+  EF_TRY(ensure(c, t->bands, std::max<int64_t>(band_bytes, 16)));
+  EF_TRY(ensure(c, t->d_probs, std::max<size_t>(t->probs.size() * sizeof(TmProblem), 16)));
+  EF_TRY(ensure(c, t->d_pieces, std::max<size_t>(pieces.size() * sizeof(TmPiece), 16)));
+  EF_TRY(ensure(c, t->d_works, std::max<size_t>(works.size() * sizeof(TmWork), 16)));
+  EF_TRY(ensure(c, t->d_stat, std::max<size_t>((size_t)n_problems * sizeof(TmStat), 16)));
+  EF_TRY(ensure(c, t->parts, std::max<int64_t>(part_elems * 4, 16)));
+  EF_TRY(ensure(c, t->keys, std::max<size_t>((size_t)n_problems * 8, 16)));
+  EF_TRY(ensure(c, t->f8, (size_t)(frame_h + kTmTile + 32) * t->pitch));
+  EF_TRY(ensure(c, t->ii1, (size_t)(frame_h + 1) * (frame_w + 1) * 8));
+  EF_TRY(ensure(c, t->ii2, (size_t)(frame_h + 1) * (frame_w + 1) * 8));
+  EF_TRY(ensure(c, t->frame_stage, (size_t)frame_h * frame_w));
+  EF_HIP(c, hipMemsetAsync(t->f8.p, 0, t->f8.bytes, s), "memset frame");
+  if (raw_bytes > 0)
+    EF_HIP(c, hipMemcpyAsync(t->raw.p, templ_data, raw_bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s),
+           "templates");
+  if (n_problems > 0) {
+    ImgDesc* drd = nullptr;
+    EF_TRY(ensure(c, c->p_stage, rd.size() * sizeof(ImgDesc)));
+    drd = static_cast<ImgDesc*>(c->p_stage.p);
+    EF_HIP(c, hipMemcpyAsync(drd, rd.data(), rd.size() * sizeof(ImgDesc), hipMemcpyHostToDevice, s), "H2D desc");
+    EF_HIP(c, hipMemcpyAsync(t->d_probs.p, t->probs.data(), t->probs.size() * sizeof(TmProblem),
+                             hipMemcpyHostToDevice, s), "H2D problems");
+    EF_HIP(c, hipMemcpyAsync(t->d_pieces.p, pieces.data(), pieces.size() * sizeof(TmPiece), hipMemcpyHostToDevice, s),
+           "H2D pieces");
+    EF_HIP(c, hipMemcpyAsync(t->d_works.p, works.data(), works.size() * sizeof(TmWork), hipMemcpyHostToDevice, s),
+           "H2D works");
+    int64_t max_out = 0;
+    for (auto& d : rd) max_out = std::max<int64_t>(max_out, (int64_t)d.oh * d.ow);
+    EF_HIP(c, launch_resize(s, static_cast<const uint8_t*>(t->raw.p), drd, (int)rd.size(), max_out, false,
+                            static_cast<uint8_t*>(t->scaled.p)), "resize templates");
+    hipLaunchKernelGGL(tm_stat_kernel, dim3((unsigned)n_problems), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(t->scaled.p), static_cast<const TmProblem*>(t->d_probs.p),
+                       static_cast<TmStat*>(t->d_stat.p));
+    hipLaunchKernelGGL(tm_band_kernel, dim3((unsigned)max_h, (unsigned)pieces.size()), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(t->scaled.p), static_cast<const TmProblem*>(t->d_probs.p),
+                       static_cast<const TmPiece*>(t->d_pieces.p), static_cast<uint8_t*>(t->bands.p));
+    EF_HIP(c, hipGetLastError(), "template prepare kernels");
+  }
+  EF_HIP(c, hipStreamSynchronize(s), "sync");  // host vectors and staged descriptors go out of scope
+  return EF_OK;
+}
+
+int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_out, int32_t* x_out, int32_t* y_out,
+                float* maps_out, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  TmState* t = static_cast<TmState*>(c->tm);
+  if (!t) return set_err(c, EF_E_STATE, "ef_tm_match: call ef_tm_prepare first");
+  if (!frame || frame_ld < t->W) return set_err(c, EF_E_INVALID, "ef_tm_match: bad frame");
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  const bool dev = flags & EF_MEM_DEVICE;
+  hipStream_t s = c->stream;
+  const int H = t->H, W = t->W;
+  const uint8_t* f = frame;
+  if (!dev) {
+    EF_HIP(c, hipMemcpy2DAsync(t->frame_stage.p, W, frame, frame_ld, W, H, hipMemcpyHostToDevice, s), "H2D frame");
+    f = static_cast<const uint8_t*>(t->frame_stage.p);
+    frame_ld = W;
+  }
+  int8_t* f8 = static_cast<int8_t*>(t->f8.p);
+  long long* ii1 = static_cast<long long*>(t->ii1.p);
+  long long* ii2 = static_cast<long long*>(t->ii2.p);
+  const int64_t np = (int64_t)H * W;
+  TimerEvt tev;
+  timer_begin(c, EF_KERNEL_TMATCH, &tev);
+  hipLaunchKernelGGL(tm_frame_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, f, H, W, frame_ld, f8,
+                     t->pitch);
+  hipLaunchKernelGGL(tm_rowscan_kernel, dim3((unsigned)((H + 1 + 63) / 64)), dim3(64), 0, s, f8, H, W, t->pitch, ii1,
+                     ii2);
+  hipLaunchKernelGGL(tm_colscan_kernel, dim3((unsigned)((W + 1 + 63) / 64)), dim3(64), 0, s, H, W, ii1, ii2);
+  if (t->nprob > 0) {
+    unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
+    hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((t->nprob + 255) / 256)), dim3(256), 0, s, keys, t->nprob);
+    if (t->nwork > 0)
+      hipLaunchKernelGGL(tm_corr_kernel, dim3((unsigned)t->nwork), dim3(256), 0, s, f8, t->pitch,
+                         static_cast<const uint8_t*>(t->bands.p), static_cast<const TmPiece*>(t->d_pieces.p),
+                         static_cast<const TmWork*>(t->d_works.p), static_cast<const TmProblem*>(t->d_probs.p),
+                         static_cast<int*>(t->parts.p));
+    float* maps = nullptr;
+    if (maps_out) {
+      if (dev) {
+        maps = maps_out;
+      } else {
+        EF_TRY(ensure(c, t->maps, (size_t)t->map_total * 4));
+        maps = static_cast<float*>(t->maps.p);
+      }
+    }
+    hipLaunchKernelGGL(tm_score_kernel, dim3((unsigned)((t->max_pos + 255) / 256), (unsigned)t->nprob), dim3(256), 0,
+                       s, static_cast<const TmProblem*>(t->d_probs.p), static_cast<const TmStat*>(t->d_stat.p),
+                       static_cast<const int*>(t->parts.p), ii1, ii2, W, maps, keys);
+    timer_end(c, &tev);
+    EF_HIP(c, hipGetLastError(), "template match kernels");
+    std::vector<unsigned long long> hk((size_t)t->nprob);
+    EF_HIP(c, hipMemcpyAsync(hk.data(), keys, hk.size() * 8, hipMemcpyDeviceToHost, s), "D2H keys");
+    if (maps_out && !dev)
+      EF_HIP(c, hipMemcpyAsync(maps_out, maps, (size_t)t->map_total * 4, hipMemcpyDeviceToHost, s), "D2H maps");
+    EF_HIP(c, hipStreamSynchronize(s), "sync");
+    for (int p = 0; p < t->nprob; ++p) {
+      const unsigned o = ~(unsigned)(hk[p] >> 32);
+      const unsigned b = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+      float v;
+      std::memcpy(&v, &b, 4);
+      const unsigned idx = (unsigned)(hk[p] & 0xffffffffu);
+      if (best_out) best_out[p] = v;
+      if (x_out) x_out[p] = (int32_t)(idx % (unsigned)t->probs[p].wr);
+      if (y_out) y_out[p] = (int32_t)(idx / (unsigned)t->probs[p].wr);
+    }
+  } else {
+    timer_end(c, &tev);
+    EF_HIP(c, hipStreamSynchronize(s), "sync");
+  }
+  return EF_OK;
+}
+
+int ef_tm_info(ef_ctx* c, int32_t* n_problems, int64_t* map_elems, int32_t* result_h, int32_t* result_w) {
+  if (!c) return EF_E_INVALID;
+  TmState* t = static_cast<TmState*>(c->tm);
+  if (!t) return set_err(c, EF_E_STATE, "ef_tm_info: call ef_tm_prepare first");
+  if (n_problems) *n_problems = t->nprob;
+  if (map_elems) *map_elems = t->map_total;
+  for (int p = 0; p < t->nprob; ++p) {
+    if (result_h) result_h[p] = t->probs[p].hr;
+    if (result_w) result_w[p] = t->probs[p].wr;
+  }
+  return EF_OK;
+}
+
+}  // extern "C"

@@ -94,6 +94,7 @@ struct ef_ctx {
   ef::DevBuf proj_part; // float[nsplit][bpad][kpw]
   ef::DevBuf feats_dev; // float[b][k] staging for host output
 
+  void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* blas = nullptr;  // rocBLAS handle (fit's plain dense products), lazily created
 
   bool timing = false;
@@ -106,6 +107,7 @@ namespace ef {
 
 int set_err(ef_ctx* c, int code, const std::string& msg);
 void blas_release(ef_ctx* c);
+void tm_release(ef_ctx* c);
 int hip_err(ef_ctx* c, hipError_t e, const char* what);
 int ensure(ef_ctx* c, DevBuf& b, size_t bytes);
 void release(DevBuf& b);

@@ -17,7 +17,8 @@ EF_METRIC_L2, EF_METRIC_COSINE = 0, 1
 EF_FIT_STANDARDIZE = 0x1
 EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
-EF_KERNEL_SEARCH, EF_KERNEL_PROJECT = 0, 1
+EF_IMG_RGB = 0x200
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH = 0, 1, 2
 EF_KEY_NONE = (1 << 63) - 1
 
 _ERRNAMES = {-1: "EF_E_INVALID", -2: "EF_E_HIP", -3: "EF_E_STATE", -4: "EF_E_NOMEM", -5: "EF_E_NUMERIC"}
@@ -54,6 +55,10 @@ _SIGS = {
     "ef_search": ([vp, vp, i64, i32, vp, u32], C.c_int),
     "ef_recognize": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
     "ef_keys_decode": ([vp, i64, i32, vp, vp], None),
+    "ef_preprocess": ([vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, u32], C.c_int),
+    "ef_tm_prepare": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, u32], C.c_int),
+    "ef_tm_match": ([vp, vp, i64, vp, vp, vp, vp, u32], C.c_int),
+    "ef_tm_info": ([vp, C.POINTER(i32), C.POINTER(i64), vp, vp], C.c_int),
     "ef_timing_enable": ([vp, C.c_int], C.c_int),
     "ef_timing_get": ([vp, i32, C.POINTER(C.c_double), C.POINTER(i64)], C.c_int),
     "ef_timing_reset": ([vp], C.c_int),

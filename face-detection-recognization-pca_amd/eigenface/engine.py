@@ -61,6 +61,12 @@ class Engine:
 
     def __init__(self, device: int = 0):
         self._lib = N.lib()
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_available():
+            # torch's HIP runtime must come up before this process's first libeigenface
+            # context, or torch afterwards reports no GPU (seen on the MI355X boxes)
+            torch.cuda.init()
         h = C.c_void_p()
         rc = self._lib.ef_create(int(device), C.byref(h))
         if rc != N.EF_OK:
@@ -268,6 +274,90 @@ class Engine:
         idx, best = decode_keys(keys, metric)
         return (idx, best, feats) if return_features else (idx, best)
 
+    # ---------------------------------------------------------------------- images
+    def preprocess(self, images, size=(64, 64), rgb=False, out=None):
+        """Grey + INTER_LINEAR resize of a ragged batch (include/eigenface.h
+        ef_preprocess): ``images`` is a list of uint8 arrays (h, w) or (h, w, 3|4)
+        (BGR unless ``rgb``); ``size`` is cv2's (width, height).  Returns an
+        (n, height*width) uint8 array (or fills device tensor ``out``)."""
+        ow, oh = int(size[0]), int(size[1])
+        n = len(images)
+        if n == 0:
+            return np.empty((0, oh * ow), np.uint8)
+        arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+        hs = np.array([a.shape[0] for a in arrs], np.int32)
+        ws = np.array([a.shape[1] for a in arrs], np.int32)
+        cs = np.array([1 if a.ndim == 2 else a.shape[2] for a in arrs], np.int32)
+        sizes = np.array([a.size for a in arrs], np.int64)
+        offs = np.zeros(n, np.int64)
+        offs[1:] = np.cumsum(sizes)[:-1]
+        buf = np.concatenate([a.reshape(-1) for a in arrs])
+        flags = N.EF_IMG_RGB if rgb else 0
+        if out is not None:  # device output: stage the pixels on the device too
+            import torch
+            dbuf = torch.from_numpy(buf).to(out.device)
+            self._chk(self._lib.ef_preprocess(self._h, dbuf.data_ptr(), offs.ctypes.data, hs.ctypes.data,
+                                              ws.ctypes.data, cs.ctypes.data, n, oh, ow, out.data_ptr(),
+                                              flags | N.EF_MEM_DEVICE))
+            return out
+        res = np.empty((n, oh * ow), np.uint8)
+        self._chk(self._lib.ef_preprocess(self._h, buf.ctypes.data, offs.ctypes.data, hs.ctypes.data,
+                                          ws.ctypes.data, cs.ctypes.data, n, oh, ow, res.ctypes.data, flags))
+        return res
+
+    def tm_prepare(self, templates, problems, frame_shape):
+        """Resident template-localiser operands (ef_tm_prepare).  ``templates``: list of
+        grey uint8 (h, w) arrays; ``problems``: list of (template index, height, width)
+        scaled sizes; ``frame_shape``: (H, W)."""
+        arrs = [np.ascontiguousarray(t, dtype=np.uint8) for t in templates]
+        nt = len(arrs)
+        th = np.array([a.shape[0] for a in arrs], np.int32)
+        tw = np.array([a.shape[1] for a in arrs], np.int32)
+        sizes = np.array([a.size for a in arrs], np.int64)
+        offs = np.zeros(nt, np.int64)
+        if nt > 1:
+            offs[1:] = np.cumsum(sizes)[:-1]
+        buf = np.concatenate([a.reshape(-1) for a in arrs]) if nt else np.zeros(1, np.uint8)
+        pr = np.asarray(problems, dtype=np.int64).reshape(-1, 3)
+        pt, ph, pw = (np.ascontiguousarray(pr[:, i], dtype=np.int32) for i in range(3))
+        H, W = (int(v) for v in frame_shape)
+        self._chk(self._lib.ef_tm_prepare(self._h, buf.ctypes.data, offs.ctypes.data, th.ctypes.data,
+                                          tw.ctypes.data, nt, pt.ctypes.data, ph.ctypes.data, pw.ctypes.data,
+                                          len(pr), H, W, 0))
+        self._tm = (len(pr), H, W, pr.copy())
+
+    def tm_match(self, frame, maps=False):
+        """Run the prepared problems on one grey frame: (best float32[P], x int32[P],
+        y int32[P]) and, with ``maps``, the list of TM_CCOEFF_NORMED result maps."""
+        if getattr(self, "_tm", None) is None:
+            raise RuntimeError("call tm_prepare first")
+        npb, H, W, _ = self._tm
+        f = np.ascontiguousarray(frame, dtype=np.uint8)
+        if f.shape != (H, W):
+            raise ValueError(f"frame must be {(H, W)}, got {f.shape}")
+        best = np.empty(npb, np.float32)
+        xs = np.empty(npb, np.int32)
+        ys = np.empty(npb, np.int32)
+        mp = None
+        if maps:
+            n = C.c_int32(0)
+            tot = C.c_int64(0)
+            hr = np.empty(max(npb, 1), np.int32)
+            wr = np.empty(max(npb, 1), np.int32)
+            self._chk(self._lib.ef_tm_info(self._h, C.byref(n), C.byref(tot), hr.ctypes.data, wr.ctypes.data))
+            flat = np.empty(tot.value, np.float32)
+            mp = flat
+        self._chk(self._lib.ef_tm_match(self._h, f.ctypes.data, W, best.ctypes.data, xs.ctypes.data,
+                                        ys.ctypes.data, mp.ctypes.data if mp is not None else None, 0))
+        if not maps:
+            return best, xs, ys
+        out, o = [], 0
+        for p in range(npb):
+            m = int(hr[p]) * int(wr[p])
+            out.append(flat[o:o + m].reshape(int(hr[p]), int(wr[p])))
+            o += m
+        return best, xs, ys, out
+
     # --------------------------------------------------------------------- timing
     def timing(self, on=True):
         self._chk(self._lib.ef_timing_enable(self._h, 1 if on else 0))
@@ -276,7 +366,7 @@ class Engine:
         self._chk(self._lib.ef_timing_reset(self._h))
 
     def timing_get(self, kernel="search"):
-        kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT}[kernel]
+        kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT, "tmatch": N.EF_KERNEL_TMATCH}[kernel]
         ms = C.c_double(0)
         n = C.c_int64(0)
         self._chk(self._lib.ef_timing_get(self._h, kid, C.byref(ms), C.byref(n)))

@@ -52,10 +52,12 @@ extern "C" {
 #define EF_FIT_STANDARDIZE 0x1u /* StandardScaler before PCA (train-v4.py:131)                */
 #define EF_MODEL_BF16 0x2u      /* ef_model_set: project on bf16 MFMA (config 5), fp32 features */
 #define EF_MEM_DEVICE 0x100u    /* pointer args are device pointers, call is asynchronous    */
+#define EF_IMG_RGB 0x200u       /* ef_preprocess: 3/4-channel pixels are RGB(A), not BGR(A)  */
 
 /* kernels whose device time can be queried with ef_timing_get */
 #define EF_KERNEL_SEARCH 0  /* distance GEMM + fused arg-best   */
 #define EF_KERNEL_PROJECT 1 /* (p - mean).W projection GEMM     */
+#define EF_KERNEL_TMATCH 2  /* template localiser, one frame    */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX
@@ -126,6 +128,41 @@ int ef_recognize(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, int32_t
 /* Host-side key decoding: L2 -> squared distance, COSINE -> similarity;
  * EF_KEY_NONE -> idx -1, best NaN. */
 void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx);
+
+/* ------------------------------------------------------------------ ingest
+ * Replaces the per-image cv2.cvtColor(img, COLOR_BGR2GRAY) + cv2.resize(gray, (w, h))
+ * (INTER_LINEAR) of train-v4.py:59-68 and scan-template-v4.py:257-263 for a ragged
+ * batch of decoded images in one launch, with OpenCV's CV_8U fixed-point arithmetic
+ * (parity against OpenCV unpinned: OpenCV is not installed where this was built).
+ * Image i: heights[i] x widths[i] x channels[i] (1, 3 = BGR, 4 = BGRA; EF_IMG_RGB for
+ * RGB order; channels NULL = all 1) uint8 pixels at data + offsets[i], row-major.
+ * out: count x out_h x out_w uint8 (the probe / training row layout, train-v4.py:68).
+ * data/out are host pointers, or device pointers with EF_MEM_DEVICE; the metadata
+ * arrays are always host arrays.  At most 65535 images per call. */
+int ef_preprocess(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int32_t* heights,
+                  const int32_t* widths, const int32_t* channels, int64_t count, int32_t out_h,
+                  int32_t out_w, uint8_t* out, uint32_t flags);
+
+/* -------------------------------------------------------- template localiser
+ * Replaces template_match_all_models' inner loops (scan-template-v4.py:127-200):
+ * for every problem p = (template t, scaled size h x w):
+ *   R_p = cv2.matchTemplate(frame, cv2.resize(template_t, (w, h)), TM_CCOEFF_NORMED)
+ *   (best, (x, y)) = cv2.minMaxLoc(R_p) maximum (first in raster order).
+ * The correlation is exact (int8 matrix cores, int64 sums); the normalisation follows
+ * OpenCV's rule in float64, R is float32.  ef_tm_prepare uploads the grey templates
+ * (templ_h[i] x templ_w[i] at templ_data + templ_offsets[i]), resizes them on the GPU
+ * and builds the resident operands for a frame_h x frame_w frame; ef_tm_match then
+ * runs one frame (row stride frame_ld bytes) and returns per problem best_out, x_out,
+ * y_out (each optional) and, if maps_out is non-NULL, every R_p concatenated
+ * (sizes from ef_tm_info).  Host pointers unless EF_MEM_DEVICE. */
+int ef_tm_prepare(ef_ctx* ctx, const uint8_t* templ_data, const int64_t* templ_offsets,
+                  const int32_t* templ_h, const int32_t* templ_w, int32_t n_templates,
+                  const int32_t* prob_templ, const int32_t* prob_h, const int32_t* prob_w,
+                  int32_t n_problems, int32_t frame_h, int32_t frame_w, uint32_t flags);
+int ef_tm_match(ef_ctx* ctx, const uint8_t* frame, int64_t frame_ld, float* best_out, int32_t* x_out,
+                int32_t* y_out, float* maps_out, uint32_t flags);
+int ef_tm_info(ef_ctx* ctx, int32_t* n_problems, int64_t* map_elems, int32_t* result_h,
+               int32_t* result_w);
 
 /* ------------------------------------------------------------------ timing
  * Device time of each launch of a kernel, measured with hipEvents on the

@@ -33,6 +33,11 @@ def local_golden(name):
 
 @pytest.fixture(scope="session")
 def eng():
+    # torch's HIP runtime must initialise before libeigenface creates its context in this
+    # process (device tensors are used by some tests); otherwise torch reports no GPU.
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from eigenface import Engine
     e = Engine(0)
     yield e
