@@ -178,6 +178,108 @@ def fit_bench(eng, with_cpu: bool):
     return out
 
 
+# First five detection sizes of each lock_version model (the templates scan-template-v4.py
+# loads, :45-55), from faces/lock_version/*/*_faces_detection.json: shun, ruiyi,
+# Joseph_Lai, ruisheng.  Square crops.
+TEMPLATE_SIDES = [[224, 232, 234, 235, 82], [217, 219, 214, 219, 224], [100] * 5, [143, 314, 130, 321, 325]]
+PEAK_I8_TOPS = 5000.0   # MI355X dense int8 MFMA (2x the bf16 rate, MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def image_bench(eng, with_cpu: bool, frames=20):
+    """Secondary measurements of SURVEY.md §8f ranks 2-3 on the GPU (synthetic pixels):
+    ingest = 4096 BGR face crops of the reference's detection sizes (82-325 px) ->
+    grey -> 64x64 (train-v4.py:59-68); tmatch = one 640x480 grey camera frame against
+    4 models x 5 templates x 3 scales (scan-template-v4.py:127-200)."""
+    import torch
+    from eigenface.image import scaled_sizes
+    rng = np.random.default_rng(3)
+    sides = [s for grp in TEMPLATE_SIDES for s in grp]
+    # ---- ingest
+    n_img = 4096
+    crops = [rng.integers(0, 256, (sides[i % len(sides)], sides[i % len(sides)], 3), dtype=np.uint8)
+             for i in range(n_img)]
+    src_bytes = sum(c.size for c in crops)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((n_img, 4096), dtype=torch.uint8, device=dev)
+    hs = np.array([c.shape[0] for c in crops], np.int32)
+    offs = np.zeros(n_img, np.int64)
+    offs[1:] = np.cumsum([c.size for c in crops])[:-1]
+    dbuf = torch.from_numpy(np.concatenate([c.reshape(-1) for c in crops])).to(dev)
+    chans = np.full(n_img, 3, np.int32)
+    from eigenface import _native as N
+    import ctypes as C
+
+    def ingest():
+        N.check(eng._h, eng._lib.ef_preprocess(eng._h, dbuf.data_ptr(), offs.ctypes.data, hs.ctypes.data,
+                                               hs.ctypes.data, chans.ctypes.data, n_img, 64, 64,
+                                               out.data_ptr(), N.EF_MEM_DEVICE))
+    ingest()
+    torch.cuda.synchronize(dev)
+    eng.timing_reset()
+    reps = 10
+    for _ in range(reps):
+        ingest()
+    k_ms, k_n = eng.timing_get("ingest")
+    dt = k_ms / max(k_n, 1) * 1e-3  # resize kernel, hipEvents on its stream
+    # algorithmic bytes: every source pixel read once (3 B) + 4 KiB written per face
+    ib = src_bytes + n_img * 4096
+    res = {"ingest": {
+        "config": f"{n_img} BGR crops {min(sides)}-{max(sides)} px -> grey 64x64, device-resident",
+        "faces_per_s": round(n_img / dt, 1), "ms_per_batch_device": round(dt * 1e3, 4),
+        "algorithmic_bytes": ib, "achieved_GBs": round(ib / dt / 1e9, 1), "peak_GBs": PEAK_HBM_GBS,
+        "frac": round(ib / dt / 1e9 / PEAK_HBM_GBS, 4)}}
+    if with_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import image_oracle as io
+        t = time.perf_counter()
+        m = 256
+        for c in crops[:m]:
+            io.preprocess(c)
+        res["ingest"]["cpu"] = {"faces_per_s": round(m / (time.perf_counter() - t), 1), "cores": 1,
+                                "kind": "port", "sample": f"{m} crops, NumPy restatement of cvtColor+resize"}
+    # ---- template localiser
+    H, W = 480, 640
+    frame = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    templates, probs = [], []
+    for grp in TEMPLATE_SIDES:
+        for sd in grp:
+            ti = len(templates)
+            templates.append(rng.integers(0, 256, (sd, sd), dtype=np.uint8))
+            probs += [(ti, nh, nw) for _, nw, nh in scaled_sizes(sd, sd, H, W)]
+    eng.tm_prepare(templates, probs, (H, W))
+    ops = sum(2.0 * (H - ph + 1) * (W - pw + 1) * ph * pw for _, ph, pw in probs)
+    eng.tm_match(frame)
+    eng.timing_reset()
+    t = time.perf_counter()
+    for _ in range(frames):
+        eng.tm_match(frame)
+    dt = (time.perf_counter() - t) / frames
+    k_ms, k_n = eng.timing_get("tmatch")
+    kdt = k_ms / max(k_n, 1) * 1e-3
+    res["tmatch"] = {
+        "config": f"640x480 frame, {len(templates)} templates x 3 scales = {len(probs)} TM_CCOEFF_NORMED maps",
+        "frames_per_s": round(1 / dt, 2), "ms_per_frame_host": round(dt * 1e3, 4),
+        "ms_per_frame_device": round(kdt * 1e3, 4),
+        "algorithmic_ops": ops, "achieved_TOPS": round(ops / kdt / 1e12, 2), "peak_TOPS": PEAK_I8_TOPS,
+        "frac": round(ops / kdt / 1e12 / PEAK_I8_TOPS, 4)}
+    if with_cpu:
+        from oracle import image_oracle as io
+        from eigenface.image import scaled_sizes as ss  # noqa: F401
+        t = time.perf_counter()
+        ncpu = 0
+        for ti, ph, pw in probs:
+            if time.perf_counter() - t > 8.0:
+                break
+            io.match_template_fft(frame, io.resize_linear(templates[ti], (pw, ph)))
+            ncpu += 1
+        el = time.perf_counter() - t
+        res["tmatch"]["cpu"] = {"frames_per_s": round(ncpu / len(probs) / el, 4), "cores": _blas_threads(),
+                                "kind": "port", "sample": f"{ncpu}/{len(probs)} maps of one frame, "
+                                "scipy FFT correlation + integral-image normalisation (OpenCV's CPU method)"}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +290,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary fit timing")
+    ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -316,6 +419,11 @@ def main():
         }
         if world == 1 and not args.no_fit:
             rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu), "c2": fit_bench(eng, not args.no_cpu)}
+        if world == 1 and not args.no_image:
+            eng.use_own_stream()
+            eng.timing(True)
+            rec.update(image_bench(eng, not args.no_cpu))
+            eng.timing(False)
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
         else:

@@ -37,8 +37,10 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
+#include "ef_dma.hpp"
 #include "ef_internal.hpp"
 
 namespace ef {
@@ -153,43 +155,89 @@ struct TmStat {
   long long sT, varT;  // sum(T'), N*sum(T'^2) - sum(T')^2
 };
 
-// frame8 = I - 128 (int8) in a zero-padded [rows][pitch] image; integral images of I'
-// and I'^2 (int64, (H+1) x (W+1)).
-__global__ void tm_frame_kernel(const uint8_t* __restrict__ f, int H, int W, int64_t ld, int8_t* __restrict__ f8,
-                                int64_t pitch) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)H * W) return;
-  const int64_t y = i / W, x = i - (i / W) * W;
-  f8[y * pitch + x] = (int8_t)((int)f[y * ld + x] - 128);
-}
-
-__global__ void tm_rowscan_kernel(const int8_t* __restrict__ f8, int H, int W, int64_t pitch,
-                                  long long* __restrict__ ii1, long long* __restrict__ ii2) {
-  const int y = blockIdx.x * blockDim.x + threadIdx.x;
-  if (y > H) return;
-  long long* r1 = ii1 + (int64_t)y * (W + 1);
-  long long* r2 = ii2 + (int64_t)y * (W + 1);
-  r1[0] = 0;
-  r2[0] = 0;
+// frame8 = I - 128 (int8) in a zero-padded [rows][pitch] image, and row prefix sums of I'
+// and I'^2 (int64): one wave per integral-image row (row 0 is zero).
+__global__ __launch_bounds__(256) void tm_rows_kernel(const uint8_t* __restrict__ f, int H, int W, int64_t ld,
+                                                      int8_t* __restrict__ f8, int64_t pitch,
+                                                      long long* __restrict__ ii1, long long* __restrict__ ii2) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row > H) return;
+  const int64_t W1 = W + 1;
+  long long* r1 = ii1 + row * W1;
+  long long* r2 = ii2 + row * W1;
+  if (row == 0) {
+    for (int x = lane; x <= W; x += 64) r1[x] = r2[x] = 0;
+    return;
+  }
+  const int y = row - 1;
+  const int per = (W + 63) / 64, xb = lane * per;
   long long s1 = 0, s2 = 0;
-  for (int x = 0; x < W; ++x) {
-    const long long v = y == 0 ? 0 : f8[(int64_t)(y - 1) * pitch + x];
-    s1 += v;
-    s2 += v * v;
-    r1[x + 1] = s1;
-    r2[x + 1] = s2;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb + i;
+    if (x < W) {
+      const int v = (int)f[(int64_t)y * ld + x] - 128;
+      f8[(int64_t)y * pitch + x] = (int8_t)v;
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  long long e1 = s1, e2 = s2;  // inclusive scan of the lane totals
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const long long t1 = __shfl_up(e1, off), t2 = __shfl_up(e2, off);
+    if (lane >= off) {
+      e1 += t1;
+      e2 += t2;
+    }
+  }
+  e1 -= s1;
+  e2 -= s2;
+  if (lane == 0) r1[0] = r2[0] = 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb + i;
+    if (x < W) {
+      const long long v = f8[(int64_t)y * pitch + x];
+      e1 += v;
+      e2 += v * v;
+      r1[x + 1] = e1;
+      r2[x + 1] = e2;
+    }
   }
 }
 
-__global__ void tm_colscan_kernel(int H, int W, long long* __restrict__ ii1, long long* __restrict__ ii2) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x > W) return;
+// Column prefix of the row sums: block = 64 columns x 16 row segments.
+__global__ __launch_bounds__(1024) void tm_cols_kernel(int H, int W, long long* __restrict__ ii1,
+                                                       long long* __restrict__ ii2) {
+  __shared__ long long t1[16][64], t2[16][64];
+  const int cx = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + cx;
+  const int64_t W1 = W + 1;
+  const int per = (H + 15) / 16;
+  const int ya = 1 + sg * per, yb = ya + per < H + 1 ? ya + per : H + 1;
   long long s1 = 0, s2 = 0;
-  for (int y = 0; y <= H; ++y) {
-    s1 += ii1[(int64_t)y * (W + 1) + x];
-    s2 += ii2[(int64_t)y * (W + 1) + x];
-    ii1[(int64_t)y * (W + 1) + x] = s1;
-    ii2[(int64_t)y * (W + 1) + x] = s2;
+  if (x <= W) {
+#pragma unroll 4
+    for (int y = ya; y < yb; ++y) {
+      s1 += ii1[(int64_t)y * W1 + x];
+      s2 += ii2[(int64_t)y * W1 + x];
+    }
+  }
+  t1[sg][cx] = s1;
+  t2[sg][cx] = s2;
+  __syncthreads();
+  long long o1 = 0, o2 = 0;
+  for (int q = 0; q < sg; ++q) {
+    o1 += t1[q][cx];
+    o2 += t2[q][cx];
+  }
+  if (x <= W) {
+#pragma unroll 4
+    for (int y = ya; y < yb; ++y) {
+      o1 += ii1[(int64_t)y * W1 + x];
+      o2 += ii2[(int64_t)y * W1 + x];
+      ii1[(int64_t)y * W1 + x] = o1;
+      ii2[(int64_t)y * W1 + x] = o2;
+    }
   }
 }
 
@@ -248,54 +296,131 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 }
 
 // One workgroup = one work item: a 128 x 128 output tile of one problem, template rows
-// [ya, yb) of one column piece.  Wave w owns output rows y0 + 32w + [0, 32) and all four
-// 32-column blocks; A (frame rows, 16 contiguous int8 per lane) and the band fragment are
-// 16-byte global loads (the frame and the bands stay L2-resident).
-__global__ __launch_bounds__(256) void tm_corr_kernel(const int8_t* __restrict__ f8, int64_t pitch,
-                                                      const uint8_t* __restrict__ bands,
-                                                      const TmPiece* __restrict__ pieces,
-                                                      const TmWork* __restrict__ works,
-                                                      const TmProblem* __restrict__ probs, int* __restrict__ parts) {
+// [ya, ya + J) of one column piece.  8 waves (2 per SIMD): wave w owns output rows
+// y0 + 32 (w & 3) + [0, 32) and the 32-column blocks 2 (w >> 2) and 2 (w >> 2) + 1.
+// Operands live in LDS, filled by LDS-DMA two template rows ahead:
+//   * A ring: frame rows y0 + ya + q (q = 0 .. J + 126) in slot q % kTmRing, each row the
+//     32 (nkb + 3) bytes the tile reads, slot stride SA = 16 (mod 256) bytes, so the 16
+//     rows a ds_read_b128 lane group touches fall in distinct banks.  Iteration j reads
+//     slots j .. j + 127 and prefetches row j + 129 (one row per template row).
+//   * B ring: the band slice of template row ya + j (nkb KiB, lane-linear fragments) in
+//     stage j % 3, prefetched two rows ahead (A rows likewise).
+// One barrier per template row; a wave reads its NKB + 1 A and NKB B fragments of a
+// template row up front (compile-time NKB) for 2 NKB MFMAs.
+constexpr int kTmRing = 144;  // A-ring slots (>= 129; 144 * 16 = 0 mod 256 keeps banks aligned)
+constexpr int kTmMaxSA = 528;
+constexpr int kTmMaxNkb = (kTmPiece + 31 + 31) / 32;
+
+__global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restrict__ f8, int64_t pitch,
+                                                         const uint8_t* __restrict__ bands,
+                                                         const TmPiece* __restrict__ pieces,
+                                                         const TmWork* __restrict__ works,
+                                                         const TmProblem* __restrict__ probs, int* __restrict__ parts,
+                                                         int nwork) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kTmRing * kTmMaxSA + 3 * kTmMaxNkb * 1024 + 1024];
   const TmWork wk = works[blockIdx.x];
   const TmPiece pc = pieces[wk.piece];
   const TmProblem pb = probs[pc.prob];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr4 = wave & 3, wc = wave >> 2;  // 32-row block, column half (blocks 2wc, 2wc+1)
   const int r = lane & 31, h = lane >> 5;
   const int nkb = pc.nkb;
-  i32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
-  const int8_t* abase = f8 + (int64_t)(wk.y0 + 32 * wave + r) * pitch + wk.x0 + pc.px + 16 * h;
-  const uint8_t* bbase = bands + pc.band_off + lane * 16;
-  for (int yy = wk.ya; yy < wk.yb; ++yy) {
-    const int8_t* arow = abase + (int64_t)yy * pitch;
-    const uint8_t* brow = bbase + (int64_t)yy * nkb * 1024;
-    i32x4 b1 = {}, b2 = {}, b3 = {};
-    for (int kb = 0; kb < nkb + 3; ++kb) {
-      const i32x4 a = *reinterpret_cast<const i32x4*>(arow + 32 * kb);
-      const i32x4 b0 = kb < nkb ? *reinterpret_cast<const i32x4*>(brow + kb * 1024) : i32x4{};
-      acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b1, acc1, 0, 0, 0);
-      acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b2, acc2, 0, 0, 0);
-      acc3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b3, acc3, 0, 0, 0);
-      b3 = b2;
-      b2 = b1;
-      b1 = b0;
+  const int RW = 32 * (nkb + 3);   // A-row bytes a tile reads
+  const int SA = (RW + 255) / 256 * 256 + 16;  // slot stride = 16 (mod 256)
+  const int nl = RW / 16;          // DMA lanes per A row
+  const int J = wk.yb - wk.ya;
+  const unsigned lds = lds_addr(smem);
+  const unsigned ldsB = lds + (unsigned)(kTmRing * kTmMaxSA);
+  const unsigned ldsD = ldsB + (unsigned)(3 * kTmMaxNkb * 1024);  // dummy DMA target
+  const int8_t* arow0 = f8 + (int64_t)(wk.y0 + wk.ya) * pitch + wk.x0 + pc.px + 16 * lane;  // + q * pitch
+  const uint8_t* bsl0 = bands + pc.band_off + (int64_t)wk.ya * nkb * 1024 + 16 * lane;     // + j * nkb KiB
+  // Rows >= hr are skipped per wave (uniform); NKB is a compile-time constant so the
+  // k-block loop unrolls and every fragment read of a template row is issued up front.
+  const bool wact = wk.y0 + 32 * wr4 < pb.hr && wk.x0 + 64 * wc < pb.wr;
+  i32x16 acc0 = {}, acc1 = {};
+  auto run = [&](auto nkb_c) {
+    constexpr int NKB = decltype(nkb_c)::value;
+    constexpr int Q = (NKB + 1 + 7) / 8;  // DMA instructions per wave per template row
+    // Template row j's operands: B pieces 0 .. NKB-1 into stage j % 3 and A row q = j + 127
+    // (completing the window j .. j + 127); wave w issues pieces w, w + 4, ..., padded with
+    // harmless dummy DMAs to exactly Q instructions, so "row j landed" is one vmcnt(Q).
+    auto issue = [&](int j) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        const int p = wave + 8 * i;
+        if (p < NKB) {
+          glds16(bsl0 + ((int64_t)j * NKB + p) * 1024, ldsB + (unsigned)(((j % 3) * kTmMaxNkb + p) * 1024));
+        } else if (p == NKB) {
+          if (lane < nl) {
+            const int q = j + 127;
+            glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)((q % kTmRing) * SA));
+          }
+        } else {
+          glds16(bsl0, ldsD);
+        }
+      }
+    };
+    for (int q = wave; q < 127; q += 8)
+      if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)(q * SA));
+    issue(0);
+    if (J > 1) {
+      issue(1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");
+    } else {
+      dma_wait_all();
     }
+    __syncthreads();
+    for (int j = 0; j < J; ++j) {
+      const bool ahead = j + 2 < J;
+      if (ahead) issue(j + 2);
+      if (wact) {
+        // this wave's A starts 64 columns in for the second column half; block 2wc + n
+        // then uses B's k-block kb - n of its own A steps
+        const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 64 * wc + 16 * h;
+        const uint8_t* bst = smem + kTmRing * kTmMaxSA + (j % 3) * kTmMaxNkb * 1024 + 16 * lane;
+        i32x4 A[NKB + 1], B[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB + 1; ++kb) A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
+#pragma unroll
+        for (int kb = 0; kb < NKB + 1; ++kb) {
+          if (kb < NKB) acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb], acc0, 0, 0, 0);
+          if (kb >= 1) acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - 1], acc1, 0, 0, 0);
+        }
+      }
+      if (ahead)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");  // row j + 1 landed
+      else
+        dma_wait_all();
+      __syncthreads();  // ... for every wave; everyone is done with stage j % 3 and slot j
+    }
+  };
+  switch (nkb) {
+#define EF_TM_NKB(V) \
+  case V:            \
+    run(std::integral_constant<int, V>{}); \
+    break;
+    EF_TM_NKB(1) EF_TM_NKB(2) EF_TM_NKB(3) EF_TM_NKB(4) EF_TM_NKB(5) EF_TM_NKB(6)
+    EF_TM_NKB(7) EF_TM_NKB(8) EF_TM_NKB(9) EF_TM_NKB(10) EF_TM_NKB(11) EF_TM_NKB(12)
+#undef EF_TM_NKB
+    default:
+      break;
   }
+  if (!wact) return;
   int* out = parts + pb.part_off + (int64_t)wk.part * pb.hr * pb.wr;
   auto store = [&](const i32x16& v, int n) {
     const int x = wk.x0 + 32 * n + r;
     if (x >= pb.wr) return;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const int y = wk.y0 + 32 * wave + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int y = wk.y0 + 32 * wr4 + (g & 3) + 8 * (g >> 2) + 4 * h;
       if (y < pb.hr) out[(int64_t)y * pb.wr + x] = v[g];
     }
   };
-  store(acc0, 0);
-  store(acc1, 1);
-  store(acc2, 2);
-  store(acc3, 3);
+  store(acc0, 2 * wc);
+  store(acc1, 2 * wc + 1);
 }
 
 // OpenCV's TM_CCOEFF_NORMED rule (templmatch.cpp common_matchTemplate) on exact integers.
@@ -321,7 +446,8 @@ __device__ __forceinline__ unsigned long long tm_key(float v, unsigned idx) {
   return ((unsigned long long)(~o) << 32) | idx;
 }
 
-// grid (ceil(max positions / 256), nprob): score every position, optional map, arg-max.
+// grid (blocks per problem, nprob): score every position (grid-stride), optional map,
+// then one packed-key atomicMin per block for the first raster-order maximum.
 __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restrict__ probs,
                                                        const TmStat* __restrict__ st, const int* __restrict__ parts,
                                                        const long long* __restrict__ ii1,
@@ -329,32 +455,37 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
                                                        float* __restrict__ maps,
                                                        unsigned long long* __restrict__ keys) {
   const TmProblem pb = probs[blockIdx.y];
+  const TmStat ts = st[blockIdx.y];
   const int64_t npos = (int64_t)pb.hr * pb.wr;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const long long n = (long long)pb.th * pb.tw;
+  const int64_t W1 = W + 1;
   unsigned long long key = ~0ull;
-  if (i < npos) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npos; i += (int64_t)gridDim.x * 256) {
     const int y = (int)(i / pb.wr), x = (int)(i - (i / pb.wr) * pb.wr);
     long long P = 0;
     const int* pp = parts + pb.part_off + i;
     for (int q = 0; q < pb.nparts; ++q) P += pp[(int64_t)q * npos];
-    const int64_t W1 = W + 1;
-    auto box = [&](const long long* ii) {
-      return ii[(int64_t)(y + pb.th) * W1 + x + pb.tw] - ii[(int64_t)y * W1 + x + pb.tw] -
-             ii[(int64_t)(y + pb.th) * W1 + x] + ii[(int64_t)y * W1 + x];
-    };
-    const long long sI = box(ii1), sI2 = box(ii2);
-    const long long n = (long long)pb.th * pb.tw;
-    const TmStat ts = st[blockIdx.y];
+    const int64_t a = (int64_t)y * W1 + x, b = (int64_t)(y + pb.th) * W1 + x;
+    const long long sI = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
+    const long long sI2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
     const float v = tm_score(n * P - ts.sT * sI, n * sI2 - sI * sI, ts.varT);
     if (maps) maps[pb.map_off + i] = v;
-    key = tm_key(v, (unsigned)i);
+    const unsigned long long k = tm_key(v, (unsigned)i);
+    key = k < key ? k : key;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const unsigned long long o = __shfl_xor(key, off);
     key = o < key ? o : key;
   }
-  if ((threadIdx.x & 63) == 0 && key != ~0ull) atomicMin(keys + blockIdx.y, key);
+  __shared__ unsigned long long red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = key;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = red[0];
+    for (int w = 1; w < 4; ++w) m = red[w] < m ? red[w] : m;
+    if (m != ~0ull) atomicMin(keys + blockIdx.y, m);
+  }
 }
 
 __global__ void fill_u64_kernel(unsigned long long* p, int n) {
@@ -425,8 +556,11 @@ int ef_preprocess(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const 
     src = s;
     dst = reinterpret_cast<uint8_t*>(base + dbytes + rup(src_bytes, 256));
   }
+  TimerEvt tev;
+  timer_begin(c, EF_KERNEL_INGEST, &tev);
   EF_HIP(c, launch_resize(c->stream, src, ddesc, (int)count, (int64_t)out_h * out_w, flags & EF_IMG_RGB, dst),
          "resize kernel");
+  timer_end(c, &tev);
   if (!dev) {
     EF_HIP(c, hipMemcpyAsync(out, dst, obytes, hipMemcpyDeviceToHost, c->stream), "D2H faces");
   }
@@ -504,6 +638,10 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     }
     t->probs.push_back(pb);
   }
+  // longest work items first (template rows x k-blocks), so the short ones fill the tail
+  std::stable_sort(works.begin(), works.end(), [&](const TmWork& a, const TmWork& b) {
+    return (int64_t)(a.yb - a.ya) * (pieces[a.piece].nkb + 3) > (int64_t)(b.yb - b.ya) * (pieces[b.piece].nkb + 3);
+  });
   t->nwork = (int)works.size();
   t->max_pos = max_pos;
   t->map_total = map_total;
@@ -571,22 +709,19 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
   int8_t* f8 = static_cast<int8_t*>(t->f8.p);
   long long* ii1 = static_cast<long long*>(t->ii1.p);
   long long* ii2 = static_cast<long long*>(t->ii2.p);
-  const int64_t np = (int64_t)H * W;
   TimerEvt tev;
   timer_begin(c, EF_KERNEL_TMATCH, &tev);
-  hipLaunchKernelGGL(tm_frame_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, f, H, W, frame_ld, f8,
-                     t->pitch);
-  hipLaunchKernelGGL(tm_rowscan_kernel, dim3((unsigned)((H + 1 + 63) / 64)), dim3(64), 0, s, f8, H, W, t->pitch, ii1,
-                     ii2);
-  hipLaunchKernelGGL(tm_colscan_kernel, dim3((unsigned)((W + 1 + 63) / 64)), dim3(64), 0, s, H, W, ii1, ii2);
+  hipLaunchKernelGGL(tm_rows_kernel, dim3((unsigned)((H + 1 + 3) / 4)), dim3(256), 0, s, f, H, W, frame_ld, f8,
+                     t->pitch, ii1, ii2);
+  hipLaunchKernelGGL(tm_cols_kernel, dim3((unsigned)((W + 1 + 63) / 64)), dim3(1024), 0, s, H, W, ii1, ii2);
   if (t->nprob > 0) {
     unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
     hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((t->nprob + 255) / 256)), dim3(256), 0, s, keys, t->nprob);
     if (t->nwork > 0)
-      hipLaunchKernelGGL(tm_corr_kernel, dim3((unsigned)t->nwork), dim3(256), 0, s, f8, t->pitch,
+      hipLaunchKernelGGL(tm_corr_kernel, dim3((unsigned)t->nwork), dim3(512), 0, s, f8, t->pitch,
                          static_cast<const uint8_t*>(t->bands.p), static_cast<const TmPiece*>(t->d_pieces.p),
                          static_cast<const TmWork*>(t->d_works.p), static_cast<const TmProblem*>(t->d_probs.p),
-                         static_cast<int*>(t->parts.p));
+                         static_cast<int*>(t->parts.p), t->nwork);
     float* maps = nullptr;
     if (maps_out) {
       if (dev) {
@@ -596,7 +731,8 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
         maps = static_cast<float*>(t->maps.p);
       }
     }
-    hipLaunchKernelGGL(tm_score_kernel, dim3((unsigned)((t->max_pos + 255) / 256), (unsigned)t->nprob), dim3(256), 0,
+    const int64_t sblk = std::min<int64_t>((t->max_pos + 255) / 256, 32);
+    hipLaunchKernelGGL(tm_score_kernel, dim3((unsigned)sblk, (unsigned)t->nprob), dim3(256), 0,
                        s, static_cast<const TmProblem*>(t->d_probs.p), static_cast<const TmStat*>(t->d_stat.p),
                        static_cast<const int*>(t->parts.p), ii1, ii2, W, maps, keys);
     timer_end(c, &tev);

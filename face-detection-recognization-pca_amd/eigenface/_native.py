@@ -18,7 +18,7 @@ EF_FIT_STANDARDIZE = 0x1
 EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
-EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH = 0, 1, 2
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST = 0, 1, 2, 3
 EF_KEY_NONE = (1 << 63) - 1
 
 _ERRNAMES = {-1: "EF_E_INVALID", -2: "EF_E_HIP", -3: "EF_E_STATE", -4: "EF_E_NOMEM", -5: "EF_E_NUMERIC"}

@@ -58,6 +58,7 @@ extern "C" {
 #define EF_KERNEL_SEARCH 0  /* distance GEMM + fused arg-best   */
 #define EF_KERNEL_PROJECT 1 /* (p - mean).W projection GEMM     */
 #define EF_KERNEL_TMATCH 2  /* template localiser, one frame    */
+#define EF_KERNEL_INGEST 3  /* grey + resize of one image batch */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX

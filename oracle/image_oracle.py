@@ -52,6 +52,7 @@ __all__ = [
     "resize_linear",
     "preprocess",
     "match_template_ccoeff_normed",
+    "match_template_fft",
     "min_max_loc_max",
     "is_detection_in_corner",
     "scaled_sizes",
@@ -159,6 +160,31 @@ def _normalise(numN, varI, varT):
     with np.errstate(divide="ignore", invalid="ignore"):
         r = np.where(an < t, num / np.where(t > 0, t, 1.0),
                      np.where(an < t * 1.125, np.sign(num), 0.0))
+    return r.astype(np.float32)
+
+
+def match_template_fft(frame, templ):
+    """CPU baseline only (bench.py cpu_baseline leg): TM_CCOEFF_NORMED the way OpenCV
+    evaluates it on the CPU — the cross-correlation by FFT (float64 here, float32 DFT in
+    OpenCV), window sums from integral images, the same normalisation rule."""
+    from scipy.signal import fftconvolve
+    I = np.asarray(frame, dtype=np.float64)
+    T = np.asarray(templ, dtype=np.float64)
+    h, w = T.shape
+    n = h * w
+    corr = fftconvolve(I, T[::-1, ::-1], mode="valid")
+    Ii = np.asarray(frame, dtype=np.int64)
+    sI = _box(_integral(Ii), h, w).astype(np.float64)
+    sI2 = _box(_integral(Ii * Ii), h, w).astype(np.float64)
+    sT, sT2 = T.sum(), (T * T).sum()
+    varT = n * sT2 - sT * sT
+    if varT == 0:
+        return np.ones(corr.shape, np.float32)
+    num = n * corr - sT * sI
+    t = np.sqrt(np.maximum(n * sI2 - sI * sI, 0.0)) * np.sqrt(varT)
+    an = np.abs(num)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(an < t, num / np.where(t > 0, t, 1.0), np.where(an < t * 1.125, np.sign(num), 0.0))
     return r.astype(np.float32)
 
 
