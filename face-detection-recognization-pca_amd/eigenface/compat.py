@@ -11,10 +11,10 @@ Appendix A, §8a rows a1/a10/a11), backed by the GPU engine.
                                is installed (scan-template-v4.py:36-37, :265-266)
 * ``extract_face_features``, ``recognize_face_all_models`` — scan-template-v4.py:253-319
 
-Image decoding (a1) uses OpenCV when importable (the reference's exact path:
-``imread`` -> ``cvtColor(BGR2GRAY)`` -> ``resize(64, 64)``); otherwise Pillow with
-OpenCV's fixed-point BT.601 grey conversion and a bilinear resize restatement — that
-branch is *parity unpinned* (OpenCV is absent where this was built).
+Image ingest (a1): files are decoded on the host (OpenCV's ``imread`` when importable,
+else Pillow — both libjpeg), then ``cvtColor(BGR2GRAY)`` + ``resize(64, 64)`` run for the
+whole batch in one GPU launch with OpenCV's CV_8U fixed-point rules (``ef_preprocess``;
+*parity unpinned* against OpenCV itself, which is absent where this was built).
 """
 from __future__ import annotations
 
@@ -29,60 +29,45 @@ from .pca import EigenfacePCA, get_engine
 
 
 # ----------------------------------------------------------------------- images
-def _gray_resize_fallback(path, size):
-    from PIL import Image
-
-    im = Image.open(path)
-    if im.mode == "L":
-        g = np.asarray(im, dtype=np.uint8)
-    else:
-        rgb = np.asarray(im.convert("RGB"), dtype=np.int32)
-        # OpenCV CV_8U RGB->GRAY: (R*4899 + G*9617 + B*1868 + 8192) >> 14
-        g = ((rgb[..., 0] * 4899 + rgb[..., 1] * 9617 + rgb[..., 2] * 1868 + 8192) >> 14).astype(np.uint8)
-    return _resize_bilinear(g, size)
-
-
-def _resize_bilinear(img, size):
-    """cv2.resize(..., INTER_LINEAR) restatement for uint8 (half-pixel centres,
-    edge clamp, 11-bit weights, rounded).  Parity unpinned."""
-    w_out, h_out = size
-    h_in, w_in = img.shape
-    if (h_in, w_in) == (h_out, w_out):
-        return img.copy()
-
-    def axis(n_in, n_out):
-        f = (np.arange(n_out) + 0.5) * (n_in / n_out) - 0.5
-        i0 = np.floor(f).astype(np.int64)
-        a = f - i0
-        a = np.where(i0 < 0, 0.0, a)
-        i0 = np.clip(i0, 0, n_in - 1)
-        i1 = np.clip(i0 + 1, 0, n_in - 1)
-        w1 = np.rint(a * 2048).astype(np.int64)
-        return i0, i1, 2048 - w1, w1
-
-    y0, y1, wy0, wy1 = axis(h_in, h_out)
-    x0, x1, wx0, wx1 = axis(w_in, w_out)
-    src = img.astype(np.int64)
-    rows = src[:, x0] * wx0 + src[:, x1] * wx1              # (h_in, w_out), scale 2^11
-    val = rows[y0] * wy0[:, None] + rows[y1] * wy1[:, None]  # scale 2^22
-    return np.clip((val + (1 << 21)) >> 22, 0, 255).astype(np.uint8)
-
-
-def read_face(path, size=(64, 64)):
-    """Grey, resized, uint8 face (train-v4.py:59-66); None if unreadable."""
+def decode_image(path):
+    """cv2.imread(path) (IMREAD_COLOR, BGR uint8) or None if unreadable.  Decoding is
+    libjpeg either way: OpenCV when importable, else Pillow (RGB reversed to BGR)."""
     try:
-        import cv2  # noqa: F401
+        import cv2
     except ImportError:
         cv2 = None
     if cv2 is not None:
-        img = cv2.imread(path)
-        if img is None:
-            return None
-        return cv2.resize(cv2.cvtColor(img, cv2.COLOR_BGR2GRAY), size)
+        return cv2.imread(path)
     try:
-        return _gray_resize_fallback(path, size)
+        from PIL import Image
+        im = Image.open(path)
+        if im.mode == "L":
+            return np.asarray(im, dtype=np.uint8)
+        return np.ascontiguousarray(np.asarray(im.convert("RGB"), dtype=np.uint8)[..., ::-1])
     except (OSError, ValueError):
         return None
+
+
+def read_faces(paths, size=(64, 64), device=0):
+    """train-v4.py:59-68 for a list of files: decode on the host, then ONE GPU launch for
+    cvtColor(BGR2GRAY) + resize(size) of the whole batch (ef_preprocess).  Returns
+    (rows uint8 (m, h*w), kept indices) — unreadable files are skipped like the
+    reference's ``img is None`` branch."""
+    imgs, keep = [], []
+    for i, p in enumerate(paths):
+        im = decode_image(p)
+        if im is not None:
+            imgs.append(im)
+            keep.append(i)
+    if not imgs:
+        return np.zeros((0, size[0] * size[1]), np.uint8), keep
+    return get_engine(device).preprocess(imgs, size), keep
+
+
+def read_face(path, size=(64, 64), device=0):
+    """Grey, resized, uint8 face (train-v4.py:59-66); None if unreadable."""
+    rows, keep = read_faces([path], size, device)
+    return rows[0].reshape(size[1], size[0]) if keep else None
 
 
 def _save_jpg(path, arr2d):
@@ -152,7 +137,7 @@ class FaceTrainer:
         ``image_filename`` inside face_dir (train-v5.py:305-306) for Windows-style paths."""
         with open(json_path, "r", encoding="utf-8") as f:
             data = json.load(f)
-        images, valid = [], []
+        paths, infos = [], []
         for info in data["faces"]:
             path = info.get("image_path", "")
             if not os.path.exists(path):
@@ -161,15 +146,14 @@ class FaceTrainer:
                     print(f"Warning: Image {path} not found, skipping...")
                     continue
                 path = alt
-            g = read_face(path, self.face_shape)
-            if g is None:
-                print(f"Warning: Could not read image {path}, skipping...")
-                continue
-            images.append(g.flatten())
-            valid.append(info)
-        self.face_images = np.array(images, dtype=np.uint8).reshape(len(images), -1)
-        self.face_info = valid
-        return len(images)
+            paths.append(path)
+            infos.append(info)
+        rows, keep = read_faces(paths, self.face_shape, self.device)
+        for i in sorted(set(range(len(paths))) - set(keep)):
+            print(f"Warning: Could not read image {paths[i]}, skipping...")
+        self.face_images = rows
+        self.face_info = [infos[i] for i in keep]
+        return len(keep)
 
     def assign_labels_interactive(self, person_name):
         """All faces labelled as one person, id 0 (train-v4.py:78-108)."""
@@ -333,16 +317,11 @@ def _model_projection(md):
 
 def extract_face_features(face_img, model_data, device=0):
     """scan-template-v4.py:253-268 on the GPU: grey 64x64 face -> model features."""
-    g = np.asarray(face_img)
-    if g.ndim == 3:
-        g = ((g[..., 2].astype(np.int32) * 4899 + g[..., 1].astype(np.int32) * 9617 +
-              g[..., 0].astype(np.int32) * 1868 + 8192) >> 14).astype(np.uint8)
-    if g.shape != (64, 64):
-        g = _resize_bilinear(g.astype(np.uint8), (64, 64))
     eng = get_engine(device)
+    g = eng.preprocess([np.asarray(face_img, dtype=np.uint8)], (64, 64))  # grey + resize on the GPU
     mu, w = _model_projection(model_data)
     eng.set_model(mu, w)
-    return eng.project(g.reshape(1, -1).astype(np.uint8))[0].astype(np.float64)
+    return eng.project(g)[0].astype(np.float64)
 
 
 def recognize_face_all_models(face_img, models, threshold=0.8, device=0):

@@ -49,19 +49,15 @@ def test_sklearn_objects_roundtrip_transform():
     np.testing.assert_allclose(f, g["probe_features"], rtol=1e-9, atol=1e-8)
 
 
-def test_resize_and_gray_fallback(tmp_path):
+def test_decode_image_is_bgr(tmp_path):
+    """Host decode feeding the GPU ingest: BGR channel order like cv2.imread."""
     from PIL import Image
-    from eigenface.compat import _resize_bilinear, read_face
-    img = (np.arange(100 * 100) % 251).astype(np.uint8).reshape(100, 100)
-    np.testing.assert_array_equal(_resize_bilinear(img, (100, 100)), img)
-    flat = np.full((100, 100), 77, np.uint8)
-    np.testing.assert_array_equal(_resize_bilinear(flat, (64, 64)), np.full((64, 64), 77, np.uint8))
-    r = _resize_bilinear(img, (64, 64))
-    assert r.shape == (64, 64) and r.dtype == np.uint8
-    rgb = np.zeros((50, 50, 3), np.uint8)
+    from eigenface.compat import decode_image
+    rgb = np.zeros((50, 40, 3), np.uint8)
     rgb[..., 0], rgb[..., 1], rgb[..., 2] = 200, 100, 50
     Image.fromarray(rgb).save(tmp_path / "a.png")
-    g = read_face(str(tmp_path / "a.png"))
-    assert g.shape == (64, 64)
-    assert int(g[0, 0]) == (200 * 4899 + 100 * 9617 + 50 * 1868 + 8192) >> 14
-    assert read_face(str(tmp_path / "missing.png")) is None
+    g = decode_image(str(tmp_path / "a.png"))
+    assert g.shape == (50, 40, 3) and tuple(g[0, 0]) == (50, 100, 200)
+    Image.fromarray(rgb[..., 0]).save(tmp_path / "g.png")
+    assert decode_image(str(tmp_path / "g.png")).shape == (50, 40)
+    assert decode_image(str(tmp_path / "missing.png")) is None

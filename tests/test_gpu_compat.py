@@ -80,3 +80,26 @@ def test_train_manual_cli(tmp_path):
     from eigenface import recognize_face
     name, sim, ok = recognize_face(x[11].astype(np.float64), md, 0.7)
     assert name == "carol" and ok and sim > 0.9999
+
+
+def test_read_faces_gpu_ingest_matches_oracle(tmp_path):
+    """compat.read_faces: host decode + one GPU grey/resize launch == the OpenCV-rule
+    restatement (oracle/image_oracle.py); unreadable files are skipped."""
+    from PIL import Image
+    from eigenface.compat import read_face, read_faces
+    from oracle import image_oracle as io
+    rng = np.random.default_rng(9)
+    paths, ref = [], []
+    for i, shp in enumerate([(100, 100, 3), (224, 230, 3), (37, 53), (128, 128, 3)]):
+        a = rng.integers(0, 256, shp, dtype=np.uint8)
+        p = str(tmp_path / f"f{i}.png")
+        Image.fromarray(a).save(p)
+        paths.append(p)
+        bgr = a[..., ::-1] if a.ndim == 3 else a
+        ref.append(io.preprocess(bgr, (64, 64)))
+    paths.insert(2, str(tmp_path / "missing.png"))
+    rows, keep = read_faces(paths)
+    assert keep == [0, 1, 3, 4]
+    np.testing.assert_array_equal(rows, np.stack(ref))
+    np.testing.assert_array_equal(read_face(paths[0]).ravel(), ref[0])
+    assert read_face(paths[2]) is None
