@@ -17,6 +17,7 @@
 //   * eigenfaces: E = A^T.U (:91), unit columns (:94-95), sklearn svd_flip sign rule.
 #include <rocblas/rocblas.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -174,11 +175,12 @@ hipError_t tri_solve_right(ef_ctx* c, hipStream_t s, double* Y, int64_t dim, int
 // Wide-block subspace iteration (m > kJacobiMax): orthonormalise by CholQR every
 // iteration (G = Y^T.Y = L.L^T, Q = Y.L^-T — one small Cholesky instead of an m x m
 // eigensolve), Rayleigh-Ritz (H = Q^T.C.Q, grid Jacobi) at iterations 1, 2, 4 and every
-// kRRPeriod after: its Ritz values give the convergence test, its vectors re-order the
+// rr_period(dim) after: its Ritz values give the convergence test, its vectors re-order the
 // block (Y <- Y.V), and the converged RR is the final one.  A numerically rank-deficient
 // block (Cholesky pivot <= 1e-13 of the largest) falls back to the eigen-orthonormalisation
 // Q = Y.W.L^-1/2 for that iteration.
-constexpr int kRRPeriod = 8;
+// Rayleigh-Ritz period: a grid-Jacobi RR costs ~ a few iterations at dim ~ 16k, ~10 at dim ~ 2k
+inline int rr_period(int64_t dim) { return dim >= 12288 ? 8 : 16; }
 constexpr int kCholeskyMax = 512;  // launch_cholesky's LDS panel limit (wider: eigen-orthonormalise)
 
 int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int m, double* work, double* U_out,
@@ -234,8 +236,8 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
                          work, kWorkElems),
            "Y = C.Q");
-    // Rayleigh-Ritz at iterations 1, 2, 4, then every kRRPeriod
-    const bool rr = it <= 2 || it == 4 || it % kRRPeriod == 0 || it == kMaxIters;
+    // Rayleigh-Ritz at iterations 1, 2, 4, 8, then every rr_period(dim)
+    const bool rr = it <= 2 || it == 4 || it == 8 || it % rr_period(dim) == 0 || it == kMaxIters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
                            work, kWorkElems),
@@ -299,14 +301,18 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
   // Block subspace iteration of width m: Y = C.Q; G = Y^T.Y = W.L.W^T; Q = Y.W.L^-1/2
   // (orthonormal, Ritz-ordered); k <= 80 keeps the historical m = kJacobiMax (LDS Jacobi),
   // wider k uses m = 2k (even, <= dim) on the grid Jacobi.
-  int m = kJacobiMax;
-  if (kk > kJacobiMax - 8) {
-    int64_t mm = 2 * (int64_t)kk;  // Ritz values converge as (lambda_{m+1} / lambda_k)^2
-    mm = (mm + 7) / 8 * 8;
-    if (mm > dim) mm = dim & ~int64_t(1);
-    m = (int)mm;
+  // Block width m = max(2k, 88) (Ritz values converge as (lambda_{m+1} / lambda_k)^2 per
+  // iteration), even, <= dim: CholQR subspace iteration with periodic Rayleigh-Ritz.
+  int64_t mm = std::max<int64_t>(2 * (int64_t)kk, kJacobiMax);
+  mm = (mm + 7) / 8 * 8;
+  if (mm > dim) mm = dim & ~int64_t(1);
+  int m = (int)mm;
+  if (const char* em = getenv("EF_FIT_M")) {  // experiments only
+    const int64_t e = atoi(em);
+    if (e >= kk + 2 && e <= dim) m = (int)(e & ~int64_t(1));
   }
-  if (m > kJacobiMax) return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
+  const char* ep = getenv("EF_FIT_PATH");
+  if (!(ep && ep[0] == 'n')) return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
   SmallEig se;
   EF_TRY(se.init(c, B, m));
   double *Q, *Y, *G, *Wm, *W2, *lam;

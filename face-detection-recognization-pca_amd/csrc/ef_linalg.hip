@@ -413,8 +413,95 @@ __global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int 
   if (tid == 0) *info = 0;
 }
 
+// Small orders (m <= 128): the whole factorisation in one workgroup with the matrix in
+// registers — thread (bi, bj) of a 32 x 32 grid owns the 4 x 4 block of rows 4bi.., columns
+// 4bj..  Step t: the owners of column t publish it (already final) to LDS, one barrier,
+// then every thread applies the rank-1 update  A[i][l] -= A[i][t] A[l][t] / A[t][t]  to its
+// entries with l > t (unscaled column; the diagonal's square root and the column scaling
+// are applied at the end).  One barrier per column, no global traffic inside the loop.
+constexpr int kCholSmall = 128;
+__global__ __launch_bounds__(1024) void chol_small_kernel(double* __restrict__ A, int m, int64_t lda, double tol_rel,
+                                                          int* __restrict__ info) {
+  __shared__ double col[2][kCholSmall];
+  __shared__ double red[32];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  const int bi = tid >> 5, bj = tid & 31;
+  double a[4][4];
+  double dmax = 0.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = 4 * bi + u, l = 4 * bj + v;
+      a[u][v] = (i < m && l < m) ? A[(int64_t)i * lda + l] : 0.0;
+      if (i == l && i < m) dmax = fmax(dmax, a[u][v]);
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, off));
+  if ((tid & 63) == 0) red[tid >> 6] = dmax;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  double mx = 0.0;
+  for (int w = 0; w < 16; ++w) mx = fmax(mx, red[w]);
+  const double tol = tol_rel * mx;
+  for (int t = 0; t < m; ++t) {
+    const int buf = t & 1;
+    if (bj == (t >> 2)) {  // publish column t (rows 4bi..4bi+3)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (v == (t & 3)) col[buf][4 * bi + u] = a[u][v];
+    }
+    __syncthreads();
+    const double d = col[buf][t];
+    if (!(d > tol)) {
+      if (tid == 0) *info = -(t + 1);
+      return;  // uniform: every thread read the same d
+    }
+    const double inv = 1.0 / d;
+    if (4 * bj + 3 > t && 4 * bi + 3 > t) {
+      double ci[4], cl[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ci[u] = col[buf][4 * bi + u];
+        cl[u] = col[buf][4 * bj + u] * inv;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = 4 * bi + u, l = 4 * bj + v;
+          if (l > t && i >= l) a[u][v] = fma(-ci[u], cl[v], a[u][v]);
+        }
+    }
+  }
+  // L[i][l] = a[i][l] / sqrt(a[l][l]) for l <= i (the diagonal becomes its square root);
+  // the diagonal is published once more through LDS
+  __syncthreads();
+  if (bi == bj) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) col[0][4 * bi + u] = a[u][u];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = 4 * bi + u, l = 4 * bj + v;
+      if (i < m && l < m) A[(int64_t)i * lda + l] = l <= i ? a[u][v] / sqrt(col[0][l]) : 0.0;
+    }
+  if (tid == 0) *info = 0;
+  (void)bad;
+}
+
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info) {
   if (m < 1 || m > kCholMaxM) return hipErrorInvalidValue;
+  if (m <= kCholSmall) {
+    hipLaunchKernelGGL(chol_small_kernel, dim3(1), dim3(1024), 0, s, A, m, lda, tol_rel, info);
+    return hipGetLastError();
+  }
   static bool attr_set = false;
   const size_t lds = (size_t)kCholMaxM * kCholPS * sizeof(double);
   if (!attr_set) {
