@@ -291,6 +291,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary fit timing")
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
+    ap.add_argument("--gallery", type=int, default=0, help="override the gallery size (per-rank studies)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +311,8 @@ def main():
     from eigenface.distributed import ShardedGallery, shard_range
 
     n_total, side, k, bsz, precision = CONFIGS[args.config]
+    if args.gallery:
+        n_total = args.gallery
     d = side * side
     lo, hi = shard_range(n_total, rank, world)
 
