@@ -280,6 +280,86 @@ def image_bench(eng, with_cpu: bool, frames=20):
     return res
 
 
+# Stage sizes of a 25-stage frontal-face cascade like OpenCV's default one (2913 stumps);
+# the cascade itself ships inside OpenCV, which is absent here, so the bench synthesises
+# one of that shape and calibrates its stage thresholds so ~60 % of the windows reaching
+# a stage pass it (a realistic early-rejection profile).
+FRONTAL_STAGES = [9, 16, 27, 32, 52, 53, 62, 72, 83, 91, 99, 115, 127, 135, 136, 137, 159, 155, 169, 196, 197,
+                  181, 199, 211, 200]
+
+
+def synth_frontal_cascade(frame, n_feat=2135, seed=7, keep=0.6, n_windows=4000):
+    rng = np.random.default_rng(seed)
+    feats = []
+    for _ in range(n_feat):
+        w, h = int(rng.integers(1, 12)), int(rng.integers(1, 24))
+        x, y = int(rng.integers(0, 24 - 2 * w + 1)), int(rng.integers(0, 24 - h + 1))
+        feats.append([(x, y, 2 * w, h, -1.0), (x + w, y, w, h, 2.0)])
+    # normalised feature values of random base-layer windows (HaarEvaluator arithmetic)
+    H, W = frame.shape
+    ii = np.zeros((H + 1, W + 1), np.int64)
+    ii[1:, 1:] = frame.astype(np.int64).cumsum(0).cumsum(1)
+    sq = np.zeros((H + 1, W + 1), np.int64)
+    sq[1:, 1:] = (frame.astype(np.int64) ** 2).cumsum(0).cumsum(1)
+    ys, xs = rng.integers(0, H - 24, n_windows), rng.integers(0, W - 24, n_windows)
+
+    def box(a, x, y, w, h):
+        return a[ys + y + h, xs + x + w] - a[ys + y, xs + x + w] - a[ys + y + h, xs + x] + a[ys + y, xs + x]
+    area = 22.0 * 22.0
+    nf = area * box(sq, 1, 1, 22, 22) - box(ii, 1, 1, 22, 22).astype(np.float64) ** 2
+    vnf = (1.0 / np.sqrt(np.maximum(nf, 1.0))).astype(np.float32)
+    stages, alive, fi = [], np.ones(n_windows, bool), 0
+    for n in FRONTAL_STAGES:
+        stumps, tot = [], np.zeros(n_windows)
+        for _ in range(n):
+            f = feats[fi % n_feat]
+            fi += 1
+            val = sum(np.float32(wt) * box(ii, x, y, w, h).astype(np.float32) for x, y, w, h, wt in f) * vnf
+            thr = float(np.float32(np.median(val[alive]) if alive.any() else 0.0))
+            left, right = float(np.float32(rng.uniform(-1, 0))), float(np.float32(rng.uniform(0, 1)))
+            stumps.append((int((fi - 1) % n_feat), thr, left, right))
+            tot += np.where(val < thr, left, right)
+        sthr = float(np.float32(np.quantile(tot[alive], 1 - keep))) if alive.any() else 0.0
+        alive &= tot >= sthr
+        stages.append((sthr, stumps))
+    return {"win": (24, 24), "features": feats, "stages": stages}
+
+
+def haar_bench(eng, with_cpu: bool, frames=10):
+    """detection-v4.py:50-55 on a 640x480 grey frame: detectMultiScale(1.1, 5, (30, 30))
+    with a synthetic 25-stage / 2913-stump frontal-face-shaped cascade."""
+    import torch  # noqa: F401
+    from eigenface.haar import CascadeClassifier
+    rng = np.random.default_rng(11)
+    H, W = 480, 640
+    yy, xx = np.mgrid[0:H, 0:W]
+    f = 100 + 50 * np.sin(xx / 23.0) * np.cos(yy / 31.0) + rng.normal(0, 12, (H, W))
+    frame = np.clip(np.rint(f), 0, 255).astype(np.uint8)
+    casc = synth_frontal_cascade(frame)
+    clf = CascadeClassifier(cascade=casc, engine=eng)
+    rects, cand = clf.detect(frame, 1.1, 5, (30, 30), return_candidates=True)
+    eng.timing_reset()
+    t = time.perf_counter()
+    for _ in range(frames):
+        clf.detect(frame, 1.1, 5, (30, 30))
+    dt = (time.perf_counter() - t) / frames
+    k_ms, k_n = eng.timing_get("haar")
+    out = {"config": "640x480 grey frame, scaleFactor 1.1, minNeighbors 5, minSize 30x30, synthetic 25-stage "
+                     "2913-stump cascade (60 % pass per stage)",
+           "frames_per_s": round(1 / dt, 2), "ms_per_frame_host": round(dt * 1e3, 4),
+           "ms_per_frame_device": round(k_ms / max(k_n, 1), 4), "candidates": int(len(cand)),
+           "detections": int(len(rects))}
+    if with_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import haar_oracle as ho
+        small = frame[:120, :160]
+        t = time.perf_counter()
+        ho.detect_multi_scale(small, casc, 1.1, 5, (30, 30))
+        out["cpu"] = {"frames_per_s_160x120": round(1 / (time.perf_counter() - t), 3), "cores": 1, "kind": "port",
+                      "sample": "one 160x120 crop through the NumPy restatement (OpenCV itself is absent)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -426,6 +506,7 @@ def main():
             eng.use_own_stream()
             eng.timing(True)
             rec.update(image_bench(eng, not args.no_cpu))
+            rec["haar"] = haar_bench(eng, not args.no_cpu)
             eng.timing(False)
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)

@@ -193,6 +193,7 @@ void ef_destroy(ef_ctx* c) {
   for (DevBuf* b : bufs) release(*b);
   blas_release(c);
   tm_release(c);
+  haar_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -435,7 +436,7 @@ static int timing_drain(ef_ctx* c) {
   EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
   for (auto& t : c->pending) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess && t.kernel >= 0 && t.kernel < 4) {
+    if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess && t.kernel >= 0 && t.kernel < 8) {
       c->t_ms[t.kernel] += ms;
       c->t_n[t.kernel] += 1;
     }
@@ -447,7 +448,7 @@ static int timing_drain(ef_ctx* c) {
 }
 
 int ef_timing_get(ef_ctx* c, int32_t kernel, double* total_ms, int64_t* launches) {
-  if (!c || kernel < 0 || kernel >= 4) return EF_E_INVALID;
+  if (!c || kernel < 0 || kernel >= 8) return EF_E_INVALID;
   EF_TRY(timing_drain(c));
   if (total_ms) *total_ms = c->t_ms[kernel];
   if (launches) *launches = c->t_n[kernel];
@@ -457,7 +458,7 @@ int ef_timing_get(ef_ctx* c, int32_t kernel, double* total_ms, int64_t* launches
 int ef_timing_reset(ef_ctx* c) {
   if (!c) return EF_E_INVALID;
   EF_TRY(timing_drain(c));
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 8; ++i) {
     c->t_ms[i] = 0;
     c->t_n[i] = 0;
   }

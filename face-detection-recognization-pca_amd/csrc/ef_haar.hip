@@ -1,0 +1,589 @@
+// Haar cascade face detector: the
+//     face_cascade.detectMultiScale(gray, scaleFactor=1.1, minNeighbors=5, minSize=(30, 30))
+// of detection-v4.py:18, :50-55, evaluated the way OpenCV 4.x's CascadeClassifierImpl runs
+// a stump-based HAAR cascade (cascadedetect.cpp), for a cascade the caller loads (the
+// reference's haarcascade_frontalface_default.xml ships inside OpenCV, which is absent
+// here, so parity is unpinned; tests use synthetic cascades against oracle/haar_oracle.py).
+//
+// Per frame, all on the GPU except the final rectangle grouping:
+//   1. pyramid: one ragged resize launch builds every layer (W/s, H/s) of the scale list
+//      (INTER_LINEAR rules of ef_image.hip; OpenCV uses INTER_LINEAR_EXACT here — the one
+//      documented deviation);
+//   2. integral images of every layer (int32, as OpenCV's CV_32S sum) and of its squares
+//      (uint32 with wrap-around, as OpenCV's: window sums are differences mod 2^32 and a
+//      window's sum of squares fits); row scan per wave, column scan per 64-column strip;
+//   3. `haar_stage0_kernel`: one thread per window origin of every layer — variance
+//      normalisation (HaarEvaluator::setWindow: nf = area * sqsum - sum^2 over the window
+//      shrunk by one pixel, 1/sqrt(nf) as float, reject when area / sqrt(nf) >= 0.1) and
+//      the first stage, result -1 / 0 / 1;
+//   4. `haar_rows_kernel`: CascadeClassifierInvoker's scan order — a stage-0 rejection
+//      skips the next x position — resolved per (layer, row) from the stage-0 results,
+//      compacting the surviving windows into a work list;
+//   5. `haar_cascade_kernel`: the remaining stages in groups (1-2, 3-5, 6-9, 10-14, 15-..),
+//      one launch per group over the compacted survivors of the previous one (thread per
+//      window), so waves stay full as the cascade rejects; accepted windows appended as
+//      candidates;
+// then the host sorts the candidates into OpenCV's (scale, y, x) order and runs
+// cv::groupRectangles(minNeighbors, eps = 0.2) (connected components of SimilarRects,
+// averaged rectangles, neighbour threshold, nested-rectangle filter).
+// Float arithmetic follows predictOrderedStump: feature = w0*S0 + w1*S1 (+ w2*S2) in
+// float (no contraction), times the float normalisation factor, compared with the stump
+// threshold; the stage sum accumulates the float leaves in double.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "ef_internal.hpp"
+
+namespace ef {
+
+#define EF_TRY(expr)              \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != EF_OK) return _rc; \
+  } while (0)
+#define EF_HIP(ctx, expr, what)                          \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return hip_err(ctx, _e, what); \
+  } while (0)
+
+struct HaarFeat {
+  int x[3], y[3], w[3], h[3];
+  float wt[3];
+  int nr;
+};
+struct HaarStump {
+  int feat;
+  float thr, left, right;
+};
+struct HaarStage {
+  int first, count;
+  float thr;
+  int pad;
+};
+struct HaarLayer {
+  int w, h, nx, ny, step;
+  float scale;
+  int64_t pix_off, ii_off, res_off;
+};
+struct HaarCand {
+  int layer, y, x, pad;
+};
+
+// ------------------------------------------------------------------ integral images
+// Row prefix sums of one layer row per wave (row 0 of the integral image is zero).
+__global__ __launch_bounds__(256) void haar_rows_ii_kernel(const uint8_t* __restrict__ pix,
+                                                           const HaarLayer* __restrict__ L, int* __restrict__ ii1,
+                                                           unsigned* __restrict__ ii2) {
+  const HaarLayer ly = L[blockIdx.y];
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row > ly.h) return;
+  const int64_t W1 = ly.w + 1;
+  int* r1 = ii1 + ly.ii_off + row * W1;
+  unsigned* r2 = ii2 + ly.ii_off + row * W1;
+  if (row == 0) {
+    for (int x = lane; x <= ly.w; x += 64) r1[x] = 0, r2[x] = 0u;
+    return;
+  }
+  const uint8_t* src = pix + ly.pix_off + (int64_t)(row - 1) * ly.w;
+  const int per = (ly.w + 63) / 64, xb = lane * per;
+  int s1 = 0;
+  unsigned s2 = 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb + i;
+    if (x < ly.w) {
+      const int v = src[x];
+      s1 += v;
+      s2 += (unsigned)(v * v);
+    }
+  }
+  int e1 = s1;
+  unsigned e2 = s2;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t1 = __shfl_up(e1, off);
+    const unsigned t2 = __shfl_up(e2, off);
+    if (lane >= off) {
+      e1 += t1;
+      e2 += t2;
+    }
+  }
+  e1 -= s1;
+  e2 -= s2;
+  if (lane == 0) r1[0] = r2[0] = 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = xb + i;
+    if (x < ly.w) {
+      const int v = src[x];
+      e1 += v;
+      e2 += (unsigned)(v * v);
+      r1[x + 1] = e1;
+      r2[x + 1] = e2;
+    }
+  }
+}
+
+// Column prefix: block = 64 columns x 16 row segments of one layer.
+__global__ __launch_bounds__(1024) void haar_cols_ii_kernel(const HaarLayer* __restrict__ L, int* __restrict__ ii1,
+                                                            unsigned* __restrict__ ii2) {
+  const HaarLayer ly = L[blockIdx.y];
+  __shared__ int t1[16][64];
+  __shared__ unsigned t2[16][64];
+  const int cx = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + cx;
+  if (blockIdx.x * 64 > ly.w) return;  // uniform per block
+  const int64_t W1 = ly.w + 1;
+  int* a1 = ii1 + ly.ii_off;
+  unsigned* a2 = ii2 + ly.ii_off;
+  const int per = (ly.h + 15) / 16;
+  const int ya = 1 + sg * per, yb = ya + per < ly.h + 1 ? ya + per : ly.h + 1;
+  int s1 = 0;
+  unsigned s2 = 0;
+  if (x <= ly.w)
+    for (int y = ya; y < yb; ++y) {
+      s1 += a1[y * W1 + x];
+      s2 += a2[y * W1 + x];
+    }
+  t1[sg][cx] = s1;
+  t2[sg][cx] = s2;
+  __syncthreads();
+  int o1 = 0;
+  unsigned o2 = 0;
+  for (int q = 0; q < sg; ++q) {
+    o1 += t1[q][cx];
+    o2 += t2[q][cx];
+  }
+  if (x <= ly.w)
+    for (int y = ya; y < yb; ++y) {
+      o1 += a1[y * W1 + x];
+      o2 += a2[y * W1 + x];
+      a1[y * W1 + x] = o1;
+      a2[y * W1 + x] = o2;
+    }
+}
+
+// ------------------------------------------------------------------ cascade evaluation
+template <typename T>
+__device__ __forceinline__ T box(const T* ii, int64_t W1, int x, int y, int w, int h) {
+  return ii[(int64_t)(y + h) * W1 + x + w] - ii[(int64_t)y * W1 + x + w] - ii[(int64_t)(y + h) * W1 + x] +
+         ii[(int64_t)y * W1 + x];
+}
+
+// HaarEvaluator::setWindow: the float normalisation factor, or 0 for a rejected window.
+__device__ __forceinline__ float haar_norm(const int* ii1, const unsigned* ii2, int64_t W1, int x, int y, int ww,
+                                           int wh) {
+  const double area = (double)((ww - 2) * (wh - 2));
+  const int s = box(ii1, W1, x + 1, y + 1, ww - 2, wh - 2);
+  const unsigned q = box(ii2, W1, x + 1, y + 1, ww - 2, wh - 2);
+  const double nf = __dsub_rn(__dmul_rn(area, (double)q), __dmul_rn((double)s, (double)s));
+  if (!(nf > 0.0)) return 0.f;
+  const float v = __double2float_rn(__ddiv_rn(1.0, sqrt(nf)));
+  return __dmul_rn(area, (double)v) < 0.1 ? v : 0.f;
+}
+
+// One stage (predictOrderedStump's inner loop): true when the window passes it.
+__device__ __forceinline__ bool haar_stage(const int* ii1, int64_t W1, int x, int y, float vnf,
+                                           const HaarStage& st, const HaarStump* __restrict__ stumps,
+                                           const HaarFeat* __restrict__ feats) {
+  double tmp = 0.0;
+  for (int i = 0; i < st.count; ++i) {
+    const HaarStump sp = stumps[st.first + i];
+    const HaarFeat& f = feats[sp.feat];
+    float val = __fmul_rn(f.wt[0], (float)box(ii1, W1, x + f.x[0], y + f.y[0], f.w[0], f.h[0]));
+    val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(ii1, W1, x + f.x[1], y + f.y[1], f.w[1], f.h[1])));
+    if (f.wt[2] != 0.f)
+      val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(ii1, W1, x + f.x[2], y + f.y[2], f.w[2], f.h[2])));
+    val = __fmul_rn(val, vnf);
+    tmp = __dadd_rn(tmp, (double)(val < sp.thr ? sp.left : sp.right));
+  }
+  return !(tmp < (double)st.thr);
+}
+
+// Pass 1: variance + first stage for every window origin of every layer (grid (pos/256,
+// layers)); res = -1 (low variance), 0 (rejected by stage 0), 1 (passed stage 0).
+__global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __restrict__ L,
+                                                          const int* __restrict__ ii1,
+                                                          const unsigned* __restrict__ ii2,
+                                                          const HaarStage* __restrict__ stages,
+                                                          const HaarStump* __restrict__ stumps,
+                                                          const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                          signed char* __restrict__ res) {
+  const HaarLayer ly = L[blockIdx.y];
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (int64_t)ly.nx * ly.ny) return;
+  const int y = (int)(p / ly.nx), x = (int)(p - (p / ly.nx) * ly.nx);
+  const int64_t W1 = ly.w + 1;
+  const int* a1 = ii1 + ly.ii_off;
+  const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, x, y, ww, wh);
+  signed char r = -1;
+  if (vnf != 0.f) r = haar_stage(a1, W1, x, y, vnf, stages[0], stumps, feats) ? 1 : 0;
+  res[ly.res_off + p] = r;
+}
+
+// Pass 2: the invoker's x walk for each (layer, evaluated row): positions 0, step, ...
+// with one extra step after a stage-0 rejection; survivors of stage 0 go to the list.
+__global__ void haar_rows_kernel(const HaarLayer* __restrict__ L, int nlayers, const int* __restrict__ row_start,
+                                 const signed char* __restrict__ res, HaarCand* __restrict__ work,
+                                 int* __restrict__ nwork, int cap) {
+  const int gr = blockIdx.x * blockDim.x + threadIdx.x;  // global evaluated-row index
+  if (gr >= row_start[nlayers]) return;
+  int li = 0;
+  while (row_start[li + 1] <= gr) ++li;
+  const HaarLayer ly = L[li];
+  const int y = (gr - row_start[li]) * ly.step;
+  const signed char* rr = res + ly.res_off + (int64_t)y * ly.nx;
+  for (int x = 0; x < ly.nx; x += ly.step) {
+    const signed char r = rr[x];
+    if (r > 0) {
+      const int k = atomicAdd(nwork, 1);
+      if (k < cap) work[k] = HaarCand{li, y, x, 0};
+    }
+    if (r == 0) x += ly.step;
+  }
+}
+
+// Pass 3: stages [s0, s1) for each window of the input list; survivors go to the output
+// list (the candidates after the last group).  Grid sized by the host's upper bound, the
+// live count read from device memory.
+__global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __restrict__ L,
+                                                           const int* __restrict__ ii1,
+                                                           const unsigned* __restrict__ ii2,
+                                                           const HaarStage* __restrict__ stages, int s0, int s1,
+                                                           const HaarStump* __restrict__ stumps,
+                                                           const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                           const HaarCand* __restrict__ in, const int* __restrict__ nin,
+                                                           int cap, HaarCand* __restrict__ out, int* __restrict__ nout) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n = min(*nin, cap);
+  if (i >= n) return;
+  const HaarCand w = in[i];
+  const HaarLayer ly = L[w.layer];
+  const int64_t W1 = ly.w + 1;
+  const int* a1 = ii1 + ly.ii_off;
+  const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
+  for (int s = s0; s < s1; ++s)
+    if (!haar_stage(a1, W1, w.x, w.y, vnf, stages[s], stumps, feats)) return;
+  const int k = atomicAdd(nout, 1);
+  if (k < cap) out[k] = w;
+}
+
+// ------------------------------------------------------------------ host side
+struct HaarState {
+  int ww = 0, wh = 0, nstages = 0;
+  DevBuf feats, stumps, stages;
+  DevBuf pix, ii1, ii2, res, layers, rowstart, work, cand, counters, frame, desc;
+};
+
+void haar_release(ef_ctx* c) {
+  if (!c || !c->haar) return;
+  HaarState* h = static_cast<HaarState*>(c->haar);
+  DevBuf* bufs[] = {&h->feats, &h->stumps, &h->stages, &h->pix, &h->ii1,      &h->ii2,     &h->res,
+                    &h->layers, &h->rowstart, &h->work, &h->cand, &h->counters, &h->frame, &h->desc};
+  for (DevBuf* b : bufs) release(*b);
+  delete h;
+  c->haar = nullptr;
+}
+
+static int cv_round(double v) { return (int)std::lrint(v); }
+
+struct RectI {
+  int x, y, w, h;
+};
+
+// cv::groupRectangles(rects, thr, eps): SimilarRects components numbered by lowest member,
+// averaged per class, classes with <= thr members dropped, then the nested-rectangle filter.
+static std::vector<RectI> group_rectangles(const std::vector<RectI>& rects, int thr, double eps) {
+  if (thr <= 0 || rects.empty()) return rects;
+  const int n = (int)rects.size();
+  std::vector<int> parent(n);
+  for (int i = 0; i < n; ++i) parent[i] = i;
+  auto find = [&](int i) {
+    while (parent[i] != i) {
+      parent[i] = parent[parent[i]];
+      i = parent[i];
+    }
+    return i;
+  };
+  auto similar = [&](const RectI& a, const RectI& b) {
+    const double delta = eps * (std::min(a.w, b.w) + std::min(a.h, b.h)) * 0.5;
+    return std::abs(a.x - b.x) <= delta && std::abs(a.y - b.y) <= delta &&
+           std::abs(a.x + a.w - b.x - b.w) <= delta && std::abs(a.y + a.h - b.y - b.h) <= delta;
+  };
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (similar(rects[i], rects[j])) {
+        const int ri = find(i), rj = find(j);
+        if (ri != rj) parent[std::max(ri, rj)] = std::min(ri, rj);
+      }
+  std::vector<int> label(n), cls_of_root(n, -1);
+  int nc = 0;
+  for (int i = 0; i < n; ++i) {
+    const int r = find(i);
+    if (cls_of_root[r] < 0) cls_of_root[r] = nc++;
+    label[i] = cls_of_root[r];
+  }
+  std::vector<long long> acc((size_t)nc * 4, 0);
+  std::vector<int> cnt(nc, 0);
+  for (int i = 0; i < n; ++i) {
+    long long* a = &acc[(size_t)label[i] * 4];
+    a[0] += rects[i].x;
+    a[1] += rects[i].y;
+    a[2] += rects[i].w;
+    a[3] += rects[i].h;
+    cnt[label[i]]++;
+  }
+  std::vector<RectI> rr(nc);
+  for (int c = 0; c < nc; ++c) {
+    const float s = 1.f / (float)cnt[c];
+    const long long* a = &acc[(size_t)c * 4];
+    rr[c] = RectI{(int)std::lrint((float)a[0] * s), (int)std::lrint((float)a[1] * s), (int)std::lrint((float)a[2] * s),
+                  (int)std::lrint((float)a[3] * s)};
+  }
+  std::vector<RectI> out;
+  for (int i = 0; i < nc; ++i) {
+    const RectI r1 = rr[i];
+    const int n1 = cnt[i];
+    if (n1 <= thr) continue;
+    int j = 0;
+    for (; j < nc; ++j) {
+      const int n2 = cnt[j];
+      if (j == i || n2 <= thr) continue;
+      const RectI r2 = rr[j];
+      const int dx = cv_round(r2.w * eps), dy = cv_round(r2.h * eps);
+      if (r1.x >= r2.x - dx && r1.y >= r2.y - dy && r1.x + r1.w <= r2.x + r2.w + dx &&
+          r1.y + r1.h <= r2.y + r2.h + dy && (n2 > std::max(3, n1) || n1 < 3))
+        break;
+    }
+    if (j == nc) out.push_back(r1);
+  }
+  return out;
+}
+
+// The ImgDesc / resize launcher of ef_image.hip (same translation-unit-free interface).
+hipError_t launch_resize_gray(hipStream_t s, const uint8_t* src, const void* desc_dev, int count, int64_t max_out,
+                              uint8_t* dst);
+size_t img_desc_size();
+void img_desc_fill(void* d, int64_t src_off, int64_t dst_off, int h, int w, int c, int oh, int ow);
+
+}  // namespace ef
+
+using namespace ef;
+
+extern "C" {
+
+int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_features, const int32_t* rects,
+                        const float* weights, int32_t n_stages, const int32_t* stage_count,
+                        const float* stage_threshold, int32_t n_stumps, const int32_t* stump_feature,
+                        const float* stump_threshold, const float* stump_left, const float* stump_right) {
+  if (!c) return EF_E_INVALID;
+  if (win_w < 3 || win_h < 3 || n_features < 1 || n_stages < 1 || n_stumps < 1 || !rects || !weights ||
+      !stage_count || !stage_threshold || !stump_feature || !stump_threshold || !stump_left || !stump_right)
+    return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: bad arguments");
+  std::vector<HaarFeat> f((size_t)n_features);
+  for (int i = 0; i < n_features; ++i) {
+    HaarFeat& q = f[i];
+    q.nr = 0;
+    for (int k = 0; k < 3; ++k) {
+      const int* r = rects + ((size_t)i * 3 + k) * 4;
+      q.x[k] = r[0], q.y[k] = r[1], q.w[k] = r[2], q.h[k] = r[3];
+      q.wt[k] = weights[(size_t)i * 3 + k];
+      if (k == 2 && q.wt[k] == 0.f) q.x[k] = q.y[k] = q.w[k] = q.h[k] = 0;
+      if (q.wt[k] != 0.f || k < 2) {
+        if (q.x[k] < 0 || q.y[k] < 0 || q.w[k] < 0 || q.h[k] < 0 || q.x[k] + q.w[k] > win_w ||
+            q.y[k] + q.h[k] > win_h)
+          return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: feature " + std::to_string(i) +
+                                              " has a rectangle outside the window (tilted features are not supported)");
+        ++q.nr;
+      }
+    }
+  }
+  std::vector<HaarStage> st((size_t)n_stages);
+  int first = 0;
+  for (int s = 0; s < n_stages; ++s) {
+    if (stage_count[s] < 1) return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: empty stage");
+    st[s] = HaarStage{first, stage_count[s], stage_threshold[s], 0};
+    first += stage_count[s];
+  }
+  if (first != n_stumps) return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: stage counts do not add up to n_stumps");
+  std::vector<HaarStump> sp((size_t)n_stumps);
+  for (int i = 0; i < n_stumps; ++i) {
+    if (stump_feature[i] < 0 || stump_feature[i] >= n_features)
+      return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: stump feature index out of range");
+    sp[i] = HaarStump{stump_feature[i], stump_threshold[i], stump_left[i], stump_right[i]};
+  }
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  haar_release(c);
+  HaarState* h = new HaarState();
+  c->haar = h;
+  h->ww = win_w;
+  h->wh = win_h;
+  h->nstages = n_stages;
+  EF_TRY(ensure(c, h->feats, f.size() * sizeof(HaarFeat)));
+  EF_TRY(ensure(c, h->stumps, sp.size() * sizeof(HaarStump)));
+  EF_TRY(ensure(c, h->stages, st.size() * sizeof(HaarStage)));
+  EF_HIP(c, hipMemcpy(h->feats.p, f.data(), f.size() * sizeof(HaarFeat), hipMemcpyHostToDevice), "H2D features");
+  EF_HIP(c, hipMemcpy(h->stumps.p, sp.data(), sp.size() * sizeof(HaarStump), hipMemcpyHostToDevice), "H2D stumps");
+  EF_HIP(c, hipMemcpy(h->stages.p, st.data(), st.size() * sizeof(HaarStage), hipMemcpyHostToDevice), "H2D stages");
+  return EF_OK;
+}
+
+int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t ld, double scale_factor,
+                   int32_t min_neighbors, int32_t min_w, int32_t min_h, int32_t max_w, int32_t max_h,
+                   int32_t* rects_out, int32_t max_rects, int32_t* n_rects, int32_t* cand_out, int32_t max_cand,
+                   int32_t* n_cand, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  HaarState* h = static_cast<HaarState*>(c->haar);
+  if (!h) return set_err(c, EF_E_STATE, "ef_haar_detect: call ef_haar_set_cascade first");
+  if (!gray || H < 1 || W < 1 || ld < W || !(scale_factor > 1.0) || !n_rects || (max_rects > 0 && !rects_out))
+    return set_err(c, EF_E_INVALID, "ef_haar_detect: bad arguments");
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  const int mw = (max_w > 0 && max_h > 0) ? max_w : W, mh = (max_w > 0 && max_h > 0) ? max_h : H;
+  // detectMultiScaleNoGrouping's scale list and FeatureEvaluator::updateScaleData's layers
+  std::vector<HaarLayer> layers;
+  std::vector<float> scales;
+  for (double factor = 1.0;; factor *= scale_factor) {
+    const int sw = cv_round(h->ww * factor), sh = cv_round(h->wh * factor);
+    if (sw > mw || sh > mh) break;
+    if (sw < min_w || sh < min_h) continue;
+    scales.push_back((float)factor);
+  }
+  int64_t pix = 0, ii = 0, resn = 0;
+  for (float sc : scales) {
+    HaarLayer ly{};
+    ly.w = cv_round((float)W / sc);
+    ly.h = cv_round((float)H / sc);
+    ly.nx = std::max(ly.w + 1 - h->ww, 0);
+    ly.ny = std::max(ly.h + 1 - h->wh, 0);
+    ly.step = sc >= 2.f ? 1 : 2;
+    ly.scale = sc;
+    ly.pix_off = pix;
+    ly.ii_off = ii;
+    ly.res_off = resn;
+    pix += (int64_t)ly.w * ly.h;
+    ii += (int64_t)(ly.w + 1) * (ly.h + 1);
+    resn += (int64_t)ly.nx * ly.ny;
+    if (ly.nx > 0 && ly.ny > 0) layers.push_back(ly);
+  }
+  *n_rects = 0;
+  if (n_cand) *n_cand = 0;
+  if (layers.empty()) return EF_OK;
+  const int nl = (int)layers.size();
+  std::vector<int> row_start(nl + 1, 0);
+  for (int i = 0; i < nl; ++i) row_start[i + 1] = row_start[i] + (layers[i].ny + layers[i].step - 1) / layers[i].step;
+  const int cap = 1 << 20;  // candidate / work-list capacity (windows surviving stage 0)
+  EF_TRY(ensure(c, h->pix, pix));
+  EF_TRY(ensure(c, h->ii1, ii * 4));
+  EF_TRY(ensure(c, h->ii2, ii * 4));
+  EF_TRY(ensure(c, h->res, std::max<int64_t>(resn, 16)));
+  EF_TRY(ensure(c, h->layers, layers.size() * sizeof(HaarLayer)));
+  EF_TRY(ensure(c, h->rowstart, row_start.size() * sizeof(int)));
+  EF_TRY(ensure(c, h->work, (size_t)cap * sizeof(HaarCand)));
+  EF_TRY(ensure(c, h->cand, (size_t)cap * sizeof(HaarCand)));
+  EF_TRY(ensure(c, h->counters, 64));
+  EF_TRY(ensure(c, h->desc, layers.size() * img_desc_size()));
+  const uint8_t* src = gray;
+  if (!(flags & EF_MEM_DEVICE) || ld != W) {
+    EF_TRY(ensure(c, h->frame, (size_t)H * W));
+    EF_HIP(c, hipMemcpy2DAsync(h->frame.p, W, gray, ld, W, H,
+                               (flags & EF_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s),
+           "frame");
+    src = static_cast<const uint8_t*>(h->frame.p);
+  }
+  std::vector<char> desc(layers.size() * img_desc_size());
+  int64_t max_out = 0;
+  for (int i = 0; i < nl; ++i) {
+    img_desc_fill(desc.data() + i * img_desc_size(), 0, layers[i].pix_off, H, W, 1, layers[i].h, layers[i].w);
+    max_out = std::max<int64_t>(max_out, (int64_t)layers[i].w * layers[i].h);
+  }
+  EF_HIP(c, hipMemcpyAsync(h->desc.p, desc.data(), desc.size(), hipMemcpyHostToDevice, s), "H2D desc");
+  EF_HIP(c, hipMemcpyAsync(h->layers.p, layers.data(), layers.size() * sizeof(HaarLayer), hipMemcpyHostToDevice, s),
+         "H2D layers");
+  EF_HIP(c, hipMemcpyAsync(h->rowstart.p, row_start.data(), row_start.size() * sizeof(int), hipMemcpyHostToDevice, s),
+         "H2D rows");
+  EF_HIP(c, hipMemsetAsync(h->counters.p, 0, 64, s), "memset");
+  TimerEvt tev;
+  timer_begin(c, EF_KERNEL_HAAR, &tev);
+  EF_HIP(c, launch_resize_gray(s, src, h->desc.p, nl, max_out, static_cast<uint8_t*>(h->pix.p)), "pyramid");
+  const HaarLayer* dl = static_cast<const HaarLayer*>(h->layers.p);
+  int* ii1 = static_cast<int*>(h->ii1.p);
+  unsigned* ii2 = static_cast<unsigned*>(h->ii2.p);
+  int maxh = 0, maxw = 0;
+  int64_t maxpos = 0;
+  for (auto& ly : layers) {
+    maxh = std::max(maxh, ly.h);
+    maxw = std::max(maxw, ly.w);
+    maxpos = std::max<int64_t>(maxpos, (int64_t)ly.nx * ly.ny);
+  }
+  const uint8_t* lp = static_cast<const uint8_t*>(h->pix.p);
+  hipLaunchKernelGGL(haar_rows_ii_kernel, dim3((unsigned)((maxh + 1 + 3) / 4), (unsigned)nl), dim3(256), 0, s, lp, dl,
+                     ii1, ii2);
+  hipLaunchKernelGGL(haar_cols_ii_kernel, dim3((unsigned)((maxw + 1 + 63) / 64), (unsigned)nl), dim3(1024), 0, s, dl,
+                     ii1, ii2);
+  const HaarStage* dst = static_cast<const HaarStage*>(h->stages.p);
+  const HaarStump* dsp = static_cast<const HaarStump*>(h->stumps.p);
+  const HaarFeat* dft = static_cast<const HaarFeat*>(h->feats.p);
+  signed char* res = static_cast<signed char*>(h->res.p);
+  hipLaunchKernelGGL(haar_stage0_kernel, dim3((unsigned)((maxpos + 255) / 256), (unsigned)nl), dim3(256), 0, s, dl, ii1,
+                     ii2, dst, dsp, dft, h->ww, h->wh, res);
+  int* cnt = static_cast<int*>(h->counters.p);
+  HaarCand* work = static_cast<HaarCand*>(h->work.p);
+  HaarCand* cand = static_cast<HaarCand*>(h->cand.p);
+  hipLaunchKernelGGL(haar_rows_kernel, dim3((unsigned)((row_start[nl] + 63) / 64)), dim3(64), 0, s, dl, nl,
+                     static_cast<const int*>(h->rowstart.p), res, work, cnt, cap);
+  int hc[16] = {0};
+  EF_HIP(c, hipMemcpyAsync(hc, cnt, sizeof(int), hipMemcpyDeviceToHost, s), "D2H work count");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  if (hc[0] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: work-list capacity exceeded");
+  // stage groups; the lists ping-pong between work and cand, counters cnt[g]
+  const int groups[] = {1, 3, 6, 10, 15, 1 << 30};
+  int gi = 0;
+  const int live = hc[0];  // upper bound of every group's input
+  HaarCand* bin = work;
+  HaarCand* bout = cand;
+  for (; groups[gi] < h->nstages; ++gi) {
+    const int s0 = groups[gi], s1 = std::min(groups[gi + 1], h->nstages);
+    if (live > 0)
+      hipLaunchKernelGGL(haar_cascade_kernel, dim3((unsigned)((live + 255) / 256)), dim3(256), 0, s, dl, ii1, ii2, dst,
+                         s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+    std::swap(bin, bout);
+  }
+  timer_end(c, &tev);
+  EF_HIP(c, hipGetLastError(), "haar kernels");
+  EF_HIP(c, hipMemcpyAsync(hc, cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, s), "D2H counts");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  hc[1] = hc[gi];  // survivors of the last group (all of stage 0's when the cascade has 1 stage)
+  cand = bin;
+  if (hc[1] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: candidate capacity exceeded");
+  std::vector<HaarCand> hcand((size_t)hc[1]);
+  if (hc[1] > 0)
+    EF_HIP(c, hipMemcpy(hcand.data(), cand, hcand.size() * sizeof(HaarCand), hipMemcpyDeviceToHost), "D2H cand");
+  // OpenCV's order: scale, then y, then x
+  std::sort(hcand.begin(), hcand.end(), [](const HaarCand& a, const HaarCand& b) {
+    return a.layer != b.layer ? a.layer < b.layer : (a.y != b.y ? a.y < b.y : a.x < b.x);
+  });
+  std::vector<RectI> rects;
+  rects.reserve(hcand.size());
+  for (const HaarCand& q : hcand) {
+    const float sc = layers[q.layer].scale;
+    rects.push_back(RectI{(int)std::lrint((float)q.x * sc), (int)std::lrint((float)q.y * sc),
+                          cv_round(h->ww * sc), cv_round(h->wh * sc)});
+  }
+  if (n_cand) *n_cand = (int32_t)rects.size();
+  if (cand_out)
+    for (int i = 0; i < (int)rects.size() && i < max_cand; ++i) {
+      cand_out[4 * i] = rects[i].x, cand_out[4 * i + 1] = rects[i].y;
+      cand_out[4 * i + 2] = rects[i].w, cand_out[4 * i + 3] = rects[i].h;
+    }
+  const std::vector<RectI> g = group_rectangles(rects, min_neighbors, 0.2);
+  *n_rects = (int32_t)g.size();
+  for (int i = 0; i < (int)g.size() && i < max_rects; ++i) {
+    rects_out[4 * i] = g[i].x, rects_out[4 * i + 1] = g[i].y, rects_out[4 * i + 2] = g[i].w, rects_out[4 * i + 3] = g[i].h;
+  }
+  return EF_OK;
+}
+
+}  // extern "C"

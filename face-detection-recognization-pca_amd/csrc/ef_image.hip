@@ -132,6 +132,16 @@ static hipError_t launch_resize(hipStream_t s, const uint8_t* src, const ImgDesc
   return hipGetLastError();
 }
 
+// Interface used by the Haar pyramid (ef_haar.hip): grey single-channel ragged resize.
+hipError_t launch_resize_gray(hipStream_t s, const uint8_t* src, const void* desc_dev, int count, int64_t max_out,
+                              uint8_t* dst) {
+  return launch_resize(s, src, static_cast<const ImgDesc*>(desc_dev), count, max_out, false, dst);
+}
+size_t img_desc_size() { return sizeof(ImgDesc); }
+void img_desc_fill(void* d, int64_t src_off, int64_t dst_off, int h, int w, int c, int oh, int ow) {
+  *static_cast<ImgDesc*>(d) = ImgDesc{src_off, dst_off, h, w, c, oh, ow, 0};
+}
+
 // ---------------------------------------------------------------- template localiser
 constexpr int kTmChunk = 128;   // template rows per int32 partial
 constexpr int kTmPiece = 352;   // template columns per piece (nkb <= 12)

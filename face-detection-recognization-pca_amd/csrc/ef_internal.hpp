@@ -95,12 +95,13 @@ struct ef_ctx {
   ef::DevBuf feats_dev; // float[b][k] staging for host output
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
+  void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
   void* blas = nullptr;  // rocBLAS handle (fit's plain dense products), lazily created
 
   bool timing = false;
   std::vector<ef::TimerEvt> pending;
-  double t_ms[4] = {0, 0, 0, 0};
-  int64_t t_n[4] = {0, 0, 0, 0};
+  double t_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t t_n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace ef {
@@ -108,6 +109,7 @@ namespace ef {
 int set_err(ef_ctx* c, int code, const std::string& msg);
 void blas_release(ef_ctx* c);
 void tm_release(ef_ctx* c);
+void haar_release(ef_ctx* c);
 int hip_err(ef_ctx* c, hipError_t e, const char* what);
 int ensure(ef_ctx* c, DevBuf& b, size_t bytes);
 void release(DevBuf& b);

@@ -18,7 +18,7 @@ EF_FIT_STANDARDIZE = 0x1
 EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
-EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST = 0, 1, 2, 3
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR = 0, 1, 2, 3, 4
 EF_KEY_NONE = (1 << 63) - 1
 
 _ERRNAMES = {-1: "EF_E_INVALID", -2: "EF_E_HIP", -3: "EF_E_STATE", -4: "EF_E_NOMEM", -5: "EF_E_NUMERIC"}
@@ -59,6 +59,9 @@ _SIGS = {
     "ef_tm_prepare": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, u32], C.c_int),
     "ef_tm_match": ([vp, vp, i64, vp, vp, vp, vp, u32], C.c_int),
     "ef_tm_info": ([vp, C.POINTER(i32), C.POINTER(i64), vp, vp], C.c_int),
+    "ef_haar_set_cascade": ([vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp], C.c_int),
+    "ef_haar_detect": ([vp, vp, i32, i32, i64, C.c_double, i32, i32, i32, i32, i32, vp, i32, C.POINTER(i32), vp, i32,
+                        C.POINTER(i32), u32], C.c_int),
     "ef_timing_enable": ([vp, C.c_int], C.c_int),
     "ef_timing_get": ([vp, i32, C.POINTER(C.c_double), C.POINTER(i64)], C.c_int),
     "ef_timing_reset": ([vp], C.c_int),

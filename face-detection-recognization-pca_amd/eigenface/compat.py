@@ -70,6 +70,17 @@ def read_face(path, size=(64, 64), device=0):
     return rows[0].reshape(size[1], size[0]) if keep else None
 
 
+def _save_bgr_jpg(path, bgr):
+    """cv2.imwrite of a BGR (or grey) uint8 crop (detection-v4.py:64)."""
+    a = np.ascontiguousarray(bgr, dtype=np.uint8)
+    try:
+        import cv2
+        cv2.imwrite(path, a)
+    except ImportError:
+        from PIL import Image
+        Image.fromarray(a[..., ::-1] if a.ndim == 3 else a).save(path, quality=95)
+
+
 def _save_jpg(path, arr2d):
     """cv2.normalize(NORM_MINMAX, 0..255, CV_8U) + imwrite (train-v4.py:164-177)."""
     a = np.asarray(arr2d, dtype=np.float64)

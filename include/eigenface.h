@@ -59,6 +59,7 @@ extern "C" {
 #define EF_KERNEL_PROJECT 1 /* (p - mean).W projection GEMM     */
 #define EF_KERNEL_TMATCH 2  /* template localiser, one frame    */
 #define EF_KERNEL_INGEST 3  /* grey + resize of one image batch */
+#define EF_KERNEL_HAAR 4    /* Haar cascade detection, one frame (GPU part) */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX
@@ -164,6 +165,30 @@ int ef_tm_match(ef_ctx* ctx, const uint8_t* frame, int64_t frame_ld, float* best
                 int32_t* y_out, float* maps_out, uint32_t flags);
 int ef_tm_info(ef_ctx* ctx, int32_t* n_problems, int64_t* map_elems, int32_t* result_h,
                int32_t* result_w);
+
+/* --------------------------------------------------------- Haar cascade detector
+ * Replaces face_cascade.detectMultiScale(gray, scaleFactor, minNeighbors, minSize)
+ * (detection-v4.py:18, :50-55) for a stump-based HAAR cascade as OpenCV stores it
+ * (stages of depth-1 trees over up-to-3-rectangle features, no tilted features):
+ *   features i: rects[i][k] = {x, y, w, h} in window coordinates, weights[i][k] (k < 3,
+ *               weight 0 = unused third rectangle);
+ *   stages s:   stage_count[s] consecutive stumps, stage_threshold[s];
+ *   stumps j:   feature index, threshold, left leaf (value < threshold), right leaf.
+ * ef_haar_detect runs the image pyramid, variance normalisation and cascade on the GPU
+ * and cv::groupRectangles(min_neighbors, 0.2) on the host; rects_out holds up to
+ * max_rects {x, y, w, h}, *n_rects the total; cand_out (optional) the ungrouped
+ * candidates in OpenCV's (scale, y, x) order.  max_w/max_h <= 0 means the frame size.
+ * The frame is a host pointer (row stride ld) unless EF_MEM_DEVICE.  Parity against
+ * OpenCV is unpinned (OpenCV and its cascade files are absent where this was built);
+ * OpenCV's pyramid uses INTER_LINEAR_EXACT, this one INTER_LINEAR. */
+int ef_haar_set_cascade(ef_ctx* ctx, int32_t win_w, int32_t win_h, int32_t n_features, const int32_t* rects,
+                        const float* weights, int32_t n_stages, const int32_t* stage_count,
+                        const float* stage_threshold, int32_t n_stumps, const int32_t* stump_feature,
+                        const float* stump_threshold, const float* stump_left, const float* stump_right);
+int ef_haar_detect(ef_ctx* ctx, const uint8_t* gray, int32_t h, int32_t w, int64_t ld, double scale_factor,
+                   int32_t min_neighbors, int32_t min_w, int32_t min_h, int32_t max_w, int32_t max_h,
+                   int32_t* rects_out, int32_t max_rects, int32_t* n_rects, int32_t* cand_out, int32_t max_cand,
+                   int32_t* n_cand, uint32_t flags);
 
 /* ------------------------------------------------------------------ timing
  * Device time of each launch of a kernel, measured with hipEvents on the
