@@ -7,17 +7,30 @@
 //   covariance (n >= d):  (n-1) n C_ij = n S'_ij - c_i c_j,           S' = X'^T X'
 //   Gram       (n <  d):  (n-1) n^2 C_ij = n^2 S'_ij - n (R_i + R_j) + Q,   S' = X' X'^T
 // with X' = X - 128, c = column sums of X', R_i = X'_i . c, Q = c . c — all exact
-// integers.  S' runs on v_mfma_i32_32x32x32_i8 with int32 accumulators flushed into an
-// int64 tile every 65536 samples (|x'| <= 128: 65536 * 128^2 = 2^30 fits), so the only
-// rounding of the whole covariance is the final int128 -> fp64 conversion and division
-// (<= 1 ulp), tighter than the fp64 GEMM the reference runs.  StandardScaler scaling
-// (train-v4.py:131) is applied afterwards as C_ij / (scale_i scale_j).
+// integers.  S' runs on v_mfma_i32_32x32x32_i8 with int32 accumulators: a work item covers
+// at most kMaxSplitK samples (|x'x'| <= 2^14, 131008 * 2^14 < 2^31), so it ends with one
+// plain int32 store into its split's slab, and the finalize sums the slabs in int64/int128.
+// The only rounding of the whole covariance is the final int128 -> fp64 conversion and
+// division (<= 1 ulp), tighter than the fp64 GEMM the reference runs.  StandardScaler
+// scaling (train-v4.py:131) is applied afterwards as C_ij / (scale_i scale_j).
+//
+// Operand layout in HBM: At = [kpad/64][dim][64] bytes ("K-blocked"): the 64 samples of one
+// K-stage for all dim rows are one contiguous dim*64-byte block, so a stage's 256-row panel
+// is a single 16-KiB run (a row-major [dim][kpad] copy puts every row of a panel on its own
+// page, 1 MB apart at n = 1M).  The covariance path writes it with a fused transpose that
+// also produces the exact column sums (sum x, sum x^2) the StandardScaler needs, so X is
+// read once for both.
 //
 // SYRK kernel: 256 x 256 output tile per workgroup (upper triangle of tiles only), 8 waves
 // of 128 x 64, K-slices of 64 samples staged by global_load_lds into a 4-stage LDS ring
-// (4 x 32 KiB, three stages in flight), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the
-// ds_read_b128 fragment reads are conflict-free.  Operands come from a K-contiguous int8 copy At (dim x Kpad):
-// X' itself for the Gram path, its transpose for the covariance path.
+// (4 x 32 KiB, three stages in flight behind the landed one, fragments of the next stage
+// read ahead of the current stage's last MFMAs), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the
+// ds_read_b128 fragment reads are conflict-free.  Work items = (tile, K-split): the split
+// count is chosen so items fill whole rounds of the chip (no tail round), and the item list
+// is split-major, so each XCD (blocks b = x mod 8) streams its own K range of every panel
+// while its ~32 resident workgroups run one 4 x 8 block of tiles (12 panels shared in L2).
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "ef_dma.hpp"
@@ -28,51 +41,143 @@ namespace ef {
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int YT = 256;                 // output tile (rows and columns)
-constexpr int YK = 64;                  // samples per stage
-constexpr int YSL = YT * YK;            // bytes per operand stage
-constexpr int YNB = 4;                  // LDS stages in the ring (prefetch distance YNB - 1)
-constexpr int64_t kFlushK = 65536;      // int32-safe accumulation length
+constexpr int YT = 256;                   // output tile (rows and columns)
+constexpr int YK = 64;                    // samples per stage
+constexpr int YSL = YT * YK;              // bytes per operand stage
+constexpr int YNB = 4;                    // LDS stages in the ring (prefetch distance YNB - 1)
+constexpr int64_t kMaxSplitStages = 2047; // 2047 * 64 = 131008 samples: int32-safe
+constexpr int FB = 64;                    // finalize block
 
-// At[r][k] = X[r][k] - 128 (Gram path: rows = samples), zero for k >= d.
-__global__ void shift_copy_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d, int64_t ldk,
+// ---------------------------------------------------------------- operand preparation
+// Gram path (rows = samples): At[kb][r][kk] = X[r][64 kb + kk] - 128, zero past d.
+__global__ void shift_copy_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d, int64_t nkb,
                                   uint8_t* __restrict__ At) {
-  const int64_t r = blockIdx.y;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ldk; k += (int64_t)gridDim.x * blockDim.x)
-    At[r * ldk + k] = k < d ? (uint8_t)(X[r * d + k] ^ 0x80u) : (uint8_t)0;
+  const int64_t total = nkb * n * 4;  // 16-byte chunks
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t kb = q / (n * 4), rem = q - kb * n * 4;
+    const int64_t r = rem >> 2;
+    const int64_t k0 = kb * 64 + (rem & 3) * 16;
+    unsigned w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t k = k0 + 4 * i + b;
+        const unsigned x = k < d ? (unsigned)(X[r * d + k] ^ 0x80u) : 0u;
+        v |= x << (8 * b);
+      }
+      w[i] = v;
+    }
+    *reinterpret_cast<uint4*>(At + q * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
 }
 
-// At[c][k] = X[k][c] - 128 (covariance path: rows = pixels), zero for k >= n; 64x64 tiles.
-__global__ void shift_transpose_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d, int64_t ldk,
+// Covariance path (rows = pixels), byte-granular fallback for d % 4 != 0 or unaligned X:
+// At[kb][c][kk] = X[64 kb + kk][c] - 128, zero past n.
+__global__ void shift_transpose_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d, int64_t nkb,
                                        uint8_t* __restrict__ At) {
   __shared__ uint8_t t[64][65];
-  const int64_t k0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int64_t kb = blockIdx.x, c0 = (int64_t)blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 4 rows per pass
   for (int r = ty; r < 64; r += 4) {
-    const int64_t k = k0 + r, c = c0 + tx;
+    const int64_t k = kb * 64 + r, c = c0 + tx;
     t[r][tx] = (k < n && c < d) ? (uint8_t)(X[k * d + c] ^ 0x80u) : (uint8_t)0;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
-    const int64_t c = c0 + r, k = k0 + tx;
-    if (c < d && k < ldk) At[c * ldk + k] = t[tx][r];
+    const int64_t c = c0 + r;
+    if (c < d) At[(kb * d + c) * 64 + tx] = t[tx][r];
   }
 }
 
-// S64[i][j] = sum_k At[i][k] At[j][k] for the upper triangle of 256-tiles (i-tile <= j-tile).
-__global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim, int64_t ldk,
-                                                         int64_t kpad, int ntiles, const int2* __restrict__ order,
-                                                         long long* __restrict__ S64) {
+// Covariance path, d % 4 == 0: the fused transpose + exact column statistics.  Wave q of
+// a workgroup owns rows 16q..16q+15 of every 64-sample block it visits, lane l the four
+// pixels c0 + 4l..+3: 16 coalesced dword loads, a register 4x4 byte transpose, four 16-B
+// stores (one per pixel row of At).  S1[c] += sum x, S2[c] += sum x^2 (uint32 partials per
+// thread — at most 16 * 4096 rows — reduced over the 4 waves in LDS, one uint64 atomic
+// per pixel and workgroup).
+__global__ __launch_bounds__(256) void transpose_stats_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
+                                                              int64_t nkb, uint8_t* __restrict__ At,
+                                                              unsigned long long* __restrict__ S1,
+                                                              unsigned long long* __restrict__ S2) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.y * 256 + 4 * lane;
+  const bool cok = c < d;
+  unsigned s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  for (int64_t kb = blockIdx.x; kb < nkb; kb += gridDim.x) {
+    const int64_t kr = kb * 64 + 16 * q;
+    unsigned v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      v[r] = (cok && kr + r < n) ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(X + (kr + r) * d + c))
+                                 : 0x80808080u;  // pad rows: x = 128, x' = 0 (excluded from the sums below)
+    if (cok) {
+      const int valid = (int)(n - kr < 16 ? (n - kr < 0 ? 0 : n - kr) : 16);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < valid) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const unsigned x = (v[r] >> (8 * m)) & 0xffu;
+            s1[m] += x;
+            s2[m] += x * x;
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        unsigned o[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          unsigned t = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) t |= ((v[4 * w + b] >> (8 * m)) & 0xffu) << (8 * b);
+          o[w] = t ^ 0x80808080u;
+        }
+        *reinterpret_cast<uint4*>(At + (kb * d + c + m) * 64 + 16 * q) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+  __shared__ unsigned red[2][4][256];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    red[0][q][4 * lane + m] = s1[m];
+    red[1][q][4 * lane + m] = s2[m];
+  }
+  __syncthreads();
+  const int cc = threadIdx.x;  // pixel c0 + cc
+  const int64_t col = (int64_t)blockIdx.y * 256 + cc;
+  if (col < d) {
+    unsigned long long a = 0, b = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      a += red[0][w][cc];
+      b += red[1][w][cc];
+    }
+    atomicAdd(&S1[col], a);
+    atomicAdd(&S2[col], b);
+  }
+}
+
+// ---------------------------------------------------------------- SYRK on int8 MFMA
+// Slab[ks][i][j] = sum over split ks's samples of At[.][i][k] At[.][j][k], for the upper
+// triangle of 256-tiles (i-tile <= j-tile).  Item = (split, tile), split-major.
+__global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
+                                                         int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
+                                                         int nitems, const int2* __restrict__ order,
+                                                         int* __restrict__ slabs, int abl) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[YNB * 2 * YSL];  // [stage][A | B], 128 KiB
   const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
-  // consecutive list entries run on one XCD (blocks b and b+8 share an XCD), and the
-  // host orders the list in 4 x 8 blocks of tiles, so the ~32 workgroups an XCD runs at
-  // once read 4 row panels and 8 column panels: most panel bytes hit its L2
+  // blocks b and b+8 share an XCD: XCD x runs list entries [x*total/8, (x+1)*total/8)
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  if (lin >= ntiles) return;
-  const int2 tt = order[lin];
-  const int ti = tt.x, tj = tt.y;
-  const int64_t i0 = (int64_t)ti * YT, j0 = (int64_t)tj * YT;
+  if (lin >= nitems) return;
+  const int ks = lin / ntiles;
+  const int2 tt = order[lin - ks * ntiles];
+  const int64_t i0 = (int64_t)tt.x * YT, j0 = (int64_t)tt.y * YT;
+  const int64_t sb = st_begin + ks * kps;
+  const int64_t se = sb + kps < st_end ? sb + kps : st_end;
+  const int64_t nst = se > sb ? se - sb : 0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -85,17 +190,21 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   const unsigned lds_base = lds_addr(smem);
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
-  auto issue = [&](int64_t k0, int buf) {
+  const int64_t blk = dim * YK;  // bytes per K-stage block of At
+  auto issue = [&](int64_t st, int buf) {
+    if (abl == 2) return;
+    if (abl == 1) st = st & 7;
     int lr = lrow, lc = lchunk;
     asm volatile("" : "+v"(lr), "+v"(lc));
+    const uint8_t* base = At + st * blk;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wave * 2 + jj;
       int64_t ra = i0 + j * 16 + lr, rb = j0 + j * 16 + lr;
       ra = ra < dim ? ra : dim - 1;
       rb = rb < dim ? rb : dim - 1;
-      glds16(At + ra * ldk + k0 + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + j * 1024));
-      glds16(At + rb * ldk + k0 + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + YSL + j * 1024));
+      glds16(base + ra * YK + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + j * 1024));
+      glds16(base + rb * YK + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + YSL + j * 1024));
     }
   };
 
@@ -105,63 +214,77 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = i32x16{};
 
-  auto flush = [&]() {  // WG-owned tile: plain read-modify-write of the int64 output
+  const int sw = (c32 >> 2) & 3;  // swizzle key of every row this lane reads
+  // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r] for k-step s of a stage
+  auto frag = [&](const uint8_t* sa, int s, i32x4 (&a)[4], i32x4 (&b)[2]) {
+    const int pch = ((2 * s + h) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const i32x4*>(sa + (wm * 128 + i * 32 + c32) * YK + pch);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sa + YSL + (wn * 64 + j * 32 + c32) * YK + pch);
+  };
+  auto mma = [&](const i32x4 (&a)[4], const i32x4 (&b)[2]) {
+    if (abl == 3) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t col = j0 + wn * 64 + j * 32 + c32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = i0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row < dim && col < dim) S64[row * dim + col] += (long long)acc[i][j][r];
-          acc[i][j][r] = 0;
-        }
-      }
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
   };
-
-  const int sw = (c32 >> 2) & 3;  // swizzle key of every row this lane reads
-  const int64_t nst = kpad / YK;
-  // ring of YNB stages, YNB - 1 in flight ahead of the one being consumed (an HBM miss is
-  // several stages of MFMA time); each stage is 4 DMA instructions per wave, so "stage st
-  // landed" is vmcnt <= 4 x (stages issued after it).  Tail stages past nst are issued as
-  // harmless re-reads of stage 0 so the count stays uniform.
-  for (int j = 0; j < YNB - 1; ++j) issue((j < nst ? j : 0) * YK, j);
-  for (int64_t st = 0; st < nst; ++st) {
-    const int buf = (int)(st % YNB);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage st landed (2 newer stages pending)
-    __syncthreads();                                   // ... for every wave; stage st-1 consumed
-    {
-      const int64_t nx = st + YNB - 1;
-      issue((nx < nst ? nx : 0) * YK, (int)(nx % YNB));
+  // Ring of YNB stages.  Each stage is 4 DMA instructions per wave, so "stage t landed" is
+  // vmcnt <= 4 x (stages issued after it); tail stages past nst are issued as harmless
+  // re-reads of the first stage so the count stays uniform.  One barrier per stage, placed
+  // between the stage's two k-steps: it publishes stage st+1 and retires stage st's slot,
+  // so the next stage's first fragments are read, and the DMA into the retired slot issued,
+  // while the second k-step's 8 MFMAs are still to run — the MFMA pipe never waits for
+  // the barrier plus an LDS round trip.  3 stages stay in flight behind the landed one.
+  if (nst > 0) {
+    for (int j = 0; j < YNB; ++j) issue(sb + (j < nst ? j : 0), j);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // stage 0 landed
+    __syncthreads();
+    i32x4 a0[4], b0[2], a1[4], b1[2];
+    frag(smem, 0, a0, b0);
+    for (int64_t st = 0; st < nst; ++st) {
+      const uint8_t* cur = smem + (st % YNB) * 2 * YSL;
+      frag(cur, 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (abl == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage st+1 landed (st+2, st+3 pending)
+      __syncthreads();  // every wave done reading stage st; stage st+1 visible
+      {
+        const int64_t nx = st + YNB;
+        issue(sb + (nx < nst ? nx : 0), (int)(nx % YNB));  // into stage st's slot
+      }
+      if (st + 1 < nst) frag(smem + ((st + 1) % YNB) * 2 * YSL, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    const uint8_t* sa = smem + buf * 2 * YSL;
-    const uint8_t* sb = sa + YSL;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {  // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r]
-      const int pch = ((2 * s + h) ^ sw) * 16;
-      i32x4 a[4], b[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const i32x4*>(sa + (wm * 128 + i * 32 + c32) * YK + pch);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sb + (wn * 64 + j * 32 + c32) * YK + pch);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (((st + 1) * YK) % kFlushK == 0 && st + 1 < nst) flush();
+    dma_wait_all();
   }
-  dma_wait_all();
-  flush();
+  int* out = slabs + (int64_t)ks * dim * dim;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = j0 + wn * 64 + j * 32 + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = i0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < dim && col < dim) out[row * dim + col] = acc[i][j][r];
+      }
+    }
 }
 
-// R[r] = sum_k At[r][k] * c[k]   (Gram path; exact in int64)
-__global__ void rowdot_kernel(const uint8_t* __restrict__ At, int64_t rows, int64_t ldk, int64_t d,
+// ---------------------------------------------------------------- exact finishing
+// R[r] = sum_k At[.][r][k] * c[k]   (Gram path; exact in int64)
+__global__ void rowdot_kernel(const uint8_t* __restrict__ At, int64_t rows, int64_t d,
                               const long long* __restrict__ c, long long* __restrict__ R) {
   const int64_t r = blockIdx.x;
   long long s = 0;
-  for (int64_t k = threadIdx.x; k < d; k += blockDim.x) s += (long long)(int8_t)At[r * ldk + k] * c[k];
+  for (int64_t k = threadIdx.x; k < d; k += blockDim.x)
+    s += (long long)(int8_t)At[((k >> 6) * rows + r) * YK + (k & 63)] * c[k];
   __shared__ long long red[256];
   red[threadIdx.x] = s;
   __syncthreads();
@@ -198,30 +321,58 @@ __global__ void sumsq128_kernel(const long long* __restrict__ c, int64_t d, unsi
   }
 }
 
-// C[i][j] from the exact integer pieces (one rounding); w = 1/scale or null.
-__global__ void cov_finalize_kernel(const long long* __restrict__ S64, int64_t dim, int64_t n, int gram,
-                                    const long long* __restrict__ cvec, const long long* __restrict__ R,
-                                    const unsigned long long* __restrict__ Q2, const double* __restrict__ w,
-                                    double* __restrict__ C) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= dim * dim) return;
-  const int64_t i = e / dim, j = e - (e / dim) * dim;
-  const bool upper = (i / YT) <= (j / YT);
-  const __int128 s = upper ? S64[i * dim + j] : S64[j * dim + i];
-  const __int128 nn = n;
-  double v;
-  if (gram) {
-    const __int128 q = (__int128)(((unsigned __int128)Q2[1] << 64) | Q2[0]);
-    const __int128 num = nn * nn * s - nn * ((__int128)R[i] + R[j]) + q;
-    v = (double)num / ((double)n * (double)n * (double)(n - 1));
-  } else {
-    const __int128 num = nn * s - (__int128)cvec[i] * cvec[j];
-    v = (double)num / ((double)n * (double)(n - 1));
+// S64 (+)= sum of the slabs, over the upper 64-blocks (multi-pass accumulation).
+__global__ void slab_accumulate_kernel(const int* __restrict__ slabs, int nslab, int64_t dim,
+                                       long long* __restrict__ S64) {
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bi > bj) return;
+  for (int e = threadIdx.x; e < FB * FB; e += blockDim.x) {
+    const int64_t i = bi * FB + e / FB, j = bj * FB + (e & (FB - 1));
+    if (i >= dim || j >= dim) continue;
+    long long s = S64[i * dim + j];
+    for (int q = 0; q < nslab; ++q) s += slabs[(int64_t)q * dim * dim + i * dim + j];
+    S64[i * dim + j] = s;
   }
-  if (w) v *= w[i] * w[j];
-  C[e] = v;
 }
 
+// C from the exact integer pieces (one rounding); w = 1/scale or null.  One workgroup per
+// upper 64-block: the block and (off the diagonal) its mirror, the mirror through LDS so
+// both writes are row-contiguous.
+__global__ __launch_bounds__(256) void cov_finalize_kernel(const int* __restrict__ slabs, int nslab,
+                                                           const long long* __restrict__ S64, int64_t dim, int64_t n,
+                                                           int gram, const long long* __restrict__ cvec,
+                                                           const long long* __restrict__ R,
+                                                           const unsigned long long* __restrict__ Q2,
+                                                           const double* __restrict__ w, double* __restrict__ C) {
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bi > bj) return;
+  __shared__ double tr[FB][FB + 1];
+  const __int128 nn = n;
+  const __int128 q = gram ? (__int128)(((unsigned __int128)Q2[1] << 64) | Q2[0]) : 0;
+  const double den = gram ? (double)n * (double)n * (double)(n - 1) : (double)n * (double)(n - 1);
+  for (int e = threadIdx.x; e < FB * FB; e += blockDim.x) {
+    const int li = e / FB, lj = e & (FB - 1);
+    const int64_t i = bi * FB + li, j = bj * FB + lj;
+    if (i >= dim || j >= dim) continue;
+    long long s = S64 ? S64[i * dim + j] : 0;
+    for (int t = 0; t < nslab; ++t) s += slabs[(int64_t)t * dim * dim + i * dim + j];
+    const __int128 num = gram ? nn * nn * (__int128)s - nn * ((__int128)R[i] + R[j]) + q
+                              : nn * (__int128)s - (__int128)cvec[i] * cvec[j];
+    double v = (double)num / den;
+    if (w) v *= w[i] * w[j];
+    C[i * dim + j] = v;
+    tr[lj][li] = v;
+  }
+  if (bi == bj) return;
+  __syncthreads();
+  for (int e = threadIdx.x; e < FB * FB; e += blockDim.x) {
+    const int lj = e / FB, li = e & (FB - 1);
+    const int64_t i = bi * FB + li, j = bj * FB + lj;
+    if (i < dim && j < dim) C[j * dim + i] = tr[lj][li];
+  }
+}
+
+// ---------------------------------------------------------------- host side
 int64_t cov_i8_kpad(int64_t K) { return (K + YK - 1) / YK * YK; }
 
 int64_t cov_i8_order_bytes(int64_t dim) {
@@ -229,22 +380,69 @@ int64_t cov_i8_order_bytes(int64_t dim) {
   return t * (t + 1) / 2 * (int64_t)sizeof(int2) + 64;
 }
 
-hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
-                         const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
-                         long long* cvec, long long* R, unsigned long long* Q2, void* order_dev, double* C) {
-  const int64_t dim = gram ? n : d;
-  const int64_t K = gram ? d : n;
-  const int64_t kpad = cov_i8_kpad(K);
-  if (gram) {
-    hipLaunchKernelGGL(shift_copy_kernel, dim3((unsigned)((kpad + 255) / 256 < 64 ? (kpad + 255) / 256 : 64),
-                                               (unsigned)n),
-                       dim3(256), 0, s, X, n, d, kpad, At);
-  } else {
-    hipLaunchKernelGGL(shift_transpose_kernel, dim3((unsigned)(kpad / 64), (unsigned)((d + 63) / 64)), dim3(256), 0,
-                       s, X, n, d, kpad, At);
+CovPlan cov_i8_plan(int64_t dim, int64_t K) {
+  CovPlan p;
+  p.nst = cov_i8_kpad(K) / YK;
+  const int64_t t = (dim + YT - 1) / YT;
+  p.ntiles = (int)(t * (t + 1) / 2);
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (ncu < 1) ncu = 256;
+  // slab memory budget 8 GiB (8 splits at d = 16384); EF_COV_SLAB_BUDGET (bytes) overrides
+  // it, which the tests use to force the multi-pass schedule on small inputs
+  const int64_t slab = dim * dim * (int64_t)sizeof(int);
+  int64_t budget = (int64_t)8 << 30;
+  if (const char* env = getenv("EF_COV_SLAB_BUDGET")) budget = std::max<int64_t>(atoll(env), 1);
+  int64_t smax = budget / std::max<int64_t>(slab, 1);
+  smax = std::min<int64_t>(std::max<int64_t>(smax, 1), 64);
+  const int64_t smin_total = (p.nst + kMaxSplitStages - 1) / kMaxSplitStages;
+  p.passes = (int)((smin_total + smax - 1) / smax);
+  p.stages_per_pass = (p.nst + p.passes - 1) / p.passes;
+  const int64_t smin = std::max<int64_t>(1, (p.stages_per_pass + kMaxSplitStages - 1) / kMaxSplitStages);
+  int64_t best = -1, best_s = smin;
+  for (int64_t s = smin; s <= smax && s <= std::max<int64_t>(smin, p.stages_per_pass); ++s) {
+    // one workgroup per CU: time ~ rounds x stages per item
+    const int64_t rounds = ((int64_t)p.ntiles * s + ncu - 1) / ncu;
+    const int64_t cost = rounds * ((p.stages_per_pass + s - 1) / s);
+    if (best < 0 || cost < best) best = cost, best_s = s;
   }
-  hipError_t e = hipMemsetAsync(S64, 0, (size_t)dim * dim * sizeof(long long), s);
-  if (e != hipSuccess) return e;
+  p.splits = (int)best_s;
+  p.kps = (p.stages_per_pass + p.splits - 1) / p.splits;
+  p.slab_elems = (int64_t)p.splits * dim * dim;
+  return p;
+}
+
+hipError_t launch_cov_i8_prep(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram, uint8_t* At,
+                              unsigned long long* S1, unsigned long long* S2) {
+  if (gram) {
+    const int64_t nkb = cov_i8_kpad(d) / YK;
+    const int64_t chunks = nkb * n * 4;
+    const int64_t blocks = std::min<int64_t>((chunks + 255) / 256, 16384);
+    hipLaunchKernelGGL(shift_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, n, d, nkb, At);
+    return hipGetLastError();
+  }
+  const int64_t nkb = cov_i8_kpad(n) / YK;
+  if (S1 && S2) {
+    if (!cov_i8_fused_stats(X, d)) return hipErrorInvalidValue;
+    // <= 4096 blocks of 64 rows per workgroup keeps the uint32 partials exact
+    int64_t gx = std::min<int64_t>(nkb, 128);
+    gx = std::max<int64_t>(gx, (nkb + 4095) / 4096);
+    hipLaunchKernelGGL(transpose_stats_kernel, dim3((unsigned)gx, (unsigned)((d + 255) / 256)), dim3(256), 0, s, X,
+                       n, d, nkb, At, S1, S2);
+  } else {
+    hipLaunchKernelGGL(shift_transpose_kernel, dim3((unsigned)nkb, (unsigned)((d + 63) / 64)), dim3(256), 0, s, X,
+                       n, d, nkb, At);
+  }
+  return hipGetLastError();
+}
+
+bool cov_i8_fused_stats(const uint8_t* X, int64_t d) { return d % 4 == 0 && ((size_t)X & 3) == 0; }
+
+hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, bool gram,
+                         const unsigned long long* S1, const double* w, const uint8_t* At, int* slabs,
+                         long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
+                         double* C) {
+  const int64_t dim = gram ? n : d;
   const int ntile = (int)((dim + YT - 1) / YT);
   // upper-triangle tiles in 4 x 8 blocks (L2 reuse within an XCD), one H2D of the list
   std::vector<int2> order;
@@ -253,22 +451,37 @@ hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, 
       for (int ti = bi; ti < bi + 4 && ti < ntile; ++ti)
         for (int tj = bj; tj < bj + 8 && tj < ntile; ++tj)
           if (ti <= tj) order.push_back(make_int2(ti, tj));
-  const int ntiles = (int)order.size();
-  const int grid = (ntiles + 7) / 8 * 8;
-  e = hipMemcpyAsync(order_dev, order.data(), order.size() * sizeof(int2), hipMemcpyHostToDevice, s);
+  if ((int)order.size() != p.ntiles) return hipErrorInvalidValue;
+  hipError_t e = hipMemcpyAsync(order_dev, order.data(), order.size() * sizeof(int2), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, kpad, kpad, ntiles,
-                     static_cast<const int2*>(order_dev), S64);
+  const int nitems = p.ntiles * p.splits;
+  const int grid = (nitems + 7) / 8 * 8;
+  const int nfb = (int)((dim + FB - 1) / FB);
+  if (p.passes > 1) {
+    if (!S64) return hipErrorInvalidValue;
+    e = hipMemsetAsync(S64, 0, (size_t)dim * dim * sizeof(long long), s);
+    if (e != hipSuccess) return e;
+  }
+  for (int pass = 0; pass < p.passes; ++pass) {
+    const int64_t st0 = (int64_t)pass * p.stages_per_pass;
+    const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
+    hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps, p.ntiles,
+                       nitems, static_cast<const int2*>(order_dev), slabs,
+                       getenv("EF_SYRK_ABL") ? atoi(getenv("EF_SYRK_ABL")) : 0);
+    if (p.passes > 1)
+      hipLaunchKernelGGL(slab_accumulate_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s, slabs,
+                         p.splits, dim, S64);
+  }
   e = hipStreamSynchronize(s);  // the host list must outlive the copy
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(shifted_sums_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, n, d, cvec);
   if (gram) {
-    hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)n), dim3(256), 0, s, At, n, kpad, d, cvec, R);
+    hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)n), dim3(256), 0, s, At, n, d, cvec, R);
     hipLaunchKernelGGL(sumsq128_kernel, dim3(1), dim3(256), 0, s, cvec, d, Q2);
   }
-  const int64_t tot = dim * dim;
-  hipLaunchKernelGGL(cov_finalize_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, S64, dim, n,
-                     gram ? 1 : 0, cvec, R, Q2, w, C);
+  hipLaunchKernelGGL(cov_finalize_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s,
+                     p.passes > 1 ? nullptr : slabs, p.passes > 1 ? 0 : p.splits,
+                     p.passes > 1 ? S64 : nullptr, dim, n, gram ? 1 : 0, cvec, R, Q2, w, C);
   return hipGetLastError();
 }
 

@@ -251,6 +251,16 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       bool ok = have_prev;
       for (int i = 0; i < kk && ok; ++i)
         ok = std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * std::fabs(th[i]), 1e-15 * std::fabs(th[0]));
+      if (getenv("EF_FIT_DEBUG")) {
+        double worst = 0;
+        int wi = 0;
+        for (int i = 0; i < kk && have_prev; ++i) {
+          const double r = std::fabs(th[i] - prev[i]) / std::fmax(std::fabs(th[i]), 1e-300);
+          if (r > worst) worst = r, wi = i;
+        }
+        fprintf(stderr, "[ef_fit] rr it=%d sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g\n", it,
+                se.sweeps, worst, wi, th[kk - 1], th[m - 1]);
+      }
       prev = th;
       have_prev = true;
       if (ok || it == kMaxIters) {
@@ -414,34 +424,42 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   EF_TRY(B.get(c, (size_t)d * kk, &En));
   EF_TRY(B.get(c, 1, &tv));
 
-  // K1: exact column statistics -> mean / var / scale / centring weights
+  // K1: exact column statistics -> mean / var / scale / centring weights.  On the int8
+  // covariance path the operand transpose produces the sums in the same pass over X.
+  const double inv = 1.0 / (double)(n - 1);
+  const bool int8_path = !gram || !stdz;
+  uint8_t* At = nullptr;
   EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
   EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
-  EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
+  const bool fused = int8_path && !gram && cov_i8_fused_stats(Xd, d);
+  if (int8_path) {
+    EF_TRY(B.get(c, (size_t)dim * cov_i8_kpad(gram ? d : n), &At));
+    EF_HIP(c, launch_cov_i8_prep(s, Xd, n, d, gram, At, fused ? S1 : nullptr, fused ? S2 : nullptr), "cov prep");
+  }
+  if (!fused) EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
   EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
   const double* wp = stdz ? w : nullptr;
 
   // K2+K3: covariance.  Exact integer product on the int8 matrix cores whenever the
   // pixel scaling commutes with it (covariance path; Gram path without StandardScaler),
   // else the fp64 GEMM with the centring/scaling fused into the operand loads.
-  const double inv = 1.0 / (double)(n - 1);
-  const bool int8_path = !gram || !stdz;
   if (int8_path) {
-    const int64_t kpad = cov_i8_kpad(gram ? d : n);
-    uint8_t* At;
-    long long *S64, *cvec, *R;
+    const CovPlan plan = cov_i8_plan(dim, gram ? d : n);
+    int* slabs;
+    long long *S64 = nullptr, *cvec, *R;
     unsigned long long* Q2;
-    EF_TRY(B.get(c, (size_t)dim * kpad, &At));
-    EF_TRY(B.get(c, (size_t)dim * dim, &S64));
+    EF_TRY(B.get(c, (size_t)plan.slab_elems, &slabs));
+    if (plan.passes > 1) EF_TRY(B.get(c, (size_t)dim * dim, &S64));
     EF_TRY(B.get(c, (size_t)d, &cvec));
     EF_TRY(B.get(c, (size_t)(gram ? n : 1), &R));
     EF_TRY(B.get(c, 2, &Q2));
     uint8_t* order;
     EF_TRY(B.get(c, (size_t)cov_i8_order_bytes(dim), &order));
-    EF_HIP(c, launch_cov_i8(s, Xd, n, d, gram, S1, stdz ? w : nullptr, At, S64, cvec, R, Q2, order, C),
+    EF_HIP(c, launch_cov_i8(s, plan, n, d, gram, S1, stdz ? w : nullptr, At, slabs, S64, cvec, R, Q2, order, C),
            "covariance (int8)");
     B.drop(s, At);
-    B.drop(s, S64);
+    B.drop(s, slabs);
+    if (S64) B.drop(s, S64);
   } else if (gram)
     EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::pixels(Xd, d, true, mean, wp), n, n, d,
                      inv, C, n, work, kWorkElems),

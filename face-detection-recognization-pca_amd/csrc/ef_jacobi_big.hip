@@ -10,6 +10,14 @@
 //     pivots); V <- V J is in place (thread (i, u) owns V[i][p_u], V[i][q_u]);
 //   * a sweep whose pivots are all below 1e-12 of their diagonal scale ends the solve
 //     (one host read of a flag per sweep).
+// Orders >= kBlockJacobiMin run the BLOCK variant instead: the matrix is cut into 16-wide
+// blocks, a round pairs the blocks (circle ordering over blocks, 15 rounds per sweep at
+// order 256 instead of 255), each pair's 32 x 32 subproblem is diagonalised in LDS by the
+// scalar method (bj_solve_kernel: kInnerSweeps inner sweeps of 31 rounds, each round's
+// 16 rotations computed once by one wave, rotations accumulated into Z), and one launch applies every pair's Z to
+// the matrix (G'[P][Q] = Z_P^T G[P][Q] Z_Q, block-pair parallel) and to V (V <- V Z).
+// Same fixed point and convergence flag (a sweep in which no off-diagonal entry exceeded
+// 1e-12 of its diagonal scale), 17x fewer launches per sweep.
 // Used for the Rayleigh-Ritz / orthonormalisation problems of the subspace iteration at
 // k > 80 (BASELINE.json config 3: k = 128; config 5: k = 512) and for direct solves of
 // moderate orders.  Quadratic convergence: a nearly diagonal input (warm subspace) needs
@@ -101,6 +109,178 @@ __global__ __launch_bounds__(256) void jbig_round_kernel(const double* __restric
   V[(int64_t)i * mp + b.q] = b.s * vp + b.c * vq;
 }
 
+// ------------------------------------------------------------------ block Jacobi
+constexpr int kBlockJacobiMin = 128;
+constexpr int BJ = 16;           // block width; a pair problem is 2 * BJ = 32
+constexpr int kInnerSweeps = 1;  // inner sweeps per pair problem (the outer sweeps revisit every pair)
+
+__device__ __forceinline__ int bj_index(int I, int J, int a) { return a < BJ ? I * BJ + a : J * BJ + (a - BJ); }
+
+__device__ __forceinline__ void bj_pair(int r, int t, int nb, int* I, int* J) {
+  int p = circle_pos(t, r, nb), q = circle_pos(nb - 1 - t, r, nb);
+  if (p > q) { const int x = p; p = q; q = x; }
+  *I = p;
+  *J = q;
+}
+
+// rotation of LDS pair (p, q) of a 32 x 32 matrix (row stride 33), same rule as pair_rotation
+__device__ __forceinline__ Rot lds_rotation(const double (*S)[33], int r, int t) {
+  Rot R;
+  int p = circle_pos(t, r, 2 * BJ), q = circle_pos(2 * BJ - 1 - t, r, 2 * BJ);
+  if (p > q) { const int x = p; p = q; q = x; }
+  R.p = p;
+  R.q = q;
+  const double apq = S[p][q], app = S[p][p], aqq = S[q][q];
+  const double g = 100.0 * fabs(apq);
+  if (apq == 0.0 || (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq))) {
+    R.on = false;
+    R.c = 1.0;
+    R.s = 0.0;
+  } else {
+    const double theta = (aqq - app) / (2.0 * apq);
+    double tt = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+    if (fabs(theta) > 1e150) tt = 0.5 / fabs(theta);
+    if (theta < 0.0) tt = -tt;
+    R.c = 1.0 / sqrt(tt * tt + 1.0);
+    R.s = tt * R.c;
+    R.on = true;
+  }
+  return R;
+}
+
+// One workgroup per block pair of round r: diagonalise S = G[P][P] (32 x 32) in LDS,
+// Z[pair] = the accumulated rotations.  256 threads: thread (t, u) owns the 2 x 2 block
+// {p_t, q_t} x {p_u, q_u} of each inner round (ping-pong S, one barrier per round).
+__global__ __launch_bounds__(256) void bj_solve_kernel(const double* __restrict__ G, double* __restrict__ Gout, int mp,
+                                                       int r, double* __restrict__ Zall, int* __restrict__ flag) {
+  const int nb = mp / BJ, pair = blockIdx.x;
+  int I, J;
+  bj_pair(r, pair, nb, &I, &J);
+  __shared__ double S[2][2 * BJ][33];
+  __shared__ double Z[2 * BJ][33];
+  __shared__ int any;
+  const int tid = threadIdx.x;
+  if (tid == 0) any = 0;
+  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+    const int a = e >> 5, b = e & 31;
+    S[0][a][b] = G[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)];
+    Z[a][b] = a == b ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  // outer convergence: any off-diagonal entry above 1e-12 of its diagonal scale
+  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+    const int a = e >> 5, b = e & 31;
+    if (a != b && fabs(S[0][a][b]) > 1e-12 * sqrt(fabs(S[0][a][a] * S[0][b][b]))) any = 1;
+  }
+  __syncthreads();
+  if (any) *flag = 1;
+  const int t = tid >> 4, u = tid & 15;
+  __shared__ Rot rot[BJ];
+  int cur = 0;
+  for (int sw = 0; sw < kInnerSweeps && any; ++sw) {
+    __syncthreads();
+    if (tid == 0) any = 0;
+    for (int rr = 0; rr < 2 * BJ - 1; ++rr) {
+      // the round's 16 rotations, computed once (the fp64 sqrt/div chain is the round's latency)
+      if (tid < BJ) {
+        const Rot R = lds_rotation(S[cur], rr, tid);
+        rot[tid] = R;
+        if (R.on) any = 1;
+      }
+      __syncthreads();
+      const Rot ra = rot[t], rb = rot[u];
+      const double x00 = S[cur][ra.p][rb.p], x01 = S[cur][ra.p][rb.q];
+      const double x10 = S[cur][ra.q][rb.p], x11 = S[cur][ra.q][rb.q];
+      const double y00 = ra.c * x00 - ra.s * x10, y01 = ra.c * x01 - ra.s * x11;
+      const double y10 = ra.s * x00 + ra.c * x10, y11 = ra.s * x01 + ra.c * x11;
+      double z00 = rb.c * y00 - rb.s * y01, z01 = rb.s * y00 + rb.c * y01;
+      double z10 = rb.c * y10 - rb.s * y11, z11 = rb.s * y10 + rb.c * y11;
+      if (t == u && ra.on) {
+        z01 = 0.0;
+        z10 = 0.0;
+      }
+      S[cur ^ 1][ra.p][rb.p] = z00;
+      S[cur ^ 1][ra.p][rb.q] = z01;
+      S[cur ^ 1][ra.q][rb.p] = z10;
+      S[cur ^ 1][ra.q][rb.q] = z11;
+      // Z <- Z J_b: thread (t, u) updates rows 2t, 2t+1 of the pair u columns
+      if (rb.on) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * t + h;
+          const double zp = Z[i][rb.p], zq = Z[i][rb.q];
+          Z[i][rb.p] = rb.c * zp - rb.s * zq;
+          Z[i][rb.q] = rb.s * zp + rb.c * zq;
+        }
+      }
+      cur ^= 1;
+      __syncthreads();
+    }
+  }
+  // the diagonalised pair block goes out as computed (rotated pivots exactly zero), so
+  // rounding noise of a Z^T S Z product never re-triggers the convergence flag
+  double* Zp = Zall + (int64_t)pair * 4 * BJ * BJ;
+  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+    const int a = e >> 5, b = e & 31;
+    Zp[e] = Z[a][b];
+    Gout[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)] = S[cur][a][b];
+  }
+}
+
+// Gout[P][Q] = Z_P^T Gin[P][Q] Z_Q for every pair of block pairs (blockIdx.y < npair), and
+// V[R][Q] <- V[R][Q] Z_Q for 32-row tiles R of V (blockIdx.y >= npair; in place: a tile is
+// read completely before it is written).
+__global__ __launch_bounds__(256) void bj_apply_kernel(const double* __restrict__ Gin, double* __restrict__ Gout,
+                                                       double* __restrict__ V, int mp, int r,
+                                                       const double* __restrict__ Zall) {
+  const int nb = mp / BJ, npair = nb / 2;
+  const int q = blockIdx.x, py = blockIdx.y;
+  int IQ, JQ;
+  bj_pair(r, q, nb, &IQ, &JQ);
+  __shared__ double A[2 * BJ][33], T[2 * BJ][33], ZP[2 * BJ][33], ZQ[2 * BJ][33];
+  const int tid = threadIdx.x;
+  const bool isv = py >= npair;
+  if (!isv && py == q) return;  // the pair's own block: written by bj_solve_kernel
+  int IP = 0, JP = 0;
+  if (!isv) bj_pair(r, py, nb, &IP, &JP);
+  const int64_t r0 = (int64_t)(py - npair) * 2 * BJ;  // V row tile
+  const double* zq = Zall + (int64_t)q * 4 * BJ * BJ;
+  const double* zp = Zall + (int64_t)py * 4 * BJ * BJ;
+  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+    const int a = e >> 5, b = e & 31;
+    const int64_t col = bj_index(IQ, JQ, b);
+    A[a][b] = isv ? V[(r0 + a) * mp + col] : Gin[(int64_t)bj_index(IP, JP, a) * mp + col];
+    ZQ[a][b] = zq[e];
+    if (!isv) ZP[a][b] = zp[e];
+  }
+  __syncthreads();
+  const int a0 = tid >> 5, b = tid & 31;  // thread: rows a0 + 8j, column b
+  if (!isv) {  // T = Z_P^T A
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int a = a0 + 8 * j;
+      double acc = 0.0;
+#pragma unroll 8
+      for (int k = 0; k < 2 * BJ; ++k) acc += ZP[k][a] * A[k][b];
+      T[a][b] = acc;
+    }
+    __syncthreads();
+  }
+  const double (*X)[33] = isv ? A : T;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int a = a0 + 8 * j;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < 2 * BJ; ++k) acc += X[a][k] * ZQ[k][b];
+    const int64_t col = bj_index(IQ, JQ, b);
+    if (isv)
+      V[(r0 + a) * mp + col] = acc;
+    else
+      Gout[(int64_t)bj_index(IP, JP, a) * mp + col] = acc;
+  }
+}
+
 // descending order (ties -> lower index first); evecs[r][rank] = V[r][i]
 __global__ void jbig_sort_kernel(const double* __restrict__ G, const double* __restrict__ V, int m, int mp,
                                  double* __restrict__ evals, double* __restrict__ evecs, int64_t ldv) {
@@ -121,9 +301,11 @@ __global__ void jbig_sort_kernel(const double* __restrict__ G, const double* __r
   for (int rr = threadIdx.x; rr < m; rr += blockDim.x) evecs[(int64_t)rr * ldv + rank] = V[(int64_t)rr * mp + i];
 }
 
+static int padded_order(int m) { return m >= kBlockJacobiMin ? (m + 2 * BJ - 1) / (2 * BJ) * (2 * BJ) : m + (m & 1); }
+
 size_t jacobi_big_work_elems(int m) {
-  const int64_t mp = m + (m & 1);
-  return (size_t)(3 * mp * mp) + 64;
+  const int64_t mp = padded_order(m);
+  return (size_t)(3 * mp * mp + 2 * BJ * mp) + 64;  // G ping-pong, V, pair rotations
 }
 
 // One sweep (mp - 1 rounds) per graph; two graphs for the two ping-pong parities.
@@ -136,7 +318,8 @@ void JacobiBig::destroy() {
 hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t capture) {
   destroy();
   m = m_;
-  mp = m + (m & 1);
+  mp = padded_order(m);
+  block = m >= kBlockJacobiMin;
   work = work_;
   flag = flag_;
   double* G[2] = {work, work + (int64_t)mp * mp};
@@ -144,13 +327,22 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
   const int np = mp / 2;
   const int64_t threads = (int64_t)np * np + (int64_t)mp * np;
   const dim3 grid((unsigned)((threads + 255) / 256));
+  const int nb = mp / BJ, npair = nb / 2;
+  double* Z = work + 3 * (int64_t)mp * mp;
   for (int par = 0; par < 2; ++par) {
     hipError_t e = hipStreamBeginCapture(capture, hipStreamCaptureModeRelaxed);
     if (e != hipSuccess) return e;
     (void)hipMemsetAsync(flag, 0, sizeof(int), capture);
     int cur = par;
-    for (int r = 0; r < mp - 1; ++r) {
-      hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, capture, G[cur], G[cur ^ 1], V, mp, r, flag);
+    for (int r = 0; r < rounds(); ++r) {
+      if (block) {
+        hipLaunchKernelGGL(bj_solve_kernel, dim3((unsigned)npair), dim3(256), 0, capture, G[cur], G[cur ^ 1], mp, r, Z,
+                           flag);
+        hipLaunchKernelGGL(bj_apply_kernel, dim3((unsigned)npair, (unsigned)(npair + mp / (2 * BJ))), dim3(256), 0,
+                           capture, G[cur], G[cur ^ 1], V, mp, r, Z);
+      } else {
+        hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, capture, G[cur], G[cur ^ 1], V, mp, r, flag);
+      }
       cur ^= 1;
     }
     hipGraph_t g = nullptr;
@@ -176,7 +368,7 @@ int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals,
   for (; sweep < max_sweeps; ++sweep) {
     *err = hipGraphLaunch(static_cast<hipGraphExec_t>(exec[cur]), s);
     if (*err != hipSuccess) return -1;
-    cur ^= (mp - 1) & 1;  // an odd number of rounds swaps the buffers
+    cur ^= rounds() & 1;  // an odd number of rounds swaps the buffers
     int hflag = 0;
     *err = hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
     if (*err == hipSuccess) *err = hipStreamSynchronize(s);

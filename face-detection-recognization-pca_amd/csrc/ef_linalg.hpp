@@ -75,6 +75,8 @@ hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, dou
 size_t jacobi_big_work_elems(int m);
 struct JacobiBig {
   int m = 0, mp = 0;
+  bool block = false;  // block-Jacobi rounds (orders >= 128)
+  int rounds() const { return block ? mp / 16 - 1 : mp - 1; }
   double* work = nullptr;
   int* flag = nullptr;
   void* exec[2] = {nullptr, nullptr};
@@ -85,12 +87,27 @@ struct JacobiBig {
   ~JacobiBig() { destroy(); }
 };
 // Exact integer covariance / Gram on int8 MFMA (ef_cov_i8.hip).  At: dim x cov_i8_kpad(K)
-// bytes, S64: dim*dim int64, cvec: d int64, R: n int64 (Gram), Q2: 2 uint64 (Gram).
+// bytes in the K-blocked layout [kpad/64][dim][64]; slabs: plan.slab_elems int32; S64:
+// dim*dim int64 (only when plan.passes > 1); cvec: d int64, R: n int64 (Gram), Q2: 2 uint64.
+struct CovPlan {
+  int64_t nst = 0;              // 64-sample K stages
+  int64_t stages_per_pass = 0;  // K stages per syrk launch
+  int64_t kps = 0;              // K stages per work item (<= 2047: int32-exact)
+  int64_t slab_elems = 0;       // splits * dim * dim
+  int ntiles = 0, splits = 1, passes = 1;
+};
 int64_t cov_i8_kpad(int64_t K);
 int64_t cov_i8_order_bytes(int64_t dim);  // device scratch for the tile order list
-hipError_t launch_cov_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram,
-                         const unsigned long long* S1, const double* w, uint8_t* At, long long* S64,
-                         long long* cvec, long long* R, unsigned long long* Q2, void* order_dev, double* C);
+CovPlan cov_i8_plan(int64_t dim, int64_t K);
+bool cov_i8_fused_stats(const uint8_t* X, int64_t d);  // covariance-path prep can produce S1/S2
+// Gram path: At = X' (K = d).  Covariance path: At = X'^T (K = n); with S1/S2 non-null
+// (requires cov_i8_fused_stats) also S1 += sum x, S2 += sum x^2 per pixel.
+hipError_t launch_cov_i8_prep(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, bool gram, uint8_t* At,
+                              unsigned long long* S1, unsigned long long* S2);
+hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, bool gram,
+                         const unsigned long long* S1, const double* w, const uint8_t* At, int* slabs,
+                         long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
+                         double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);

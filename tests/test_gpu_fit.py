@@ -64,7 +64,9 @@ def test_sklearn_path_golden():
     # k > 80: direct grid-Jacobi (order <= 1024) and subspace iteration + grid Jacobi
     (600, 4096, 128, 256), (1500, 4096, 100, 256), (3000, 1024, 130, 256),
     # covariance path with n > 65536: the int8 product's int32 -> int64 flush
-    (70000, 256, 12, 64)])
+    (70000, 256, 12, 64),
+    # covariance path with d % 4 != 0: byte-granular transpose + separate column stats
+    (400, 50, 10, 32), (131009, 36, 6, 16)])
 def test_fit_shapes_vs_oracle(n, d, k, r):
     """Direct-Jacobi (order <= 88), Gram and covariance (n >= d) branches, exact int8
     covariance, wide k."""
@@ -115,3 +117,16 @@ def test_standardized_covariance_path_vs_oracle():
     np.testing.assert_allclose(m.components_, o["pca"]["components_"], atol=1e-8)
     np.testing.assert_allclose(m.face_features_, o["face_features"], rtol=1e-6,
                                atol=1e-7 * np.abs(o["face_features"]).max())
+
+
+def test_covariance_multi_pass(monkeypatch):
+    """Force the int8 covariance into several syrk passes (slab budget of one split):
+    the int64 slab accumulation between passes must keep the product exact."""
+    from eigenface import manual_pca
+    monkeypatch.setenv("EF_COV_SLAB_BUDGET", str(64 * 64 * 4))
+    x, _ = orc.synth_faces(140_000, 8, r=32, seed=5)  # K = 140000 > 2047 * 64 samples per split
+    eig, mean, proj, lam = manual_pca(x, 8)
+    o_eig, o_mean, _, o_lam = orc.manual_pca(x, 8)
+    np.testing.assert_allclose(mean, o_mean, rtol=1e-14)
+    np.testing.assert_allclose(lam, o_lam, rtol=1e-9)
+    np.testing.assert_allclose(_align(eig, o_eig), o_eig, atol=1e-6)
