@@ -23,7 +23,7 @@
 //
 // SYRK kernel: 256 x 256 output tile per workgroup (upper triangle of tiles only), 8 waves
 // of 128 x 64, K-slices of 64 samples staged by global_load_lds into a 4-stage LDS ring
-// (4 x 32 KiB, three stages in flight behind the landed one, fragments of the next stage
+// (4 x 32 KiB, two stages in flight behind the landed one, fragments of the next stage
 // read ahead of the current stage's last MFMAs), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the
 // ds_read_b128 fragment reads are conflict-free.  Work items = (tile, K-split): the split
 // count is chosen so items fill whole rounds of the chip (no tail round), and the item list
@@ -44,7 +44,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int YT = 256;                   // output tile (rows and columns)
 constexpr int YK = 64;                    // samples per stage
 constexpr int YSL = YT * YK;              // bytes per operand stage
-constexpr int YNB = 4;                    // LDS stages in the ring (prefetch distance YNB - 1)
+constexpr int YNB = 4;                    // LDS stages in the ring (YNB - 2 in flight behind the landed one)
 constexpr int64_t kMaxSplitStages = 2047; // 2047 * 64 = 131008 samples: int32-safe
 constexpr int FB = 64;                    // finalize block
 
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void transpose_stats_kernel(const uint8_t* __r
 __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                          int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
                                                          int nitems, const int2* __restrict__ order,
-                                                         int* __restrict__ slabs, int abl) {
+                                                         int* __restrict__ slabs) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[YNB * 2 * YSL];  // [stage][A | B], 128 KiB
   const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
   // blocks b and b+8 share an XCD: XCD x runs list entries [x*total/8, (x+1)*total/8)
@@ -192,8 +192,6 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
   const int64_t blk = dim * YK;  // bytes per K-stage block of At
   auto issue = [&](int64_t st, int buf) {
-    if (abl == 2) return;
-    if (abl == 1) st = st & 7;
     int lr = lrow, lc = lchunk;
     asm volatile("" : "+v"(lr), "+v"(lc));
     const uint8_t* base = At + st * blk;
@@ -224,7 +222,6 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
     for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sa + YSL + (wn * 64 + j * 32 + c32) * YK + pch);
   };
   auto mma = [&](const i32x4 (&a)[4], const i32x4 (&b)[2]) {
-    if (abl == 3) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -239,7 +236,7 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   // the barrier plus an LDS round trip.  3 stages stay in flight behind the landed one.
   if (nst > 0) {
     for (int j = 0; j < YNB; ++j) issue(sb + (j < nst ? j : 0), j);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // stage 0 landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (YNB - 1)) : "memory");  // stage 0 landed
     __syncthreads();
     i32x4 a0[4], b0[2], a1[4], b1[2];
     frag(smem, 0, a0, b0);
@@ -249,8 +246,7 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
       __builtin_amdgcn_sched_barrier(0);
       mma(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (abl == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // stage st+1 landed (st+2, st+3 pending)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (YNB - 2)) : "memory");  // stage st+1 landed
       __syncthreads();  // every wave done reading stage st; stage st+1 visible
       {
         const int64_t nx = st + YNB;
@@ -466,8 +462,7 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
     hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps, p.ntiles,
-                       nitems, static_cast<const int2*>(order_dev), slabs,
-                       getenv("EF_SYRK_ABL") ? atoi(getenv("EF_SYRK_ABL")) : 0);
+                       nitems, static_cast<const int2*>(order_dev), slabs);
     if (p.passes > 1)
       hipLaunchKernelGGL(slab_accumulate_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s, slabs,
                          p.splits, dim, S64);
