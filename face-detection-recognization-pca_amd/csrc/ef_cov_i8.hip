@@ -191,18 +191,25 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
   const int64_t blk = dim * YK;  // bytes per K-stage block of At
+  // per-lane byte offsets inside a stage block are fixed for the item: the stage loop only
+  // moves the wave-uniform SGPR base (no per-lane 64-bit address arithmetic per stage)
+  unsigned voff[2][2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int j = wave * 2 + jj;
+    int64_t ra = i0 + j * 16 + lrow, rb = j0 + j * 16 + lrow;
+    ra = ra < dim ? ra : dim - 1;
+    rb = rb < dim ? rb : dim - 1;
+    voff[jj][0] = (unsigned)(ra * YK + lchunk * 16);
+    voff[jj][1] = (unsigned)(rb * YK + lchunk * 16);
+  }
   auto issue = [&](int64_t st, int buf) {
-    int lr = lrow, lc = lchunk;
-    asm volatile("" : "+v"(lr), "+v"(lc));
-    const uint8_t* base = At + st * blk;
+    const unsigned long long base = (unsigned long long)(size_t)(At + st * blk);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wave * 2 + jj;
-      int64_t ra = i0 + j * 16 + lr, rb = j0 + j * 16 + lr;
-      ra = ra < dim ? ra : dim - 1;
-      rb = rb < dim ? rb : dim - 1;
-      glds16(base + ra * YK + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + j * 1024));
-      glds16(base + rb * YK + lc * 16, lds_base + (unsigned)(buf * 2 * YSL + YSL + j * 1024));
+      glds16s(voff[jj][0], base, lds_base + (unsigned)(buf * 2 * YSL + j * 1024));
+      glds16s(voff[jj][1], base, lds_base + (unsigned)(buf * 2 * YSL + YSL + j * 1024));
     }
   };
 
