@@ -487,9 +487,15 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   // training projection A.E (projected_data / fit_transform output)
   if (proj_out) {
     EF_TRY(B.get(c, (size_t)n * kk, &proj));
-    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::dense(En, kk, false), n, kk, d, 1.0, proj,
-                     kk, work, kWorkElems),
-           "F = A.E");
+    if (proj_i8_supported(Xd, n, d, kk) && !getenv("EF_FIT_PROJ_F64")) {  // exact int8 digits (ef_proj_i8.hip)
+      uint8_t* pw;
+      EF_TRY(B.get(c, proj_i8_work_bytes(n, d, kk), &pw));
+      EF_HIP(c, launch_proj_i8(s, Xd, n, d, mean, wp, En, kk, pw, proj), "F = A.E (int8 digits)");
+    } else {
+      EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::dense(En, kk, false), n, kk, d, 1.0,
+                       proj, kk, work, kWorkElems),
+             "F = A.E");
+    }
   }
 
   const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;

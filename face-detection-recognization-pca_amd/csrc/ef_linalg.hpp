@@ -109,6 +109,12 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
                          double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
+// Training projection F (n x kk, fp64) = ((X - mu) * w) . E on int8 MFMA with E split into
+// base-256 digits (ef_proj_i8.hip); w may be null.  work: proj_i8_work_bytes bytes.
+bool proj_i8_supported(const uint8_t* X, int64_t n, int64_t d, int kk);
+size_t proj_i8_work_bytes(int64_t n, int64_t d, int kk);
+hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, const double* mu, const double* w,
+                          const double* E, int kk, void* work, double* F);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,

@@ -1,0 +1,247 @@
+// Training projection F = ((X - mu) * w) . E on the int8 matrix cores (fit K5, the
+// projected_data of useless/train.py:122 / face_features of train-v4.py:134, n x k).
+//
+// X is uint8, so X' = X - 128 is exact int8, and
+//     F = X' . E'' + 1 . c^T,   E'' = diag(w) E,   c = (128 - mu)^T E''
+// (c in fp64 by cc_kernel).  E'' is fp64; per output column it is scaled by 2^t_c so its
+// largest entry is ~2^54 and rounded to an integer V (relative error <= 2^-54, i.e. fp64
+// precision), which is written as P = 7 signed base-256 digits, V = sum_j 256^j D_j with
+// D_j in [-128, 127].  Each X' . D_j is an exact int32 (|.| <= d * 2^14 <= 2^30 for
+// d <= 65536), so the only roundings are the quantisation of E'' and the fp64 Horner
+// combine 2^-t_c sum_j 256^j I_j (proj_combine_kernel) — the same order of error as the
+// fp64 GEMM it replaces (reference: useless/train.py:122 in float64).
+//
+// proj_i8_kernel: C[n][N] (int32) = X' . D^T with D = [N = P * kk padded to 128][d] int8
+// (K-contiguous).  Workgroup tile 256 rows x 128 digit-columns, 8 waves of 64 x 64, K
+// stages of 64 bytes staged by LDS-DMA into a 4-stage ring (same 64-B row swizzle as the
+// covariance kernel); A fragments are flipped to int8 (x ^ 0x80) in registers.  The
+// N-tiles of one row block are consecutive on one XCD, so X is read from HBM about once.
+// Requires d % 64 == 0 (X rows are DMA'd 64 bytes at a time; otherwise the caller keeps
+// the fp64 GEMM).
+#include <algorithm>
+#include <cmath>
+
+#include "ef_dma.hpp"
+#include "ef_linalg.hpp"
+
+namespace ef {
+
+namespace {
+
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int PM = 256;           // rows per tile
+constexpr int PN = 128;           // digit-columns per tile
+constexpr int PK = 64;            // K bytes per stage
+constexpr int PNB = 4;            // LDS ring stages
+constexpr int kDigits = 7;        // base-256 digits of the scaled eigenvector entries
+constexpr int kTopBit = 54;       // largest scaled entry ~ 2^54
+constexpr int PSTAGE = (PM + PN) * PK;  // 24 KiB per stage
+
+// t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^53, 2^54); zero columns get t_c = 0.
+__global__ void digit_scale_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
+                                   int* __restrict__ tsh) {
+  const int c = blockIdx.x;
+  double m = 0.0;
+  for (int64_t r = threadIdx.x; r < d; r += blockDim.x) m = fmax(m, fabs((w ? w[r] : 1.0) * E[r * kk + c]));
+  __shared__ double red[256];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int e = 0;
+    if (red[0] > 0.0) (void)frexp(red[0], &e);  // red[0] in [2^(e-1), 2^e)
+    tsh[c] = red[0] > 0.0 ? kTopBit - e : 0;
+  }
+}
+
+// D[(j * kk + c) * d + r] = digit j of rint(w_r E[r][c] 2^t_c); rows kk * P .. Npad are zero.
+__global__ void digits_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
+                              const int* __restrict__ tsh, int8_t* __restrict__ D) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d * kk) return;
+  const int64_t r = e / kk;
+  const int c = (int)(e - r * kk);
+  long long v = (long long)rint(ldexp((w ? w[r] : 1.0) * E[r * kk + c], tsh[c]));
+#pragma unroll
+  for (int j = 0; j < kDigits; ++j) {
+    const long long lo = ((v + 128) & 255) - 128;  // signed low byte
+    D[((int64_t)j * kk + c) * d + r] = (int8_t)lo;
+    v = (v - lo) / 256;
+  }
+}
+
+// c[col] = sum_r (128 - mu_r) w_r E[r][col]  (fp64, one block per column)
+__global__ void cc_kernel(const double* __restrict__ E, const double* __restrict__ w, const double* __restrict__ mu,
+                          int64_t d, int kk, double* __restrict__ cc) {
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int64_t r = threadIdx.x; r < d; r += blockDim.x) s += (128.0 - mu[r]) * (w ? w[r] : 1.0) * E[r * kk + c];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cc[c] = red[0];
+}
+
+__global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
+                                                         const int8_t* __restrict__ D, int ntn, int nblocks,
+                                                         int* __restrict__ C, int64_t ldc) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[PNB * PSTAGE];  // [stage][A 16 KiB | B 8 KiB]
+  const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
+  // blocks b and b+8 share an XCD: XCD x runs items [x*total/8, (x+1)*total/8), row-block
+  // major, so the N-tiles of a row block run together and share its X rows in L2
+  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+  if (lin >= nblocks) return;
+  const int mt = lin / ntn, nt = lin - (lin / ntn) * ntn;
+  const int64_t m0 = (int64_t)mt * PM, n0 = (int64_t)nt * PN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c32 = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 x 64
+
+  // DMA: a stage = 16 A pieces + 8 B pieces of 1 KiB (16 rows x 64 B); wave w issues A
+  // pieces 2w, 2w+1 and B piece w.  Lane l -> row 16j + (l >> 2), physical chunk l & 3
+  // holding logical chunk (l & 3) ^ ((l >> 4) & 3).
+  const unsigned lds_base = lds_addr(smem);
+  const int lrow = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
+  unsigned voffB;
+  // A rows are d bytes apart (X row-major): 64-bit per-lane row base, stage offset added
+  const uint8_t* arow[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    int64_t ra = m0 + (wave * 2 + jj) * 16 + lrow;
+    ra = ra < n ? ra : n - 1;
+    arow[jj] = X + ra * d + lchunk * 16;
+  }
+  voffB = (unsigned)((n0 + wave * 16 + lrow) * d + lchunk * 16);  // D is N x d (< 4 GiB)
+  const int64_t nst = d / PK;
+  auto issue = [&](int64_t st, int buf) {
+    const unsigned sbuf = lds_base + (unsigned)(buf * PSTAGE);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) glds16(arow[jj] + st * PK, sbuf + (unsigned)((wave * 2 + jj) * 1024));
+    glds16s(voffB + (unsigned)(st * PK), (unsigned long long)(size_t)D, sbuf + (unsigned)(PM * PK + wave * 1024));
+  };
+
+  i32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = i32x16{};
+
+  const int sw = (c32 >> 2) & 3;
+  const i32x4 flip = {(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+  // ring of PNB stages, 3 DMA instructions per wave per stage: "stage st landed" is
+  // vmcnt <= 3 x (stages issued after it); tail stages re-read stage 0 to keep counts uniform
+  for (int j = 0; j < PNB - 1; ++j) issue(j < nst ? j : 0, j);
+  for (int64_t st = 0; st < nst; ++st) {
+    const int buf = (int)(st % PNB);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // stage st landed (2 newer stages pending)
+    __syncthreads();                                   // ... for every wave; stage st-1 consumed
+    {
+      const int64_t nx = st + PNB - 1;
+      issue(nx < nst ? nx : 0, (int)(nx % PNB));
+    }
+    const uint8_t* sa = smem + buf * PSTAGE;
+    const uint8_t* sb = sa + PM * PK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r]
+      const int pch = ((2 * s + h) ^ sw) * 16;
+      i32x4 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = *reinterpret_cast<const i32x4*>(sa + (wm * 64 + i * 32 + c32) * PK + pch) ^ flip;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sb + (wn * 64 + j * 32 + c32) * PK + pch);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  dma_wait_all();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 32 + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < n) C[row * ldc + col] = acc[i][j][r];
+      }
+    }
+}
+
+// F[i][c] = 2^-t_c sum_j 256^j I[i][j kk + c] + cc[c]   (fp64 Horner)
+__global__ void proj_combine_kernel(const int* __restrict__ I, int64_t n, int kk, int64_t ldi,
+                                    const int* __restrict__ tsh, const double* __restrict__ cc,
+                                    double* __restrict__ F) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * kk) return;
+  const int64_t i = e / kk;
+  const int c = (int)(e - i * kk);
+  const int* row = I + i * ldi + c;
+  double v = (double)row[(int64_t)(kDigits - 1) * kk];
+#pragma unroll
+  for (int j = kDigits - 2; j >= 0; --j) v = fma(v, 256.0, (double)row[(int64_t)j * kk]);
+  F[e] = ldexp(v, -tsh[c]) + cc[c];
+}
+
+}  // namespace
+
+struct ProjLayout {
+  int64_t np, off_i, off_t, off_c, bytes;
+};
+static ProjLayout proj_layout(int64_t n, int64_t d, int kk) {
+  auto a256 = [](int64_t v) { return (v + 255) / 256 * 256; };
+  ProjLayout L;
+  L.np = (int64_t)(kDigits * kk + PN - 1) / PN * PN;
+  L.off_i = a256(L.np * d);
+  L.off_t = L.off_i + a256(n * L.np * (int64_t)sizeof(int));
+  L.off_c = L.off_t + a256((int64_t)kk * sizeof(int));
+  L.bytes = L.off_c + (int64_t)kk * sizeof(double);
+  return L;
+}
+
+bool proj_i8_supported(const uint8_t* X, int64_t n, int64_t d, int kk) {
+  return ((size_t)X & 15) == 0 && n >= 1 && d >= PK && d % PK == 0 && d <= 65536 && kk >= 1 &&
+         proj_layout(n, d, kk).np * d < ((int64_t)1 << 32);
+}
+
+size_t proj_i8_work_bytes(int64_t n, int64_t d, int kk) { return (size_t)proj_layout(n, d, kk).bytes; }
+
+hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, const double* mu, const double* w,
+                          const double* E, int kk, void* work, double* F) {
+  const ProjLayout L = proj_layout(n, d, kk);
+  const int64_t np = L.np;
+  uint8_t* base = static_cast<uint8_t*>(work);
+  int8_t* D = reinterpret_cast<int8_t*>(base);
+  int* I = reinterpret_cast<int*>(base + L.off_i);
+  int* tsh = reinterpret_cast<int*>(base + L.off_t);
+  double* cc = reinterpret_cast<double*>(base + L.off_c);
+  hipError_t e = hipMemsetAsync(D, 0, (size_t)(np * d), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(digit_scale_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, d, kk, tsh);
+  hipLaunchKernelGGL(digits_kernel, dim3((unsigned)((d * kk + 255) / 256)), dim3(256), 0, s, E, w, d, kk, tsh, D);
+  hipLaunchKernelGGL(cc_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, mu, d, kk, cc);
+  const int ntn = (int)(np / PN);
+  const int64_t nblocks = (n + PM - 1) / PM * ntn;
+  if (nblocks > (int64_t)1 << 30) return hipErrorInvalidValue;
+  const int grid = (int)((nblocks + 7) / 8 * 8);
+  hipLaunchKernelGGL(proj_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I, np);
+  hipLaunchKernelGGL(proj_combine_kernel, dim3((unsigned)((n * kk + 255) / 256)), dim3(256), 0, s, I, n, kk, np, tsh,
+                     cc, F);
+  return hipGetLastError();
+}
+
+}  // namespace ef

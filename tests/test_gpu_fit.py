@@ -130,3 +130,23 @@ def test_covariance_multi_pass(monkeypatch):
     np.testing.assert_allclose(mean, o_mean, rtol=1e-14)
     np.testing.assert_allclose(lam, o_lam, rtol=1e-9)
     np.testing.assert_allclose(_align(eig, o_eig), o_eig, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,side,k,std", [(3000, 16, 12, False), (700, 32, 40, True), (5000, 8, 64, True)])
+def test_training_projection_int8_digits(monkeypatch, n, side, k, std):
+    """F = ((X - mu) w) E through the int8 digit GEMM (ef_proj_i8.hip) equals the fp64 GEMM
+    path (EF_FIT_PROJ_F64) and the oracle to fp64 rounding (useless/train.py:122,
+    train-v4.py:134)."""
+    from eigenface import EigenfacePCA
+    x, _ = orc.synth_faces(n, side, r=min(48, side * side), seed=n + side)
+    m = EigenfacePCA(k, standardize=std).fit(x)
+    f8 = m.face_features_
+    monkeypatch.setenv("EF_FIT_PROJ_F64", "1")
+    m64 = EigenfacePCA(k, standardize=std).fit(x)
+    np.testing.assert_array_equal(m.components_, m64.components_)
+    scale = np.abs(m64.face_features_).max()
+    np.testing.assert_allclose(f8, m64.face_features_, rtol=0, atol=1e-12 * scale)
+    # and against the CPU restatement of the centred, scaled product
+    z = (x - m.scaler_mean_) / m.scaler_scale_ if std else x - m.mean_face_
+    ref = z @ m.components_.T
+    np.testing.assert_allclose(f8, ref, rtol=0, atol=1e-11 * np.abs(ref).max())
