@@ -10,4 +10,4 @@ rc=$?
 tail -3 $O/pytest.txt
 [ $rc -ne 0 ] && exit $rc
 EF_FIT_DEBUG=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/fr -o run -- python tools/prof_fit.py > $O/out.txt 2>&1 || exit $?
-python tools/fit_breakdown.py /tmp/fr/run_kernel_trace.csv > $O/breakdown.txt
+python tools/fit_breakdown.py /tmp/fr/run_kernel_trace.csv > $O/breakdown.txt && cp /tmp/fr/run_kernel_stats.csv $O/kernel_stats.csv
