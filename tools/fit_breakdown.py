@@ -11,12 +11,10 @@ t0 = int(last[0]["Start_Timestamp"])
 agg = collections.defaultdict(lambda: [0, 0.0])
 end = t0
 for r in last:
-    if "U8Ld" in r["Kernel_Name"]:
-        break
     a = agg[r["Kernel_Name"][:80]]
     a[0] += 1
     a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     end = int(r["End_Timestamp"])
-print(f"fit span {(end - t0) / 1e6:.1f} ms (first prep kernel -> last kernel before the training projection)")
+print(f"last fit (with training projection) span under the profiler {(end - t0) / 1e6:.1f} ms")
 for k, v in sorted(agg.items(), key=lambda x: -x[1][1])[:16]:
     print(f"{v[1]:9.2f} ms {v[0]:6d}x  {k}")
