@@ -174,7 +174,7 @@ hipError_t tri_solve_right(ef_ctx* c, hipStream_t s, double* Y, int64_t dim, int
 
 // Wide-block subspace iteration (m > kJacobiMax): orthonormalise by CholQR every
 // iteration (G = Y^T.Y = L.L^T, Q = Y.L^-T — one small Cholesky instead of an m x m
-// eigensolve), Rayleigh-Ritz (H = Q^T.C.Q, grid Jacobi) at iterations 1, 2, 4 and every
+// eigensolve), Rayleigh-Ritz (H = Q^T.C.Q, block Jacobi) at iterations (1, 2, 4,) 8 and every
 // rr_period(dim) after: its Ritz values give the convergence test, its vectors re-order the
 // block (Y <- Y.V), and the converged RR is the final one.  A numerically rank-deficient
 // block (Cholesky pivot <= 1e-13 of the largest) falls back to the eigen-orthonormalisation
@@ -236,8 +236,11 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
                          work, kWorkElems),
            "Y = C.Q");
-    // Rayleigh-Ritz at iterations 1, 2, 4, 8, then every rr_period(dim)
-    const bool rr = it <= 2 || it == 4 || it == 8 || it % rr_period(dim) == 0 || it == kMaxIters;
+    // Rayleigh-Ritz at iterations 1, 2, 4 (small orders only: there they re-order the block
+    // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
+    // no iteration count), 8, then every rr_period(dim)
+    const bool early = dim < 12288 && (it <= 2 || it == 4);
+    const bool rr = early || it == 8 || it % rr_period(dim) == 0 || it == kMaxIters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
                            work, kWorkElems),
