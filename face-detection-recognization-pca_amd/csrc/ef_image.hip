@@ -307,19 +307,23 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 
 // One workgroup = one work item: a 128 x 128 output tile of one problem, template rows
 // [ya, ya + J) of one column piece.  8 waves (2 per SIMD): wave w owns output rows
-// y0 + 32 (w & 3) + [0, 32) and the 32-column blocks 2 (w >> 2) and 2 (w >> 2) + 1.
-// Operands live in LDS, filled by LDS-DMA two template rows ahead:
+// y0 + 32 (w & 3) + [0, 32) and all four 32-column blocks, and the template rows of parity
+// w >> 2 — the two waves of a row block split the template rows and add their partial
+// sums at the end.  Per template row a wave reads NKB + 3 A and NKB B fragments for
+// 4 NKB MFMAs (the band's shift invariance: block n uses k-block kb - n).
+// Operands live in LDS, filled by LDS-DMA one row PAIR per barrier, two pairs ahead:
 //   * A ring: frame rows y0 + ya + q (q = 0 .. J + 126) in slot q % kTmRing, each row the
 //     32 (nkb + 3) bytes the tile reads, slot stride SA = 16 (mod 256) bytes, so the 16
-//     rows a ds_read_b128 lane group touches fall in distinct banks.  Iteration j reads
-//     slots j .. j + 127 and prefetches row j + 129 (one row per template row).
-//   * B ring: the band slice of template row ya + j (nkb KiB, lane-linear fragments) in
-//     stage j % 3, prefetched two rows ahead (A rows likewise).
-// One barrier per template row; a wave reads its NKB + 1 A and NKB B fragments of a
-// template row up front (compile-time NKB) for 2 NKB MFMAs.
-constexpr int kTmRing = 144;  // A-ring slots (>= 129; 144 * 16 = 0 mod 256 keeps banks aligned)
+//     rows a ds_read_b128 lane group touches fall in distinct banks.  Pair p reads slots
+//     2p .. 2p + 128 and prefetches rows 2p + 131, 2p + 132.
+//   * B ring: the band slices of template rows 2p, 2p + 1 (nkb KiB each, lane-linear
+//     fragments) in stage p % 3.
+// One barrier per template-row pair (half the barriers, and half the LDS fragment reads
+// per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).
+constexpr int kTmRing = 144;  // A-ring slots (>= 133; 144 * 16 = 0 mod 256 keeps banks aligned)
 constexpr int kTmMaxSA = 528;
 constexpr int kTmMaxNkb = (kTmPiece + 31 + 31) / 32;
+constexpr int kTmBStage = 2 * kTmMaxNkb * 1024;  // one row pair of band slices
 
 __global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restrict__ f8, int64_t pitch,
                                                          const uint8_t* __restrict__ bands,
@@ -327,85 +331,128 @@ __global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restric
                                                          const TmWork* __restrict__ works,
                                                          const TmProblem* __restrict__ probs, int* __restrict__ parts,
                                                          int nwork) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kTmRing * kTmMaxSA + 3 * kTmMaxNkb * 1024 + 1024];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kTmRing * kTmMaxSA + 3 * kTmBStage + 1024];
   const TmWork wk = works[blockIdx.x];
   const TmPiece pc = pieces[wk.piece];
   const TmProblem pb = probs[pc.prob];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr4 = wave & 3, wc = wave >> 2;  // 32-row block, column half (blocks 2wc, 2wc+1)
+  const int wr4 = wave & 3, par = wave >> 2;  // 32-row block, template-row parity
   const int r = lane & 31, h = lane >> 5;
   const int nkb = pc.nkb;
   const int RW = 32 * (nkb + 3);   // A-row bytes a tile reads
   const int SA = (RW + 255) / 256 * 256 + 16;  // slot stride = 16 (mod 256)
   const int nl = RW / 16;          // DMA lanes per A row
   const int J = wk.yb - wk.ya;
+  const int NP = (J + 1) / 2;      // template-row pairs
   const unsigned lds = lds_addr(smem);
   const unsigned ldsB = lds + (unsigned)(kTmRing * kTmMaxSA);
-  const unsigned ldsD = ldsB + (unsigned)(3 * kTmMaxNkb * 1024);  // dummy DMA target
+  const unsigned ldsD = ldsB + (unsigned)(3 * kTmBStage);  // dummy DMA target
   const int8_t* arow0 = f8 + (int64_t)(wk.y0 + wk.ya) * pitch + wk.x0 + pc.px + 16 * lane;  // + q * pitch
   const uint8_t* bsl0 = bands + pc.band_off + (int64_t)wk.ya * nkb * 1024 + 16 * lane;     // + j * nkb KiB
   // Rows >= hr are skipped per wave (uniform); NKB is a compile-time constant so the
   // k-block loop unrolls and every fragment read of a template row is issued up front.
-  const bool wact = wk.y0 + 32 * wr4 < pb.hr && wk.x0 + 64 * wc < pb.wr;
-  i32x16 acc0 = {}, acc1 = {};
+  const bool wact = wk.y0 + 32 * wr4 < pb.hr;
+  i32x16 acc[4] = {};
   auto run = [&](auto nkb_c) {
     constexpr int NKB = decltype(nkb_c)::value;
-    constexpr int Q = (NKB + 1 + 7) / 8;  // DMA instructions per wave per template row
-    // Template row j's operands: B pieces 0 .. NKB-1 into stage j % 3 and A row q = j + 127
-    // (completing the window j .. j + 127); wave w issues pieces w, w + 4, ..., padded with
-    // harmless dummy DMAs to exactly Q instructions, so "row j landed" is one vmcnt(Q).
-    auto issue = [&](int j) {
-#pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        const int p = wave + 8 * i;
-        if (p < NKB) {
-          glds16(bsl0 + ((int64_t)j * NKB + p) * 1024, ldsB + (unsigned)(((j % 3) * kTmMaxNkb + p) * 1024));
-        } else if (p == NKB) {
-          if (lane < nl) {
-            const int q = j + 127;
-            glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)((q % kTmRing) * SA));
-          }
+    constexpr int NPC = 2 * NKB + 2;       // DMA pieces per pair: 2 NKB band slices + 2 A rows
+    constexpr int Q = (NPC + 7) / 8;       // DMA instructions per wave per pair
+    // Pair p's operands: band slices of rows 2p, 2p+1 into stage p % 3 and A rows
+    // q = 2p + 127, 2p + 128 (completing the windows of rows 2p, 2p + 1); wave w issues
+    // pieces w, w + 8, ..., padded with harmless dummy DMAs to exactly Q instructions, so
+    // "pair p landed" is a vmcnt of Q x (pairs issued after it).
+    auto issue_piece = [&](int p, int i) {
+      const int pi = wave + 8 * i;
+      if (pi < 2 * NKB) {
+        const int rr = pi / NKB, kb = pi - (pi / NKB) * NKB, j = 2 * p + rr;
+        if (j < J)
+          glds16(bsl0 + ((int64_t)j * NKB + kb) * 1024,
+                 ldsB + (unsigned)((p % 3) * kTmBStage + (rr * kTmMaxNkb + kb) * 1024));
+        else
+          glds16(bsl0, ldsD);
+      } else if (pi < NPC) {
+        const int q = 2 * p + 127 + (pi - 2 * NKB);
+        if (q < J + 127) {
+          if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)((q % kTmRing) * SA));
         } else {
           glds16(bsl0, ldsD);
         }
+      } else {
+        glds16(bsl0, ldsD);
       }
+    };
+    auto issue = [&](int p) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) issue_piece(p, i);
     };
     for (int q = wave; q < 127; q += 8)
       if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)(q * SA));
     issue(0);
-    if (J > 1) {
+    if (NP > 1) {
       issue(1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");
     } else {
       dma_wait_all();
     }
     __syncthreads();
-    for (int j = 0; j < J; ++j) {
-      const bool ahead = j + 2 < J;
-      if (ahead) issue(j + 2);
-      if (wact) {
-        // this wave's A starts 64 columns in for the second column half; block 2wc + n
-        // then uses B's k-block kb - n of its own A steps
-        const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 64 * wc + 16 * h;
-        const uint8_t* bst = smem + kTmRing * kTmMaxSA + (j % 3) * kTmMaxNkb * 1024 + 16 * lane;
-        i32x4 A[NKB + 1], B[NKB];
+#ifdef EF_TM_STAMP
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define EF_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph[i] += t_ - tq; tq = t_; } while (0)
+#else
+#define EF_STAMP(i) do {} while (0)
+#endif
+    for (int p = 0; p < NP; ++p) {
+      const bool ahead = p + 2 < NP;
+      const int j = 2 * p + par;
+      EF_STAMP(0);
+      if (wact && j < J) {
+        const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+        const uint8_t* bst = smem + kTmRing * kTmMaxSA + (p % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
+        i32x4 A[NKB + 3], B[NKB];
 #pragma unroll
-        for (int kb = 0; kb < NKB + 1; ++kb) A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
-#pragma unroll
-        for (int kb = 0; kb < NKB + 1; ++kb) {
-          if (kb < NKB) acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb], acc0, 0, 0, 0);
-          if (kb >= 1) acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - 1], acc1, 0, 0, 0);
+        for (int kb = 0; kb < NKB + 3; ++kb) {  // in the order the MFMAs consume them
+          A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
+          if (kb < NKB) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
         }
+        // pair p+2's DMA pieces are issued between the MFMAs (evenly spaced), not as a burst
+        // after the barrier: a burst of 32 LDS-DMA instructions per CU kept every wave in
+        // its issue phase (~800 cycles per pair) with the MFMA pipe idle
+        int m = 0;
+#pragma unroll
+        for (int kb = 0; kb < NKB + 3; ++kb)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            if (kb - n >= 0 && kb - n < NKB) {
+              acc[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - n], acc[n], 0, 0, 0);
+              ++m;
+#pragma unroll
+              for (int i = 0; i < Q; ++i)
+                if (m == (i + 1) * (4 * NKB) / (Q + 1)) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  if (ahead) issue_piece(p + 2, i);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+      } else if (ahead) {
+        issue(p + 2);
       }
+      EF_STAMP(1);
       if (ahead)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");  // row j + 1 landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");  // pair p + 1 landed
       else
         dma_wait_all();
-      __syncthreads();  // ... for every wave; everyone is done with stage j % 3 and slot j
+      EF_STAMP(2);
+      __syncthreads();  // ... for every wave; everyone is done with stage p % 3 and its slots
+      EF_STAMP(3);
     }
+#ifdef EF_TM_STAMP
+    if (blockIdx.x % 97 == 0 && lane == 0 && (wave == 0 || wave == 4))
+      printf("tmstamp blk %d wave %d nkb %d pairs %d issue %llu mfma %llu vmwait %llu barrier %llu\n", (int)blockIdx.x,
+             wave, NKB, NP, ph[0], ph[1], ph[2], ph[3]);
+#endif
+#undef EF_STAMP
   };
   switch (nkb) {
 #define EF_TM_NKB(V) \
@@ -418,19 +465,28 @@ __global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restric
     default:
       break;
   }
-  if (!wact) return;
+  // the odd-row waves hand their partial sums to the even-row waves through LDS (the ring
+  // is free: the loop ended with a barrier after every DMA landed)
+  int* red = reinterpret_cast<int*>(smem) + (wr4 * 4 * 16 * 64);
+  if (par == 1 && wact) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) red[(n * 16 + g) * 64 + lane] = acc[n][g];
+  }
+  __syncthreads();
+  if (par == 1 || !wact) return;
   int* out = parts + pb.part_off + (int64_t)wk.part * pb.hr * pb.wr;
-  auto store = [&](const i32x16& v, int n) {
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
     const int x = wk.x0 + 32 * n + r;
-    if (x >= pb.wr) return;
+    if (x >= pb.wr) continue;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int y = wk.y0 + 32 * wr4 + (g & 3) + 8 * (g >> 2) + 4 * h;
-      if (y < pb.hr) out[(int64_t)y * pb.wr + x] = v[g];
+      if (y < pb.hr) out[(int64_t)y * pb.wr + x] = acc[n][g] + red[(n * 16 + g) * 64 + lane];
     }
-  };
-  store(acc0, 2 * wc);
-  store(acc1, 2 * wc + 1);
+  }
 }
 
 // OpenCV's TM_CCOEFF_NORMED rule (templmatch.cpp common_matchTemplate) on exact integers.

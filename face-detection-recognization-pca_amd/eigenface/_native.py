@@ -10,6 +10,9 @@ import os
 import threading
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libeigenface.so")
+# diagnostic builds (instrumented / ablated kernels, never a non-HIP fallback) by name
+if os.environ.get("EF_LIB_VARIANT"):
+    LIB_PATH = LIB_PATH.replace("libeigenface.so", f"libeigenface_{os.environ['EF_LIB_VARIANT']}.so")
 
 EF_OK = 0
 EF_U8, EF_F32, EF_F64 = 0, 1, 2
