@@ -215,14 +215,16 @@ __global__ __launch_bounds__(256) void tm_rows_kernel(const uint8_t* __restrict_
   }
 }
 
-// Column prefix of the row sums: block = 64 columns x 16 row segments.
+// Column prefix of the row sums: block = 16 columns x 64 row segments (a 641-column frame
+// is 41 workgroups, not 11: the pass is latency-bound, so it wants many short segments).
+constexpr int kColW = 16, kColSeg = 64;
 __global__ __launch_bounds__(1024) void tm_cols_kernel(int H, int W, long long* __restrict__ ii1,
                                                        long long* __restrict__ ii2) {
-  __shared__ long long t1[16][64], t2[16][64];
-  const int cx = threadIdx.x & 63, sg = threadIdx.x >> 6;
-  const int x = blockIdx.x * 64 + cx;
+  __shared__ long long t1[kColSeg][kColW], t2[kColSeg][kColW];
+  const int cx = threadIdx.x % kColW, sg = threadIdx.x / kColW;
+  const int x = blockIdx.x * kColW + cx;
   const int64_t W1 = W + 1;
-  const int per = (H + 15) / 16;
+  const int per = (H + kColSeg - 1) / kColSeg;
   const int ya = 1 + sg * per, yb = ya + per < H + 1 ? ya + per : H + 1;
   long long s1 = 0, s2 = 0;
   if (x <= W) {
@@ -490,9 +492,10 @@ __global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restric
 }
 
 // OpenCV's TM_CCOEFF_NORMED rule (templmatch.cpp common_matchTemplate) on exact integers.
-__device__ __forceinline__ float tm_score(long long numN, long long varI, long long varT) {
+// sqT = sqrt((double)varT), hoisted per problem (the same correctly rounded value).
+__device__ __forceinline__ float tm_score(long long numN, long long varI, long long varT, double sqT) {
   if (varT == 0) return 1.f;  // flat template: all ones
-  const double t = __dmul_rn(sqrt((double)varI), sqrt((double)varT));
+  const double t = __dmul_rn(sqrt((double)varI), sqT);
   const double num = (double)numN;
   const double an = fabs(num);
   double rr;
@@ -522,22 +525,28 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
                                                        unsigned long long* __restrict__ keys) {
   const TmProblem pb = probs[blockIdx.y];
   const TmStat ts = st[blockIdx.y];
+  const double sqT = sqrt((double)ts.varT);
   const int64_t npos = (int64_t)pb.hr * pb.wr;
   const long long n = (long long)pb.th * pb.tw;
   const int64_t W1 = W + 1;
   unsigned long long key = ~0ull;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npos; i += (int64_t)gridDim.x * 256) {
-    const int y = (int)(i / pb.wr), x = (int)(i - (i / pb.wr) * pb.wr);
-    long long P = 0;
-    const int* pp = parts + pb.part_off + i;
-    for (int q = 0; q < pb.nparts; ++q) P += pp[(int64_t)q * npos];
-    const int64_t a = (int64_t)y * W1 + x, b = (int64_t)(y + pb.th) * W1 + x;
-    const long long sI = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
-    const long long sI2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
-    const float v = tm_score(n * P - ts.sT * sI, n * sI2 - sI * sI, ts.varT);
-    if (maps) maps[pb.map_off + i] = v;
-    const unsigned long long k = tm_key(v, (unsigned)i);
-    key = k < key ? k : key;
+  // rows are strided over the blocks of this problem, columns over the threads (no 64-bit
+  // index division per position)
+  for (int y = blockIdx.x; y < pb.hr; y += gridDim.x) {
+    const int64_t a0 = (int64_t)y * W1, b0 = (int64_t)(y + pb.th) * W1;
+    for (int x = threadIdx.x; x < pb.wr; x += 256) {
+      const int64_t i = (int64_t)y * pb.wr + x;
+      long long P = 0;
+      const int* pp = parts + pb.part_off + i;
+      for (int q = 0; q < pb.nparts; ++q) P += pp[(int64_t)q * npos];
+      const int64_t a = a0 + x, b = b0 + x;
+      const long long sI = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
+      const long long sI2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
+      const float v = tm_score(n * P - ts.sT * sI, n * sI2 - sI * sI, ts.varT, sqT);
+      if (maps) maps[pb.map_off + i] = v;
+      const unsigned long long k = tm_key(v, (unsigned)i);
+      key = k < key ? k : key;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -779,7 +788,7 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
   timer_begin(c, EF_KERNEL_TMATCH, &tev);
   hipLaunchKernelGGL(tm_rows_kernel, dim3((unsigned)((H + 1 + 3) / 4)), dim3(256), 0, s, f, H, W, frame_ld, f8,
                      t->pitch, ii1, ii2);
-  hipLaunchKernelGGL(tm_cols_kernel, dim3((unsigned)((W + 1 + 63) / 64)), dim3(1024), 0, s, H, W, ii1, ii2);
+  hipLaunchKernelGGL(tm_cols_kernel, dim3((unsigned)((W + 1 + kColW - 1) / kColW)), dim3(1024), 0, s, H, W, ii1, ii2);
   if (t->nprob > 0) {
     unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
     hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((t->nprob + 255) / 256)), dim3(256), 0, s, keys, t->nprob);
@@ -797,7 +806,7 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
         maps = static_cast<float*>(t->maps.p);
       }
     }
-    const int64_t sblk = std::min<int64_t>((t->max_pos + 255) / 256, 32);
+    const int64_t sblk = 64;  // row-strided blocks per problem
     hipLaunchKernelGGL(tm_score_kernel, dim3((unsigned)sblk, (unsigned)t->nprob), dim3(256), 0,
                        s, static_cast<const TmProblem*>(t->d_probs.p), static_cast<const TmStat*>(t->d_stat.p),
                        static_cast<const int*>(t->parts.p), ii1, ii2, W, maps, keys);
