@@ -225,23 +225,82 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
 
 // Pass 2: the invoker's x walk for each (layer, evaluated row): positions 0, step, ...
 // with one extra step after a stage-0 rejection; survivors of stage 0 go to the list.
-__global__ void haar_rows_kernel(const HaarLayer* __restrict__ L, int nlayers, const int* __restrict__ row_start,
-                                 const signed char* __restrict__ res, HaarCand* __restrict__ work,
-                                 int* __restrict__ nwork, int cap) {
-  const int gr = blockIdx.x * blockDim.x + threadIdx.x;  // global evaluated-row index
-  if (gr >= row_start[nlayers]) return;
+// One wave per row, 16 rows per workgroup: 64 positions per chunk are loaded coalesced,
+// the walk's recurrence (position i+1 is visited unless i was visited and rejected) is
+// solved in closed form on the wave-uniform ballot masks, and the workgroup appends all
+// its rows' survivors with ONE atomicAdd (count pass, then write pass).  A thread-per-row
+// walk of dependent byte loads with per-survivor atomics took ~150 us per 640x480 frame;
+// one atomic per chunk still ~90 us (a single counter serialises them).
+constexpr int kHaarRowWaves = 16;
+constexpr int kHaarMaxLayers = 255;
+
+__device__ __forceinline__ unsigned long long haar_walk(unsigned long long rej, bool& v) {
+  // within a run of rejected positions the walk visits every other one from the run's
+  // first (visited) position; right after a run it visits unless the run's last position
+  // was visited.  A position is a run start when the one before it is not rejected (or,
+  // for bit 0, when the carried-in position is visited).
+  const unsigned long long EVEN = 0x5555555555555555ull;
+  const unsigned long long R = v ? rej : (rej & ~1ull);  // an unvisited bit 0 cannot skip
+  const unsigned long long S = R & ~(R << 1);             // run starts
+  const unsigned long long RE = R & ~(R + (S & EVEN));    // runs that start at even bits
+  const unsigned long long E = (RE & EVEN) | (R & ~RE & ~EVEN);  // even offset in its run
+  unsigned long long vis = (R & E) | (~R & ~((R & E) << 1));
+  if (!v) vis &= ~1ull;
+  v = !(((vis >> 63) & 1ull) && ((rej >> 63) & 1ull));
+  return vis;
+}
+
+__global__ __launch_bounds__(1024) void haar_rows_kernel(const HaarLayer* __restrict__ L, int nlayers,
+                                                         const int* __restrict__ row_start,
+                                                         const signed char* __restrict__ res,
+                                                         HaarCand* __restrict__ work, int* __restrict__ nwork,
+                                                         int cap) {
+  __shared__ int rs[kHaarMaxLayers + 1];
+  __shared__ int woff[kHaarRowWaves];
+  for (int i = threadIdx.x; i <= nlayers; i += blockDim.x) rs[i] = row_start[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gr = blockIdx.x * kHaarRowWaves + wave;  // evaluated row of this wave
+  const bool live = gr < rs[nlayers];
   int li = 0;
-  while (row_start[li + 1] <= gr) ++li;
+  if (live)
+    while (rs[li + 1] <= gr) ++li;
   const HaarLayer ly = L[li];
-  const int y = (gr - row_start[li]) * ly.step;
+  const int y = live ? (gr - rs[li]) * ly.step : 0;
   const signed char* rr = res + ly.res_off + (int64_t)y * ly.nx;
-  for (int x = 0; x < ly.nx; x += ly.step) {
-    const signed char r = rr[x];
-    if (r > 0) {
-      const int k = atomicAdd(nwork, 1);
-      if (k < cap) work[k] = HaarCand{li, y, x, 0};
+  const int npos = live ? (ly.nx + ly.step - 1) / ly.step : 0;  // visited candidates: x = i * step
+  auto chunk = [&](int c0, bool& v) {
+    const int i = c0 + lane;
+    const signed char r = i < npos ? rr[(int64_t)i * ly.step] : (signed char)-1;
+    const unsigned long long rej = __ballot(r == 0);
+    const unsigned long long pas = __ballot(r > 0);
+    return haar_walk(rej, v) & pas;
+  };
+  int total = 0;
+  bool v = true;
+  for (int c0 = 0; c0 < npos; c0 += 64) total += __popcll(chunk(c0, v));
+  if (lane == 0) woff[wave] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int sum = 0;
+    for (int w = 0; w < kHaarRowWaves; ++w) {
+      const int t = woff[w];
+      woff[w] = sum;
+      sum += t;
     }
-    if (r == 0) x += ly.step;
+    const int base = sum ? atomicAdd(nwork, sum) : 0;
+    for (int w = 0; w < kHaarRowWaves; ++w) woff[w] += base;
+  }
+  __syncthreads();
+  int k = woff[wave];
+  v = true;
+  for (int c0 = 0; c0 < npos; c0 += 64) {
+    const unsigned long long surv = chunk(c0, v);
+    if ((surv >> lane) & 1ull) {
+      const int kk = k + __popcll(surv & ((1ull << lane) - 1ull));
+      if (kk < cap) work[kk] = HaarCand{li, y, (c0 + lane) * ly.step, 0};
+    }
+    k += __popcll(surv);
   }
 }
 
@@ -472,6 +531,9 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   if (n_cand) *n_cand = 0;
   if (layers.empty()) return EF_OK;
   const int nl = (int)layers.size();
+  if (nl > kHaarMaxLayers)
+    return set_err(c, EF_E_INVALID, "ef_haar_detect: more than " + std::to_string(kHaarMaxLayers) +
+                                        " pyramid layers (scale factor too close to 1)");
   std::vector<int> row_start(nl + 1, 0);
   for (int i = 0; i < nl; ++i) row_start[i + 1] = row_start[i] + (layers[i].ny + layers[i].step - 1) / layers[i].step;
   const int cap = 1 << 20;  // candidate / work-list capacity (windows surviving stage 0)
@@ -532,7 +594,8 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   int* cnt = static_cast<int*>(h->counters.p);
   HaarCand* work = static_cast<HaarCand*>(h->work.p);
   HaarCand* cand = static_cast<HaarCand*>(h->cand.p);
-  hipLaunchKernelGGL(haar_rows_kernel, dim3((unsigned)((row_start[nl] + 63) / 64)), dim3(64), 0, s, dl, nl,
+  hipLaunchKernelGGL(haar_rows_kernel, dim3((unsigned)((row_start[nl] + kHaarRowWaves - 1) / kHaarRowWaves)),
+                     dim3(64 * kHaarRowWaves), 0, s, dl, nl,
                      static_cast<const int*>(h->rowstart.p), res, work, cnt, cap);
   int hc[16] = {0};
   EF_HIP(c, hipMemcpyAsync(hc, cnt, sizeof(int), hipMemcpyDeviceToHost, s), "D2H work count");
