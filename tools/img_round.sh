@@ -10,4 +10,4 @@ rc=$?
 tail -3 $O/pytest.txt
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ir -o run -- python tools/prof_image.py > $O/out.txt 2>&1 || exit $?
-cp /tmp/ir/run_kernel_stats.csv $O/kernel_stats.csv
+cp /tmp/ir/run_kernel_stats.csv $O/kernel_stats.csv && grep -E "haar|Kernel_Name" /tmp/ir/run_kernel_trace.csv > $O/haar_trace.csv
