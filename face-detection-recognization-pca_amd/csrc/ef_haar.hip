@@ -32,6 +32,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -618,6 +620,11 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   EF_HIP(c, hipGetLastError(), "haar kernels");
   EF_HIP(c, hipMemcpyAsync(hc, cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, s), "D2H counts");
   EF_HIP(c, hipStreamSynchronize(s), "sync");
+  if (getenv("EF_HAAR_DEBUG")) {
+    fprintf(stderr, "[ef_haar] stage-group inputs:");
+    for (int g = 0; g <= gi; ++g) fprintf(stderr, " %d", hc[g]);
+    fprintf(stderr, "\n");
+  }
   hc[1] = hc[gi];  // survivors of the last group (all of stage 0's when the cascade has 1 stage)
   cand = bin;
   if (hc[1] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: candidate capacity exceeded");
