@@ -348,7 +348,7 @@ __global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int 
                                                     int* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) double P[];  // [m - jb][kCholPS]
   __shared__ double red[1024];
-  __shared__ double piv;
+  __shared__ double piv_s[kCholNB];
   const int tid = threadIdx.x, nth = blockDim.x;
   double mx = 0.0;
   for (int i = tid; i < m; i += nth) mx = fmax(mx, A[(int64_t)i * lda + i]);
@@ -367,27 +367,30 @@ __global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int 
       P[i * kCholPS + t] = t < nb ? A[(int64_t)(jb + i) * lda + jb + t] : 0.0;
     }
     __syncthreads();
-    for (int t = 0; t < nb; ++t) {  // unblocked factorisation of the panel
-      if (tid == 0) {
-        const double dj = P[t * kCholPS + t];
-        piv = (dj > tol) ? sqrt(dj) : -1.0;
-        if (piv > 0.0) P[t * kCholPS + t] = piv;
-      }
-      __syncthreads();
-      const double p = piv;
-      if (p < 0.0) {
+    // unblocked factorisation of the panel on UNSCALED columns (A[i][l] -= a_it a_lt / d_t,
+    // the chol_small_kernel form): every thread reads the pivot itself, so a column step
+    // is one barrier instead of three; the columns are scaled by 1/sqrt(d_t) afterwards
+    for (int t = 0; t < nb; ++t) {
+      const double d = P[t * kCholPS + t];
+      if (!(d > tol)) {  // uniform: every thread read the same pivot
         if (tid == 0) *info = -(jb + t + 1);
         return;
       }
-      for (int i = t + 1 + tid; i < rows; i += nth) P[i * kCholPS + t] /= p;
-      __syncthreads();
+      const double inv = 1.0 / d;
       const int w = nb - t - 1;  // update the panel's remaining columns
       for (int e = tid; e < (rows - t - 1) * w; e += nth) {
         const int i = t + 1 + e / w, l = t + 1 + e % w;
-        if (l <= i) P[i * kCholPS + l] -= P[i * kCholPS + t] * P[l * kCholPS + t];
+        if (l <= i) P[i * kCholPS + l] -= P[i * kCholPS + t] * (P[l * kCholPS + t] * inv);
       }
       __syncthreads();
     }
+    if (tid < nb) piv_s[tid] = sqrt(P[tid * kCholPS + tid]);
+    __syncthreads();
+    for (int e = tid; e < rows * nb; e += nth) {
+      const int i = e / nb, t = e % nb;
+      if (i >= t) P[i * kCholPS + t] /= piv_s[t];
+    }
+    __syncthreads();
     for (int e = tid; e < rows * kCholNB; e += nth) {  // store the panel
       const int i = e / kCholNB, t = e % kCholNB;
       if (t < nb && t <= i) A[(int64_t)(jb + i) * lda + jb + t] = P[i * kCholPS + t];
