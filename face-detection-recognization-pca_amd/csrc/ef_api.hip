@@ -191,6 +191,7 @@ void ef_destroy(ef_ctx* c) {
                     &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
+  for (auto& b : c->fit_pool) release(b);
   blas_release(c);
   tm_release(c);
   haar_release(c);
@@ -215,6 +216,15 @@ int ef_use_own_stream(ef_ctx* c) {
 int ef_synchronize(ef_ctx* c) {
   if (!c) return EF_E_INVALID;
   EF_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return EF_OK;
+}
+
+int ef_trim(ef_ctx* c) {
+  if (!c) return EF_E_INVALID;
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  EF_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  for (auto& b : c->fit_pool) release(b);
+  c->fit_pool.clear();
   return EF_OK;
 }
 

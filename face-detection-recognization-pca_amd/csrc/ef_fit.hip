@@ -36,24 +36,19 @@ namespace {
 
 using namespace ef;
 
+// Workspaces of one fit: slots of the context's pool (ef_ctx::fit_pool), grown on demand
+// and kept for the next fit — a C3 fit otherwise spends tens of ms in hipMalloc/hipFree of
+// its ~30 GB of operand copies and blocks.  ef_trim releases the pool.
 struct Bufs {
-  std::vector<DevBuf> v;
-  ~Bufs() {
-    for (auto& b : v) release(b);
-  }
+  size_t next = 0;
   template <class T>
-  void drop(hipStream_t s, T* p) {  // release one buffer early (after the stream drains)
-    for (auto& b : v)
-      if (b.p == static_cast<void*>(p)) {
-        (void)hipStreamSynchronize(s);
-        release(b);
-      }
-  }
+  void drop(hipStream_t, T*) {}  // pooled: the slot stays allocated for the next fit
   template <class T>
   int get(ef_ctx* c, size_t count, T** out) {
-    v.emplace_back();
-    const int rc = ensure(c, v.back(), count * sizeof(T) + 16);
-    *out = static_cast<T*>(v.back().p);
+    if (c->fit_pool.size() <= next) c->fit_pool.resize(next + 1);
+    DevBuf& b = c->fit_pool[next++];
+    const int rc = ensure(c, b, count * sizeof(T) + 16);
+    *out = static_cast<T*>(b.p);
     return rc;
   }
 };
@@ -183,6 +178,33 @@ hipError_t tri_solve_right(ef_ctx* c, hipStream_t s, double* Y, int64_t dim, int
 inline int rr_period(int64_t dim) { return dim >= 12288 ? 8 : 16; }
 constexpr int kCholeskyMax = 512;  // launch_cholesky's LDS panel limit (wider: eigen-orthonormalise)
 
+__global__ void f64_to_f32_kernel(const double* __restrict__ a, int64_t n, float* __restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = (float)a[i];
+}
+__global__ void f32_to_f64_kernel(const float* __restrict__ a, int64_t n, double* __restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = (double)a[i];
+}
+static void cvt64to32(hipStream_t s, const double* a, int64_t n, float* b) {
+  hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
+                     b);
+}
+static void cvt32to64(hipStream_t s, const float* a, int64_t n, double* b) {
+  hipLaunchKernelGGL(f32_to_f64_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
+                     b);
+}
+// Y32 (dim x m) = C32 (dim x dim) . Q32 (dim x m), row-major, rocBLAS sgemm.
+static bool sgemm_cq(ef_ctx* c, hipStream_t s, const float* C32, const float* Q32, int64_t dim, int m, float* Y32) {
+  if (!c->blas) return false;
+  rocblas_handle h = static_cast<rocblas_handle>(c->blas);
+  const float one = 1.f, zero = 0.f;
+  return rocblas_set_stream(h, s) == rocblas_status_success &&
+         rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)dim,
+                       (rocblas_int)dim, &one, Q32, (rocblas_int)m, C32, (rocblas_int)dim, &zero, Y32,
+                       (rocblas_int)m) == rocblas_status_success;
+}
+
 int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int m, double* work, double* U_out,
                   double* lam_out, int* iters) {
   hipStream_t s = c->stream;
@@ -229,13 +251,32 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   };
   EF_TRY(orthonormalise());
 
+  // Coarse phase in fp32: while the Ritz values still move by > 1e-4 between Rayleigh-Ritz
+  // steps, Y = C.Q runs as an fp32 sgemm on an fp32 copy of C (twice the fp64 matrix
+  // rate); the iteration is self-correcting, and convergence is only declared between two
+  // Rayleigh-Ritz steps that both follow fp64 products, so the result is the fp64 one.
+  float *C32 = nullptr, *Q32 = nullptr, *Y32 = nullptr;
+  bool coarse = dim >= 4096 && c->blas != nullptr && !getenv("EF_FIT_NO_FP32");
+  if (coarse) {
+    EF_TRY(B.get(c, (size_t)dim * dim, &C32));
+    EF_TRY(B.get(c, (size_t)dim * m, &Q32));
+    EF_TRY(B.get(c, (size_t)dim * m, &Y32));
+    cvt64to32(s, C, dim * dim, C32);
+  }
   std::vector<double> th(m), prev(m, 0.0);
-  bool have_prev = false;
+  bool have_prev = false, prev_fine = false;
   int it = 0;
   for (it = 1; it <= kMaxIters; ++it) {
-    EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
-                         work, kWorkElems),
-           "Y = C.Q");
+    const bool fine = !coarse;  // this iteration's product is fp64
+    if (coarse) {
+      cvt64to32(s, Q, dim * m, Q32);
+      if (!sgemm_cq(c, s, C32, Q32, dim, m, Y32)) return set_err(c, EF_E_HIP, "Y = C.Q (sgemm)");
+      cvt32to64(s, Y32, dim * m, Y);
+    } else {
+      EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
+                           work, kWorkElems),
+             "Y = C.Q");
+    }
     // Rayleigh-Ritz at iterations 1, 2, 4 (small orders only: there they re-order the block
     // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
     // no iteration count), 8, then every rr_period(dim)
@@ -251,21 +292,22 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       if (!std::isfinite(th[0])) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
       // converged when every kept Ritz value moved by <= 1e-13 relative (floor 1e-15 of
       // the largest) since the previous Rayleigh-Ritz step
-      bool ok = have_prev;
+      bool ok = have_prev && prev_fine && fine;
       for (int i = 0; i < kk && ok; ++i)
         ok = std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * std::fabs(th[i]), 1e-15 * std::fabs(th[0]));
-      if (getenv("EF_FIT_DEBUG")) {
-        double worst = 0;
-        int wi = 0;
-        for (int i = 0; i < kk && have_prev; ++i) {
-          const double r = std::fabs(th[i] - prev[i]) / std::fmax(std::fabs(th[i]), 1e-300);
-          if (r > worst) worst = r, wi = i;
-        }
-        fprintf(stderr, "[ef_fit] rr it=%d sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g\n", it,
-                se.sweeps, worst, wi, th[kk - 1], th[m - 1]);
+      double worst = have_prev ? 0.0 : 1.0;
+      int wi = 0;
+      for (int i = 0; i < kk && have_prev; ++i) {
+        const double r = std::fabs(th[i] - prev[i]) / std::fmax(std::fabs(th[i]), 1e-300);
+        if (r > worst) worst = r, wi = i;
       }
+      if (getenv("EF_FIT_DEBUG"))
+        fprintf(stderr, "[ef_fit] rr it=%d %s sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g\n", it,
+                fine ? "fp64" : "fp32", se.sweeps, worst, wi, th[kk - 1], th[m - 1]);
+      if (coarse && worst < 1e-4) coarse = false;  // fp64 products from the next iteration on
       prev = th;
       have_prev = true;
+      prev_fine = fine;
       if (ok || it == kMaxIters) {
         EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
                              kk, work, kWorkElems),

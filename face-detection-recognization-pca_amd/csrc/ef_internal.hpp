@@ -94,6 +94,8 @@ struct ef_ctx {
   ef::DevBuf proj_part; // float[nsplit][bpad][kpw]
   ef::DevBuf feats_dev; // float[b][k] staging for host output
 
+  std::vector<ef::DevBuf> fit_pool;  // ef_fit workspaces, reused across calls (ef_trim frees)
+
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
   void* blas = nullptr;  // rocBLAS handle (fit's plain dense products), lazily created

@@ -51,6 +51,7 @@ _SIGS = {
     "ef_set_stream": ([vp, vp], C.c_int),
     "ef_use_own_stream": ([vp], C.c_int),
     "ef_synchronize": ([vp], C.c_int),
+    "ef_trim": ([vp], C.c_int),
     "ef_fit": ([vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
     "ef_model_set": ([vp, vp, vp, i64, i32, u32], C.c_int),
     "ef_project": ([vp, vp, i32, i64, vp, u32], C.c_int),

@@ -111,6 +111,10 @@ class Engine:
     def synchronize(self):
         self._chk(self._lib.ef_synchronize(self._h))
 
+    def trim(self):
+        """Free the fit workspaces the context keeps between fits (ef_trim)."""
+        self._chk(self._lib.ef_trim(self._h))
+
     # ------------------------------------------------------------------------ fit
     def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
         """GPU eigenfaces fit of uint8 faces X (n x d); see include/eigenface.h ef_fit.

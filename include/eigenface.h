@@ -78,6 +78,10 @@ const char* ef_last_error(const ef_ctx* ctx);
 int ef_set_stream(ef_ctx* ctx, void* hip_stream);
 int ef_use_own_stream(ef_ctx* ctx);
 int ef_synchronize(ef_ctx* ctx);
+/* ef_fit keeps its device workspaces (operand copies, covariance, subspace blocks) in
+ * the context between calls, so repeated fits do not pay hipMalloc/hipFree; ef_trim
+ * frees them (ef_destroy does too). */
+int ef_trim(ef_ctx* ctx);
 
 /* -------------------------------------------------------------------- fit
  * Replaces manual_pca (useless/train.py:56-128) and, with EF_FIT_STANDARDIZE,
