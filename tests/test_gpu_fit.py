@@ -150,3 +150,23 @@ def test_training_projection_int8_digits(monkeypatch, n, side, k, std):
     z = (x - m.scaler_mean_) / m.scaler_scale_ if std else x - m.mean_face_
     ref = z @ m.components_.T
     np.testing.assert_allclose(f8, ref, rtol=0, atol=1e-11 * np.abs(ref).max())
+
+
+def test_pooled_workspaces_refit_and_trim():
+    """ef_fit reuses the context's pooled workspaces across calls of different shapes
+    (grow-only slots) and ef_trim frees them; results stay identical to a fresh context."""
+    from eigenface import Engine
+    xa, _ = orc.synth_faces(900, 16, r=32, seed=21)   # covariance path
+    xb, _ = orc.synth_faces(120, 32, r=32, seed=22)   # Gram path
+    with Engine(0) as e:
+        ra1 = e.fit(xa, 10)
+        rb1 = e.fit(xb, 10)
+        ra2 = e.fit(xa, 10)
+        e.trim()
+        rb2 = e.fit(xb, 10)
+    with Engine(0) as f:
+        ra3 = f.fit(xa, 10)
+    np.testing.assert_array_equal(ra1.components, ra2.components)
+    np.testing.assert_array_equal(ra1.components, ra3.components)
+    np.testing.assert_array_equal(rb1.components, rb2.components)
+    np.testing.assert_array_equal(ra1.projection, ra3.projection)
