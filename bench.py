@@ -350,7 +350,9 @@ def haar_bench(eng, with_cpu: bool, frames=10):
     dt = (time.perf_counter() - t) / frames
     k_ms, k_n = eng.timing_get("haar")
     out = {"config": "640x480 grey frame, scaleFactor 1.1, minNeighbors 5, minSize 30x30, synthetic 25-stage "
-                     "2913-stump cascade (60 % pass per stage)",
+                     "2913-stump cascade (60 % pass per stage on calibration windows); the frame holds no face, so "
+                     "no window survives all stages: the work is ~260k stage-0 survivors through up to 24 stages "
+                     "(detections are parity-tested against the oracle in tests/test_gpu_haar.py)",
            "frames_per_s": round(1 / dt, 2), "ms_per_frame_host": round(dt * 1e3, 4),
            "ms_per_frame_device": round(k_ms / max(k_n, 1), 4), "candidates": int(len(cand)),
            "detections": int(len(rects))}
