@@ -331,9 +331,68 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
   if (k < cap) out[k] = w;
 }
 
+// Pass 3, split form: a workgroup of 4 waves takes 64 windows (lane = window, as above, so
+// each stump's integral-image gathers stay coalesced over neighbouring windows) and wave q
+// evaluates the q-th quarter of every stage's stumps; the four partial sums are combined
+// in LDS.  4x the waves of the thread-per-window form and a quarter of the serial stump
+// chain per stage — the late groups have few windows and ~100-200 stumps per stage.  Only
+// used for cascades whose stage sums are exact in double in any association (checked at
+// ef_haar_set_cascade), so the decisions equal predictOrderedStump's sequential sum.
+__global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer* __restrict__ L,
+                                                                 const int* __restrict__ ii1,
+                                                                 const unsigned* __restrict__ ii2,
+                                                                 const HaarStage* __restrict__ stages, int s0, int s1,
+                                                                 const HaarStump* __restrict__ stumps,
+                                                                 const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                                 const HaarCand* __restrict__ in,
+                                                                 const int* __restrict__ nin, int cap,
+                                                                 HaarCand* __restrict__ out, int* __restrict__ nout) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int n = min(*nin, cap);
+  const int i = blockIdx.x * 64 + lane;
+  if (blockIdx.x * 64 >= n) return;  // uniform over the workgroup
+  const bool valid = i < n;
+  const HaarCand w = in[valid ? i : blockIdx.x * 64];
+  const HaarLayer ly = L[w.layer];
+  const int64_t W1 = ly.w + 1;
+  const int* a1 = ii1 + ly.ii_off;
+  const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
+  bool alive = valid;
+  for (int st = s0; st < s1; ++st) {
+    const HaarStage sg = stages[st];
+    const int a = q * sg.count / 4, b = (q + 1) * sg.count / 4;
+    double tmp = 0.0;
+    if (alive) {
+      for (int t = a; t < b; ++t) {
+        const HaarStump sp = stumps[sg.first + t];
+        const HaarFeat& f = feats[sp.feat];
+        float val = __fmul_rn(f.wt[0], (float)box(a1, W1, w.x + f.x[0], w.y + f.y[0], f.w[0], f.h[0]));
+        val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(a1, W1, w.x + f.x[1], w.y + f.y[1], f.w[1], f.h[1])));
+        if (f.wt[2] != 0.f)
+          val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(a1, W1, w.x + f.x[2], w.y + f.y[2], f.w[2], f.h[2])));
+        val = __fmul_rn(val, vnf);
+        tmp = __dadd_rn(tmp, (double)(val < sp.thr ? sp.left : sp.right));
+      }
+    }
+    part[q][lane] = tmp;
+    __syncthreads();
+    if (alive) {
+      const double tot = __dadd_rn(__dadd_rn(__dadd_rn(part[0][lane], part[1][lane]), part[2][lane]), part[3][lane]);
+      alive = !(tot < (double)sg.thr);
+    }
+    if (!__syncthreads_or(alive)) return;  // every window of the workgroup rejected
+  }
+  if (alive && q == 0) {
+    const int k = atomicAdd(nout, 1);
+    if (k < cap) out[k] = w;
+  }
+}
+
 // ------------------------------------------------------------------ host side
 struct HaarState {
   int ww = 0, wh = 0, nstages = 0;
+  bool order_free = false;  // every stage sum is exact in double in any order (see set_cascade)
   DevBuf feats, stumps, stages;
   DevBuf pix, ii1, ii2, res, layers, rowstart, work, cand, counters, frame, desc;
 };
@@ -475,6 +534,27 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
       return set_err(c, EF_E_INVALID, "ef_haar_set_cascade: stump feature index out of range");
     sp[i] = HaarStump{stump_feature[i], stump_threshold[i], stump_left[i], stump_right[i]};
   }
+  // Can a stage's sum of leaf values (floats, accumulated in double) be formed in any
+  // association?  Every value is a multiple of the smallest nonzero leaf's ulp u, so every
+  // partial sum is too; if the sum of |leaf| maxima stays <= 2^53 u, every partial sum is
+  // an exactly representable double and the order does not matter.
+  bool order_free = true;
+  for (int s = 0; s < n_stages && order_free; ++s) {
+    double u = 0.0, bound = 0.0;
+    for (int t = st[s].first; t < st[s].first + st[s].count; ++t) {
+      const float lv[2] = {sp[t].left, sp[t].right};
+      for (float v : lv) {
+        if (!std::isfinite(v)) order_free = false;
+        if (v == 0.f) continue;
+        int e = 0;
+        (void)std::frexp((double)v, &e);  // |v| in [2^(e-1), 2^e): float ulp 2^(e-24)
+        const double ul = std::ldexp(1.0, e - 24);
+        u = u == 0.0 ? ul : std::min(u, ul);
+      }
+      bound += std::max(std::fabs((double)sp[t].left), std::fabs((double)sp[t].right));
+    }
+    if (u > 0.0 && bound > std::ldexp(u, 53)) order_free = false;
+  }
   EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
   haar_release(c);
   HaarState* h = new HaarState();
@@ -482,6 +562,7 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
   h->ww = win_w;
   h->wh = win_h;
   h->nstages = n_stages;
+  h->order_free = order_free && !getenv("EF_HAAR_ORDERED");
   EF_TRY(ensure(c, h->feats, f.size() * sizeof(HaarFeat)));
   EF_TRY(ensure(c, h->stumps, sp.size() * sizeof(HaarStump)));
   EF_TRY(ensure(c, h->stages, st.size() * sizeof(HaarStage)));
@@ -605,13 +686,20 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   if (hc[0] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: work-list capacity exceeded");
   // stage groups; the lists ping-pong between work and cand, counters cnt[g]
   const int groups[] = {1, 3, 6, 10, 15, 1 << 30};
+  // groups from stage 6 on (few windows, long stages) take the split form when the
+  // cascade's stage sums are order-free; the early groups keep thread-per-window (measured:
+  // 640x480 synthetic frontal cascade, groups 3-5: 630 -> 585 us, groups 1-2 faster as threads)
+  constexpr int kHaarSplitFrom = 6;
   int gi = 0;
   const int live = hc[0];  // upper bound of every group's input
   HaarCand* bin = work;
   HaarCand* bout = cand;
   for (; groups[gi] < h->nstages; ++gi) {
     const int s0 = groups[gi], s1 = std::min(groups[gi + 1], h->nstages);
-    if (live > 0)
+    if (live > 0 && h->order_free && s0 >= kHaarSplitFrom)
+      hipLaunchKernelGGL(haar_cascade_split_kernel, dim3((unsigned)((live + 63) / 64)), dim3(256), 0, s, dl, ii1, ii2,
+                         dst, s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+    else if (live > 0)
       hipLaunchKernelGGL(haar_cascade_kernel, dim3((unsigned)((live + 255) / 256)), dim3(256), 0, s, dl, ii1, ii2, dst,
                          s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
     std::swap(bin, bout);
