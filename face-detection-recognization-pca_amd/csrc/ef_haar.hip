@@ -61,6 +61,16 @@ struct HaarStump {
   int feat;
   float thr, left, right;
 };
+// One stump with its feature inlined (stump order): what the split cascade kernel stages
+// into LDS per stage, so a stump costs no dependent scalar loads of the stump and feature
+// tables (those miss the scalar cache: the tables are ~180 KB for a frontal-face cascade).
+struct HaarRec {
+  float thr, left, right;
+  int nr;
+  int x[3], y[3], w[3], h[3];
+  float wt[3];
+  int pad;
+};
 struct HaarStage {
   int first, count;
   float thr;
@@ -338,12 +348,12 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
 // chain per stage — the late groups have few windows and ~100-200 stumps per stage.  Only
 // used for cascades whose stage sums are exact in double in any association (checked at
 // ef_haar_set_cascade), so the decisions equal predictOrderedStump's sequential sum.
+constexpr int kHaarRecChunk = 256;
 __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer* __restrict__ L,
                                                                  const int* __restrict__ ii1,
                                                                  const unsigned* __restrict__ ii2,
                                                                  const HaarStage* __restrict__ stages, int s0, int s1,
-                                                                 const HaarStump* __restrict__ stumps,
-                                                                 const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                                 const HaarRec* __restrict__ recs, int ww, int wh,
                                                                  const HaarCand* __restrict__ in,
                                                                  const int* __restrict__ nin, int cap,
                                                                  HaarCand* __restrict__ out, int* __restrict__ nout) {
@@ -359,21 +369,30 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
   const int* a1 = ii1 + ly.ii_off;
   const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
   bool alive = valid;
+  __shared__ HaarRec srec[kHaarRecChunk];
   for (int st = s0; st < s1; ++st) {
     const HaarStage sg = stages[st];
-    const int a = q * sg.count / 4, b = (q + 1) * sg.count / 4;
     double tmp = 0.0;
-    if (alive) {
-      for (int t = a; t < b; ++t) {
-        const HaarStump sp = stumps[sg.first + t];
-        const HaarFeat& f = feats[sp.feat];
-        float val = __fmul_rn(f.wt[0], (float)box(a1, W1, w.x + f.x[0], w.y + f.y[0], f.w[0], f.h[0]));
-        val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(a1, W1, w.x + f.x[1], w.y + f.y[1], f.w[1], f.h[1])));
-        if (f.wt[2] != 0.f)
-          val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(a1, W1, w.x + f.x[2], w.y + f.y[2], f.w[2], f.h[2])));
-        val = __fmul_rn(val, vnf);
-        tmp = __dadd_rn(tmp, (double)(val < sp.thr ? sp.left : sp.right));
+    for (int c0 = 0; c0 < sg.count; c0 += kHaarRecChunk) {
+      const int cn = min(kHaarRecChunk, sg.count - c0);
+      {  // stage the chunk's records (dword-wise, coalesced)
+        const int* src = reinterpret_cast<const int*>(recs + sg.first + c0);
+        int* dst = reinterpret_cast<int*>(srec);
+        for (int e = threadIdx.x; e < cn * (int)(sizeof(HaarRec) / 4); e += 256) dst[e] = src[e];
       }
+      __syncthreads();
+      if (alive) {
+        for (int t = q; t < cn; t += 4) {  // wave q: every 4th stump (the sum is order-free)
+          const HaarRec& f = srec[t];
+          float val = __fmul_rn(f.wt[0], (float)box(a1, W1, w.x + f.x[0], w.y + f.y[0], f.w[0], f.h[0]));
+          val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(a1, W1, w.x + f.x[1], w.y + f.y[1], f.w[1], f.h[1])));
+          if (f.wt[2] != 0.f)
+            val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(a1, W1, w.x + f.x[2], w.y + f.y[2], f.w[2], f.h[2])));
+          val = __fmul_rn(val, vnf);
+          tmp = __dadd_rn(tmp, (double)(val < f.thr ? f.left : f.right));
+        }
+      }
+      __syncthreads();  // the chunk is consumed before the next one is staged
     }
     part[q][lane] = tmp;
     __syncthreads();
@@ -393,14 +412,14 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
 struct HaarState {
   int ww = 0, wh = 0, nstages = 0;
   bool order_free = false;  // every stage sum is exact in double in any order (see set_cascade)
-  DevBuf feats, stumps, stages;
+  DevBuf feats, stumps, stages, recs;
   DevBuf pix, ii1, ii2, res, layers, rowstart, work, cand, counters, frame, desc;
 };
 
 void haar_release(ef_ctx* c) {
   if (!c || !c->haar) return;
   HaarState* h = static_cast<HaarState*>(c->haar);
-  DevBuf* bufs[] = {&h->feats, &h->stumps, &h->stages, &h->pix, &h->ii1,      &h->ii2,     &h->res,
+  DevBuf* bufs[] = {&h->feats, &h->stumps, &h->stages, &h->recs, &h->pix, &h->ii1,      &h->ii2,     &h->res,
                     &h->layers, &h->rowstart, &h->work, &h->cand, &h->counters, &h->frame, &h->desc};
   for (DevBuf* b : bufs) release(*b);
   delete h;
@@ -569,6 +588,15 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
   EF_HIP(c, hipMemcpy(h->feats.p, f.data(), f.size() * sizeof(HaarFeat), hipMemcpyHostToDevice), "H2D features");
   EF_HIP(c, hipMemcpy(h->stumps.p, sp.data(), sp.size() * sizeof(HaarStump), hipMemcpyHostToDevice), "H2D stumps");
   EF_HIP(c, hipMemcpy(h->stages.p, st.data(), st.size() * sizeof(HaarStage), hipMemcpyHostToDevice), "H2D stages");
+  std::vector<HaarRec> rc((size_t)n_stumps);
+  for (int i = 0; i < n_stumps; ++i) {
+    const HaarFeat& q = f[sp[i].feat];
+    HaarRec& r = rc[i];
+    r.thr = sp[i].thr, r.left = sp[i].left, r.right = sp[i].right, r.nr = q.nr, r.pad = 0;
+    for (int k = 0; k < 3; ++k) r.x[k] = q.x[k], r.y[k] = q.y[k], r.w[k] = q.w[k], r.h[k] = q.h[k], r.wt[k] = q.wt[k];
+  }
+  EF_TRY(ensure(c, h->recs, rc.size() * sizeof(HaarRec)));
+  EF_HIP(c, hipMemcpy(h->recs.p, rc.data(), rc.size() * sizeof(HaarRec), hipMemcpyHostToDevice), "H2D records");
   return EF_OK;
 }
 
@@ -698,7 +726,8 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
     const int s0 = groups[gi], s1 = std::min(groups[gi + 1], h->nstages);
     if (live > 0 && h->order_free && s0 >= kHaarSplitFrom)
       hipLaunchKernelGGL(haar_cascade_split_kernel, dim3((unsigned)((live + 63) / 64)), dim3(256), 0, s, dl, ii1, ii2,
-                         dst, s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+                         dst, s0, s1, static_cast<const HaarRec*>(h->recs.p), h->ww, h->wh, bin, cnt + gi, cap, bout,
+                         cnt + gi + 1);
     else if (live > 0)
       hipLaunchKernelGGL(haar_cascade_kernel, dim3((unsigned)((live + 255) / 256)), dim3(256), 0, s, dl, ii1, ii2, dst,
                          s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
