@@ -343,8 +343,8 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
 
 // Pass 3, split form: a workgroup of 4 waves takes 64 windows (lane = window, as above, so
 // each stump's integral-image gathers stay coalesced over neighbouring windows) and wave q
-// evaluates the q-th quarter of every stage's stumps; the four partial sums are combined
-// in LDS.  4x the waves of the thread-per-window form and a quarter of the serial stump
+// evaluates stumps q, q+4, q+8, ... of every stage, read from LDS records (stump + its
+// feature inlined, staged 256 at a time); the four partial sums are combined in LDS.  4x the waves of the thread-per-window form and a quarter of the serial stump
 // chain per stage — the late groups have few windows and ~100-200 stumps per stage.  Only
 // used for cascades whose stage sums are exact in double in any association (checked at
 // ef_haar_set_cascade), so the decisions equal predictOrderedStump's sequential sum.
