@@ -78,7 +78,7 @@ def pmc_traffic(config):
     """HBM bytes per search launch from the newest committed rocprofv3 PMC summary of
     this config (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")), reverse=True):
         rec = json.load(open(f))
         if rec.get("config") == config:
             return rec["traffic_bytes"], os.path.relpath(f, ROOT)

@@ -46,6 +46,9 @@ struct SearchWs {
 
 struct SearchPlan {
   int n_ptiles = 0, nchunks = 0, tiles_per_chunk = 0;
+  // wide kernel: (chunk, probe tile) pairs are dealt to XCDs in blocks of cblk chunks x
+  // pblk probe tiles, so one XCD's L2 holds pblk probe tiles instead of all of them
+  int pblk = 0, cblk = 1;
 };
 
 // ---- device buffer ------------------------------------------------------------------

@@ -506,6 +506,20 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
   pl.nchunks = (int)(((want + 7) / 8) * 8);
   pl.tiles_per_chunk = (int)((tiles + pl.nchunks - 1) / pl.nchunks);
   if (pl.tiles_per_chunk < 1) pl.tiles_per_chunk = 1;
+  // Wide kernel: the probes stream through LDS with every gallery tile, so an XCD whose
+  // workgroups span all probe tiles re-fetches them from beyond its L2 (32 tiles x 256 KiB
+  // at C5 = 8 MiB > 4 MiB L2: 27x the gallery bytes measured).  Deal blocks of 8 probe
+  // tiles x cblk chunks to each XCD instead: 2 MiB of probes stay L2-resident and each
+  // chunk is read by n_ptiles / 8 XCDs.
+  pl.pblk = pl.n_ptiles;
+  pl.cblk = 1;
+  if (wide && pl.n_ptiles % 8 == 0 && pl.n_ptiles > 8) {
+    const int64_t per_xcd = (int64_t)pl.nchunks * pl.n_ptiles / 8;
+    if (per_xcd % 8 == 0 && pl.nchunks % (per_xcd / 8) == 0) {
+      pl.pblk = 8;
+      pl.cblk = (int)(per_xcd / 8);
+    }
+  }
   return pl;
 }
 

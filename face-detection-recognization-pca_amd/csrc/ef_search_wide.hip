@@ -21,6 +21,15 @@
 
 namespace ef {
 
+// Diagnostic builds only (timing, wrong results): EF_WIDE_ABL 1 = no per-slice barrier,
+// 2 = no arg-best epilogue, 3 = no DMA after the first slices.
+#ifndef EF_WIDE_ABL
+#define EF_WIDE_ABL 0
+#endif
+#ifndef EF_WIDE_INTERLEAVE
+#define EF_WIDE_INTERLEAVE 0
+#endif
+
 constexpr int WR = kWideRowTile;    // gallery rows per tile
 constexpr int WP = kWideProbeTile;  // probes per workgroup
 constexpr int WBK = 32;             // k per slice
@@ -30,7 +39,7 @@ static_assert(WR == 128 && WP == 128, "4 waves x 32 probes, 4 x 32-row blocks");
 template <int KP, int METRIC, bool COLLECT>
 __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
-    int n_ptiles, int tiles_per_chunk, int64_t bpad, SearchWs ws) {
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
   constexpr int NS = KP / WBK;  // slices per tile
   // [stage 0: gallery | probes][stage 1: gallery | probes][aux of even | odd tiles]
   // (aux is double-buffered by tile: the cosine epilogue reads it in the tile's last
@@ -39,8 +48,12 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
 
   const int total = gridDim.x;  // host guarantees total % 8 == 0
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  const int gc = lin / n_ptiles;
-  const int pt = lin - gc * n_ptiles;
+  // (chunk, probe tile) blocks of cblk x pblk, one block per XCD (see search_plan)
+  const int bsz = cblk * pblk;
+  const int blk = lin / bsz, r = lin - blk * bsz;
+  const int nbp = n_ptiles / pblk;
+  const int gc = (blk / nbp) * cblk + r / pblk;
+  const int pt = (blk % nbp) * pblk + r % pblk;
 
   int n_amb = 0;
   if constexpr (COLLECT) {
@@ -73,54 +86,59 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
   // 4w..4w+3 of the gallery slice and of the probe slice.  Lane l of piece j carries
   // row 8j + (l >> 3), physical 16-B chunk l & 7, which holds logical chunk
   // (l & 7) ^ ((row >> 1) & 7) = (l & 7) ^ ((4 * jj + (l >> 4)) & 7).
+  // Per-lane byte offsets are fixed for the whole sweep (SGPR-base DMA: the slice's base
+  // address is wave-uniform), so a slice's 8 DMAs cost no per-lane address arithmetic.
   const int prow = lane >> 3;
-  int qsrc[4];  // probe row of each of this lane's probe pieces
+  unsigned goff[4], qoff[4];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
     const int slot = pt * WP + (wave * 4 + jj) * 8 + prow;
-    if constexpr (COLLECT) {
-      qsrc[jj] = slot < n_amb ? ws.amb_list[slot] : 0;
-    } else {
-      qsrc[jj] = slot;
-    }
+    int qrow = slot;
+    if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
+    const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 7)) * 16);
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
   }
+  const unsigned aoff = (unsigned)lane * 4;
   float thr = -__builtin_inff();
   if constexpr (COLLECT) {
     if (s0 < n_amb) thr = ws.thr[s0];
   }
   // settle these loads before the loop (a loop-merged wait would drain the LDS-DMA)
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qsrc[jj]));
+  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qoff[jj]));
   asm volatile("" ::"v"(thr));
 
   const unsigned lds_base = lds_addr(smem);
   const int64_t n_it = (t1 - t0) * NS;
-  auto issue = [&](int64_t it, int buf) {
+  // DMA of slice it into buffer buf, piece jj of this wave's four (+ the tile's aux).
+  auto issue_piece = [&](int64_t it, int buf, int jj) {
     const int64_t t = t0 + it / NS;
     const int sl = (int)(it % NS);
     const int nrem = (int)((n - t * WR) < WR ? (n - t * WR) : WR);
-    int ln = lane;
-    asm volatile("" : "+v"(ln));  // recompute the per-lane offsets each slice (no hoisting)
-    const int pr = ln >> 3, pc = ln & 7;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int j = wave * 4 + jj;
-      const int lchunk = pc ^ ((4 * jj + (ln >> 4)) & 7);
-      int row = j * 8 + pr;
-      if (nrem < WR) row = row < nrem ? row : nrem - 1;
-      glds16(G + (t * WR + row) * KP + sl * WBK + lchunk * 4,
-             lds_base + (unsigned)((buf * 2 * WSL + j * 256) * 4));
-      glds16(qpad + (int64_t)qsrc[jj] * KP + sl * WBK + lchunk * 4,
-             lds_base + (unsigned)((buf * 2 * WSL + WSL + j * 256) * 4));
+    const unsigned long long gb = (unsigned long long)(size_t)(G + t * WR * KP + sl * WBK);
+    const unsigned long long qb = (unsigned long long)(size_t)(qpad + sl * WBK);
+    const int j = wave * 4 + jj;
+    unsigned go = goff[jj];
+    if (nrem < WR) {  // tail tile: rows past the end re-read the last row (masked later)
+      const unsigned row = go / (KP * 4);
+      go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
     }
-    if (sl == 0 && wave == 0) {  // the tile's ||g||^2 (L2) or 1/||g|| (cosine)
+    glds16s(go, gb, lds_base + (unsigned)((buf * 2 * WSL + j * 256) * 4));
+    glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * WSL + WSL + j * 256) * 4));
+    if (jj == 3 && sl == 0 && wave == 0) {  // the tile's ||g||^2 (L2) or 1/||g|| (cosine)
+      const unsigned long long ab = (unsigned long long)(size_t)(aux + t * WR);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int r = 64 * q + ln;
-        const int rr = r < nrem ? r : nrem - 1;
-        glds4(aux + t * WR + rr, lds_base + (unsigned)((4 * WSL + ((t - t0) & 1) * WR + 64 * q) * 4));
+        const int rr = 64 * q + lane;
+        const unsigned ao = rr < nrem ? aoff + 256u * q : (unsigned)(nrem - 1) * 4;
+        glds4s(ao, ab, lds_base + (unsigned)((4 * WSL + ((t - t0) & 1) * WR + 64 * q) * 4));
       }
     }
+  };
+  auto issue = [&](int64_t it, int buf) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) issue_piece(it, buf, jj);
   };
 
   const float INF = __builtin_inff();
@@ -162,7 +180,14 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     const int buf = (int)(it & 1);
     const int sl = (int)(it % NS);
     const float* const sAux = smem + 4 * WSL + (int)((it / NS) & 1) * WR;
-    if (it + 1 < n_it) issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+#if EF_WIDE_INTERLEAVE == 0
+#if EF_WIDE_ABL == 3
+    if (it + 1 < 2)
+#else
+    if (it + 1 < n_it)
+#endif
+      issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+#endif
     if (sl == 0) {
       // L2: start from -||g||^2 / 2 and accumulate q.g, so that -2 acc = ||g||^2 - 2 q.g
       // with the rounding of the chain scaled exactly by -2.  Cosine: start from 0.
@@ -198,6 +223,11 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
       for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].z, bq.z, acc[rb], 0, 0, 0);
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].w, bq.w, acc[rb], 0, 0, 0);
+#if EF_WIDE_INTERLEAVE
+      // one DMA piece pair of slice it+1 per 16 MFMAs (buffer buf^1 was released by the
+      // previous slice's barrier)
+      if (it + 1 < n_it) issue_piece(it + 1, buf ^ 1, j);
+#endif
     }
     if (sl == NS - 1) {
       const int64_t t = t0 + it / NS;
@@ -223,11 +253,18 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
           for (int r = 0; r < 16; ++r)
             if (tbase + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h >= n) acc[rb][r] = INF;
         }
+#if EF_WIDE_ABL == 2
+        b1 = fminf(b1, acc[rb][0]);
+        (void)tbase;
+#else
         consume(acc[rb], tbase + rb * 32);  // blocks in row order (tie rule)
+#endif
       }
     }
+#if EF_WIDE_ABL != 1
     dma_wait_all();
     __syncthreads();  // slice it+1 landed; everyone is done reading buffer buf
+#endif
   }
 
   if constexpr (!COLLECT) {
@@ -250,12 +287,15 @@ template <int KP, int M>
 static hipError_t wide_t(hipStream_t s, bool collect, const SearchPlan& pl, const float* qpad, const float* G,
                          const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
+  if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
+      (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0)
+    return hipErrorInvalidValue;  // the block deal would not be a bijection
   if (collect)
     hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, bpad, ws);
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
   else
     hipLaunchKernelGGL((search_wide_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, bpad, ws);
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
   return hipGetLastError();
 }
 

@@ -15,6 +15,11 @@ import sys
 from collections import defaultdict
 
 KERNEL = "search_kernel<128, 0, false, 0>"
+# per config: (kernel name fragment, algorithmic bytes per launch = 4kN + 4N + 4kB)
+CONFIGS = {
+    "c3": ("search_kernel<128, 0, false, 0>", 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4),
+    "c5": ("search_wide_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
+}
 SIMDS = 1024  # 256 CUs x 4
 XCDS = 8
 
@@ -37,23 +42,24 @@ def avg_ns(stats_path, kernel=KERNEL):
 def main():
     fetch, write, sq, stats, out = sys.argv[1:6]
     config = sys.argv[6] if len(sys.argv) > 6 else "c3"
-    f, nf = per_launch(fetch)
-    w, _ = per_launch(write)
-    s, _ = per_launch(sq)
-    ns, calls = avg_ns(stats)
+    kernel, alg = CONFIGS[config]
+    f, nf = per_launch(fetch, kernel)
+    w, _ = per_launch(write, kernel)
+    s, _ = per_launch(sq, kernel)
+    ns, calls = avg_ns(stats, kernel)
     fetch_b = f["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE counts half of wide reads
     write_b = w["WRITE_SIZE"] * 1024
     grbm_xcd = s["GRBM_GUI_ACTIVE"] / XCDS
     rec = {
         "config": config,
-        "kernel": KERNEL,
+        "kernel": kernel,
         "launches_profiled": nf.get("FETCH_SIZE", 0),
         "fetch_size_kib_raw": f["FETCH_SIZE"],
         "write_size_kib_raw": w["WRITE_SIZE"],
         "hbm_read_bytes": fetch_b,
         "hbm_write_bytes": write_b,
         "traffic_bytes": fetch_b + write_b,
-        "algorithmic_bytes": 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4,
+        "algorithmic_bytes": alg,
         "trace_avg_ns": ns,
         "trace_calls": calls,
         "mfma_busy_frac": s["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * grbm_xcd),
