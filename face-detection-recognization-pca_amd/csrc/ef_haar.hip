@@ -198,18 +198,16 @@ __device__ __forceinline__ float haar_norm(const int* ii1, const unsigned* ii2, 
 
 // One stage (predictOrderedStump's inner loop): true when the window passes it.
 __device__ __forceinline__ bool haar_stage(const int* ii1, int64_t W1, int x, int y, float vnf,
-                                           const HaarStage& st, const HaarStump* __restrict__ stumps,
-                                           const HaarFeat* __restrict__ feats) {
+                                           const HaarStage& st, const HaarRec* __restrict__ recs) {
   double tmp = 0.0;
   for (int i = 0; i < st.count; ++i) {
-    const HaarStump sp = stumps[st.first + i];
-    const HaarFeat& f = feats[sp.feat];
+    const HaarRec f = recs[st.first + i];  // stump + feature in one (wave-uniform) record
     float val = __fmul_rn(f.wt[0], (float)box(ii1, W1, x + f.x[0], y + f.y[0], f.w[0], f.h[0]));
     val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(ii1, W1, x + f.x[1], y + f.y[1], f.w[1], f.h[1])));
     if (f.wt[2] != 0.f)
       val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(ii1, W1, x + f.x[2], y + f.y[2], f.w[2], f.h[2])));
     val = __fmul_rn(val, vnf);
-    tmp = __dadd_rn(tmp, (double)(val < sp.thr ? sp.left : sp.right));
+    tmp = __dadd_rn(tmp, (double)(val < f.thr ? f.left : f.right));
   }
   return !(tmp < (double)st.thr);
 }
@@ -220,8 +218,7 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
                                                           const int* __restrict__ ii1,
                                                           const unsigned* __restrict__ ii2,
                                                           const HaarStage* __restrict__ stages,
-                                                          const HaarStump* __restrict__ stumps,
-                                                          const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                          const HaarRec* __restrict__ recs, int ww, int wh,
                                                           signed char* __restrict__ res) {
   const HaarLayer ly = L[blockIdx.y];
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -231,7 +228,7 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
   const int* a1 = ii1 + ly.ii_off;
   const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, x, y, ww, wh);
   signed char r = -1;
-  if (vnf != 0.f) r = haar_stage(a1, W1, x, y, vnf, stages[0], stumps, feats) ? 1 : 0;
+  if (vnf != 0.f) r = haar_stage(a1, W1, x, y, vnf, stages[0], recs) ? 1 : 0;
   res[ly.res_off + p] = r;
 }
 
@@ -323,8 +320,7 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
                                                            const int* __restrict__ ii1,
                                                            const unsigned* __restrict__ ii2,
                                                            const HaarStage* __restrict__ stages, int s0, int s1,
-                                                           const HaarStump* __restrict__ stumps,
-                                                           const HaarFeat* __restrict__ feats, int ww, int wh,
+                                                           const HaarRec* __restrict__ recs, int ww, int wh,
                                                            const HaarCand* __restrict__ in, const int* __restrict__ nin,
                                                            int cap, HaarCand* __restrict__ out, int* __restrict__ nout) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -336,7 +332,7 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
   const int* a1 = ii1 + ly.ii_off;
   const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
   for (int s = s0; s < s1; ++s)
-    if (!haar_stage(a1, W1, w.x, w.y, vnf, stages[s], stumps, feats)) return;
+    if (!haar_stage(a1, W1, w.x, w.y, vnf, stages[s], recs)) return;
   const int k = atomicAdd(nout, 1);
   if (k < cap) out[k] = w;
 }
@@ -348,8 +344,12 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
 // chain per stage — the late groups have few windows and ~100-200 stumps per stage.  Only
 // used for cascades whose stage sums are exact in double in any association (checked at
 // ef_haar_set_cascade), so the decisions equal predictOrderedStump's sequential sum.
+// NQ waves per workgroup (4, 8 or 16): the late groups hold a few thousand windows, so
+// the kernel is bound by the latency of each wave's serial stump chain — more waves per
+// window block and 4 stumps' gathers in flight per wave (unrolled) shorten it.
 constexpr int kHaarRecChunk = 256;
-__global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer* __restrict__ L,
+template <int NQ>
+__global__ __launch_bounds__(NQ * 64) void haar_cascade_split_kernel(const HaarLayer* __restrict__ L,
                                                                  const int* __restrict__ ii1,
                                                                  const unsigned* __restrict__ ii2,
                                                                  const HaarStage* __restrict__ stages, int s0, int s1,
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
                                                                  const HaarCand* __restrict__ in,
                                                                  const int* __restrict__ nin, int cap,
                                                                  HaarCand* __restrict__ out, int* __restrict__ nout) {
-  __shared__ double part[4][64];
+  __shared__ double part[NQ][64];
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int n = min(*nin, cap);
   const int i = blockIdx.x * 64 + lane;
@@ -378,11 +378,12 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
       {  // stage the chunk's records (dword-wise, coalesced)
         const int* src = reinterpret_cast<const int*>(recs + sg.first + c0);
         int* dst = reinterpret_cast<int*>(srec);
-        for (int e = threadIdx.x; e < cn * (int)(sizeof(HaarRec) / 4); e += 256) dst[e] = src[e];
+        for (int e = threadIdx.x; e < cn * (int)(sizeof(HaarRec) / 4); e += NQ * 64) dst[e] = src[e];
       }
       __syncthreads();
       if (alive) {
-        for (int t = q; t < cn; t += 4) {  // wave q: every 4th stump (the sum is order-free)
+#pragma unroll 4
+        for (int t = q; t < cn; t += NQ) {  // wave q: every NQ-th stump (the sum is order-free)
           const HaarRec& f = srec[t];
           float val = __fmul_rn(f.wt[0], (float)box(a1, W1, w.x + f.x[0], w.y + f.y[0], f.w[0], f.h[0]));
           val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(a1, W1, w.x + f.x[1], w.y + f.y[1], f.w[1], f.h[1])));
@@ -397,7 +398,9 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
     part[q][lane] = tmp;
     __syncthreads();
     if (alive) {
-      const double tot = __dadd_rn(__dadd_rn(__dadd_rn(part[0][lane], part[1][lane]), part[2][lane]), part[3][lane]);
+      double tot = part[0][lane];
+#pragma unroll
+      for (int r = 1; r < NQ; ++r) tot = __dadd_rn(tot, part[r][lane]);
       alive = !(tot < (double)sg.thr);
     }
     if (!__syncthreads_or(alive)) return;  // every window of the workgroup rejected
@@ -412,14 +415,14 @@ __global__ __launch_bounds__(256) void haar_cascade_split_kernel(const HaarLayer
 struct HaarState {
   int ww = 0, wh = 0, nstages = 0;
   bool order_free = false;  // every stage sum is exact in double in any order (see set_cascade)
-  DevBuf feats, stumps, stages, recs;
+  DevBuf stages, recs;
   DevBuf pix, ii1, ii2, res, layers, rowstart, work, cand, counters, frame, desc;
 };
 
 void haar_release(ef_ctx* c) {
   if (!c || !c->haar) return;
   HaarState* h = static_cast<HaarState*>(c->haar);
-  DevBuf* bufs[] = {&h->feats, &h->stumps, &h->stages, &h->recs, &h->pix, &h->ii1,      &h->ii2,     &h->res,
+  DevBuf* bufs[] = {&h->stages, &h->recs, &h->pix, &h->ii1,      &h->ii2,     &h->res,
                     &h->layers, &h->rowstart, &h->work, &h->cand, &h->counters, &h->frame, &h->desc};
   for (DevBuf* b : bufs) release(*b);
   delete h;
@@ -582,11 +585,7 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
   h->wh = win_h;
   h->nstages = n_stages;
   h->order_free = order_free && !getenv("EF_HAAR_ORDERED");
-  EF_TRY(ensure(c, h->feats, f.size() * sizeof(HaarFeat)));
-  EF_TRY(ensure(c, h->stumps, sp.size() * sizeof(HaarStump)));
   EF_TRY(ensure(c, h->stages, st.size() * sizeof(HaarStage)));
-  EF_HIP(c, hipMemcpy(h->feats.p, f.data(), f.size() * sizeof(HaarFeat), hipMemcpyHostToDevice), "H2D features");
-  EF_HIP(c, hipMemcpy(h->stumps.p, sp.data(), sp.size() * sizeof(HaarStump), hipMemcpyHostToDevice), "H2D stumps");
   EF_HIP(c, hipMemcpy(h->stages.p, st.data(), st.size() * sizeof(HaarStage), hipMemcpyHostToDevice), "H2D stages");
   std::vector<HaarRec> rc((size_t)n_stumps);
   for (int i = 0; i < n_stumps; ++i) {
@@ -697,11 +696,10 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   hipLaunchKernelGGL(haar_cols_ii_kernel, dim3((unsigned)((maxw + 1 + 63) / 64), (unsigned)nl), dim3(1024), 0, s, dl,
                      ii1, ii2);
   const HaarStage* dst = static_cast<const HaarStage*>(h->stages.p);
-  const HaarStump* dsp = static_cast<const HaarStump*>(h->stumps.p);
-  const HaarFeat* dft = static_cast<const HaarFeat*>(h->feats.p);
+  const HaarRec* drc = static_cast<const HaarRec*>(h->recs.p);
   signed char* res = static_cast<signed char*>(h->res.p);
   hipLaunchKernelGGL(haar_stage0_kernel, dim3((unsigned)((maxpos + 255) / 256), (unsigned)nl), dim3(256), 0, s, dl, ii1,
-                     ii2, dst, dsp, dft, h->ww, h->wh, res);
+                     ii2, dst, drc, h->ww, h->wh, res);
   int* cnt = static_cast<int*>(h->counters.p);
   HaarCand* work = static_cast<HaarCand*>(h->work.p);
   HaarCand* cand = static_cast<HaarCand*>(h->cand.p);
@@ -718,19 +716,31 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   // cascade's stage sums are order-free; the early groups keep thread-per-window (measured:
   // 640x480 synthetic frontal cascade, groups 3-5: 630 -> 585 us, groups 1-2 faster as threads)
   constexpr int kHaarSplitFrom = 6;
+  static const int split_waves = [] {  // EF_HAAR_SPLITW: waves per split workgroup (experiments)
+    const char* e = getenv("EF_HAAR_SPLITW");
+    const int v = e ? atoi(e) : 8;
+    return v == 4 || v == 16 ? v : 8;
+  }();
   int gi = 0;
   const int live = hc[0];  // upper bound of every group's input
   HaarCand* bin = work;
   HaarCand* bout = cand;
   for (; groups[gi] < h->nstages; ++gi) {
     const int s0 = groups[gi], s1 = std::min(groups[gi + 1], h->nstages);
-    if (live > 0 && h->order_free && s0 >= kHaarSplitFrom)
-      hipLaunchKernelGGL(haar_cascade_split_kernel, dim3((unsigned)((live + 63) / 64)), dim3(256), 0, s, dl, ii1, ii2,
-                         dst, s0, s1, static_cast<const HaarRec*>(h->recs.p), h->ww, h->wh, bin, cnt + gi, cap, bout,
-                         cnt + gi + 1);
-    else if (live > 0)
+    if (live > 0 && h->order_free && s0 >= kHaarSplitFrom) {
+      const dim3 g((unsigned)((live + 63) / 64));
+      if (split_waves == 16)
+        hipLaunchKernelGGL(haar_cascade_split_kernel<16>, g, dim3(1024), 0, s, dl, ii1, ii2, dst, s0, s1, drc, h->ww,
+                           h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+      else if (split_waves == 8)
+        hipLaunchKernelGGL(haar_cascade_split_kernel<8>, g, dim3(512), 0, s, dl, ii1, ii2, dst, s0, s1, drc, h->ww,
+                           h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+      else
+        hipLaunchKernelGGL(haar_cascade_split_kernel<4>, g, dim3(256), 0, s, dl, ii1, ii2, dst, s0, s1, drc, h->ww,
+                           h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+    } else if (live > 0)
       hipLaunchKernelGGL(haar_cascade_kernel, dim3((unsigned)((live + 255) / 256)), dim3(256), 0, s, dl, ii1, ii2, dst,
-                         s0, s1, dsp, dft, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
+                         s0, s1, drc, h->ww, h->wh, bin, cnt + gi, cap, bout, cnt + gi + 1);
     std::swap(bin, bout);
   }
   timer_end(c, &tev);
