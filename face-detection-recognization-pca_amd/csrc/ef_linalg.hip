@@ -377,10 +377,13 @@ __global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int 
         return;
       }
       const double inv = 1.0 / d;
-      const int w = nb - t - 1;  // update the panel's remaining columns
-      for (int e = tid; e < (rows - t - 1) * w; e += nth) {
-        const int i = t + 1 + e / w, l = t + 1 + e % w;
-        if (l <= i) P[i * kCholPS + l] -= P[i * kCholPS + t] * (P[l * kCholPS + t] * inv);
+      // update the panel's remaining columns: 32 lanes per row (column l = lane), 32 rows
+      // per pass — no per-element index division
+      const int l = tid & 31;
+      if (l > t && l < nb) {
+        const double plt = P[l * kCholPS + t] * inv;
+        for (int i = t + 1 + (tid >> 5); i < rows; i += nth >> 5)
+          if (l <= i) P[i * kCholPS + l] -= P[i * kCholPS + t] * plt;
       }
       __syncthreads();
     }
@@ -395,17 +398,38 @@ __global__ __launch_bounds__(1024) void chol_kernel(double* __restrict__ A, int 
       const int i = e / kCholNB, t = e % kCholNB;
       if (t < nb && t <= i) A[(int64_t)(jb + i) * lda + jb + t] = P[i * kCholPS + t];
     }
-    // trailing lower triangle: A[i][l] -= P[i] . P[l]  (jb + nb <= l <= i)
+    // trailing lower triangle: A[i][l] -= P[i] . P[l]  (jb + nb <= l <= i), 4 x 4 output
+    // blocks per thread (8 LDS reads per t for 16 dot products; each dot product still
+    // accumulates t = 0..31 in order, so the result is unchanged)
     const int w = rows - nb;
-    for (int e = tid; e < w * w; e += nth) {
-      const int i = e / w, l = e % w;
-      if (l > i) continue;
-      const double* pi = P + (nb + i) * kCholPS;
-      const double* pl = P + (nb + l) * kCholPS;
-      double acc = 0.0;
-#pragma unroll 8
-      for (int t = 0; t < kCholNB; ++t) acc = fma(pi[t], pl[t], acc);
-      A[(int64_t)(jb + nb + i) * lda + jb + nb + l] -= acc;
+    const int nbw = (w + 3) >> 2;
+    for (int e = tid; e < nbw * nbw; e += nth) {
+      const int bi = e / nbw, bj = e - bi * nbw;
+      if (bj > bi) continue;
+      double acc[4][4] = {};
+      const double* pi = P + (nb + 4 * bi) * kCholPS;
+      const double* pl = P + (nb + 4 * bj) * kCholPS;
+      const int ri = min(4, w - 4 * bi), rl = min(4, w - 4 * bj);
+#pragma unroll 4
+      for (int t = 0; t < kCholNB; ++t) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u] = u < ri ? pi[u * kCholPS + t] : 0.0;
+          b[u] = u < rl ? pl[u * kCholPS + t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = 4 * bi + u, l = 4 * bj + v;
+          if (u < ri && v < rl && l <= i) A[(int64_t)(jb + nb + i) * lda + jb + nb + l] -= acc[u][v];
+        }
     }
     __syncthreads();
   }
