@@ -715,7 +715,10 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   // groups from stage 6 on (few windows, long stages) take the split form when the
   // cascade's stage sums are order-free; the early groups keep thread-per-window (measured:
   // 640x480 synthetic frontal cascade, groups 3-5: 630 -> 585 us, groups 1-2 faster as threads)
-  constexpr int kHaarSplitFrom = 6;
+  static const int kHaarSplitFrom = [] {  // first stage group run in split form (EF_HAAR_SPLIT_FROM: experiments)
+    const char* e = getenv("EF_HAAR_SPLIT_FROM");
+    return e ? atoi(e) : 6;
+  }();
   static const int split_waves = [] {  // EF_HAAR_SPLITW: waves per split workgroup (experiments)
     const char* e = getenv("EF_HAAR_SPLITW");
     const int v = e ? atoi(e) : 8;
