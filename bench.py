@@ -492,7 +492,8 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "search_kernel (fp32 MFMA distance GEMM + fused arg-best)",
+                "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
+                + " (fp32 MFMA distance GEMM + fused arg-best)",
                 "achieved": round(achieved, 2),
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",

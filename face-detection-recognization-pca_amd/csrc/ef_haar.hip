@@ -712,12 +712,12 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   if (hc[0] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: work-list capacity exceeded");
   // stage groups; the lists ping-pong between work and cand, counters cnt[g]
   const int groups[] = {1, 3, 6, 10, 15, 1 << 30};
-  // groups from stage 6 on (few windows, long stages) take the split form when the
-  // cascade's stage sums are order-free; the early groups keep thread-per-window (measured:
-  // 640x480 synthetic frontal cascade, groups 3-5: 630 -> 585 us, groups 1-2 faster as threads)
+  // every group takes the split form when the cascade's stage sums are order-free
+  // (measured, 640x480 synthetic frontal cascade with LDS stump records and 8 waves: split
+  // from group 1 0.637 ms, from stage 3 0.652, from stage 6 0.673 per frame)
   static const int kHaarSplitFrom = [] {  // first stage group run in split form (EF_HAAR_SPLIT_FROM: experiments)
     const char* e = getenv("EF_HAAR_SPLIT_FROM");
-    return e ? atoi(e) : 6;
+    return e ? atoi(e) : 1;
   }();
   static const int split_waves = [] {  // EF_HAAR_SPLITW: waves per split workgroup (experiments)
     const char* e = getenv("EF_HAAR_SPLITW");
