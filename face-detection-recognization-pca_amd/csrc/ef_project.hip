@@ -50,22 +50,27 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
   if (k_end > d) k_end = d;
   const int nsteps = (int)((k_end - k_beg + BK - 1) / BK);
 
-  // pixel staging: thread -> (row, 16-pixel half)
+  // pixel staging: thread -> (row, 16-pixel half).  load_stage only issues the global
+  // loads (raw pixels, mean, W) into registers; the uint8 -> float conversion and the mean
+  // subtraction happen in store_stage, after the stage's MFMAs, so the loads' latency is
+  // hidden under them instead of being waited for before the first MFMA.
   const int pr = tid >> 1, ph = (tid & 1) * 16;
   float pv[16];
+  float muv[16];
+  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+  bool raw_ok = false;
   float4 wv[W4_PT];
 
   auto load_stage = [&](int step) {
     const int64_t kb = k_beg + (int64_t)step * BK;
     const int64_t row = m0 + pr;
     const int64_t px0 = kb + ph;
+    const bool full = VEC && row < b && px0 + 16 <= k_end;
     if constexpr (PDT == EF_U8) {
       const uint8_t* P = reinterpret_cast<const uint8_t*>(Pv);
-      if (VEC && row < b && px0 + 16 <= k_end) {
-        const uint4 raw = *reinterpret_cast<const uint4*>(P + row * d + px0);
-        const unsigned w4[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) pv[j] = (float)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      raw_ok = full;
+      if (full) {
+        raw = *reinterpret_cast<const uint4*>(P + row * d + px0);
       } else {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
@@ -73,7 +78,7 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
       }
     } else {
       const float* P = reinterpret_cast<const float*>(Pv);
-      if (VEC && row < b && px0 + 16 <= k_end) {
+      if (full) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float4 v = *reinterpret_cast<const float4*>(P + row * d + px0 + 4 * j);
@@ -84,11 +89,16 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
         for (int j = 0; j < 16; ++j) pv[j] = (row < b && px0 + j < k_end) ? P[row * d + px0 + j] : 0.f;
       }
     }
-    // mean subtraction fused into the operand load (K2); padded rows/pixels stay 0
+    // mean of this thread's 16 pixels (0 on padded rows / pixels, which stay 0)
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t px = px0 + j;
-      if (row < b && px < k_end) pv[j] -= mu[px];
+      for (int j = 0; j < 4; ++j) {
+        const float4 m = *reinterpret_cast<const float4*>(mu + px0 + 4 * j);
+        muv[4 * j] = m.x; muv[4 * j + 1] = m.y; muv[4 * j + 2] = m.z; muv[4 * j + 3] = m.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) muv[j] = (row < b && px0 + j < k_end) ? mu[px0 + j] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < W4_PT; ++j) {
@@ -100,6 +110,16 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
     }
   };
   auto store_stage = [&](int buf) {
+    if constexpr (PDT == EF_U8) {
+      if (raw_ok) {
+        const unsigned w4[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pv[j] = (float)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      }
+    }
+    // mean subtraction fused into the operand staging (K2)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pv[j] -= muv[j];
     float* a = &sA[buf][pr * SA + ph];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
