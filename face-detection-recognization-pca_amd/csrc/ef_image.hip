@@ -167,66 +167,66 @@ struct TmStat {
 
 // frame8 = I - 128 (int8) in a zero-padded [rows][pitch] image, and row prefix sums of I'
 // and I'^2 (int64): one wave per integral-image row (row 0 is zero).
+// The integral images are stored as T: int64, or wrapping uint32 when every template area n
+// is < 2^18 — a window sum of I' (|.| <= 128 n < 2^31) and of I'^2 (<= 16384 n < 2^32) is
+// then recovered exactly from the mod-2^32 corner differences, at half the bytes the
+// score kernel's L2-bound corner gathers move.
+template <typename T>
 __global__ __launch_bounds__(256) void tm_rows_kernel(const uint8_t* __restrict__ f, int H, int W, int64_t ld,
                                                       int8_t* __restrict__ f8, int64_t pitch,
-                                                      long long* __restrict__ ii1, long long* __restrict__ ii2) {
+                                                      T* __restrict__ ii1, T* __restrict__ ii2) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row > H) return;
   const int64_t W1 = W + 1;
-  long long* r1 = ii1 + row * W1;
-  long long* r2 = ii2 + row * W1;
+  T* r1 = ii1 + row * W1;
+  T* r2 = ii2 + row * W1;
   if (row == 0) {
     for (int x = lane; x <= W; x += 64) r1[x] = r2[x] = 0;
     return;
   }
   const int y = row - 1;
-  const int per = (W + 63) / 64, xb = lane * per;
-  long long s1 = 0, s2 = 0;
-  for (int i = 0; i < per; ++i) {
-    const int x = xb + i;
+  // 64-pixel chunks, lane = pixel (coalesced loads and stores), an inclusive wave scan per
+  // chunk in int32 (|chunk sum of I'^2| <= 64 * 16384) carried into int64 row totals
+  if (lane == 0) r1[0] = r2[0] = 0;
+  long long c1 = 0, c2 = 0;
+  for (int x0 = 0; x0 < W; x0 += 64) {
+    const int x = x0 + lane;
+    int e1 = 0, e2 = 0;
     if (x < W) {
       const int v = (int)f[(int64_t)y * ld + x] - 128;
       f8[(int64_t)y * pitch + x] = (int8_t)v;
-      s1 += v;
-      s2 += v * v;
+      e1 = v;
+      e2 = v * v;
     }
-  }
-  long long e1 = s1, e2 = s2;  // inclusive scan of the lane totals
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const long long t1 = __shfl_up(e1, off), t2 = __shfl_up(e2, off);
-    if (lane >= off) {
-      e1 += t1;
-      e2 += t2;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t1 = __shfl_up(e1, off), t2 = __shfl_up(e2, off);
+      if (lane >= off) {
+        e1 += t1;
+        e2 += t2;
+      }
     }
-  }
-  e1 -= s1;
-  e2 -= s2;
-  if (lane == 0) r1[0] = r2[0] = 0;
-  for (int i = 0; i < per; ++i) {
-    const int x = xb + i;
     if (x < W) {
-      const long long v = f8[(int64_t)y * pitch + x];
-      e1 += v;
-      e2 += v * v;
-      r1[x + 1] = e1;
-      r2[x + 1] = e2;
+      r1[x + 1] = (T)(c1 + e1);
+      r2[x + 1] = (T)(c2 + e2);
     }
+    c1 += __shfl(e1, 63);
+    c2 += __shfl(e2, 63);
   }
 }
 
 // Column prefix of the row sums: block = 16 columns x 64 row segments (a 641-column frame
 // is 41 workgroups, not 11: the pass is latency-bound, so it wants many short segments).
 constexpr int kColW = 16, kColSeg = 64;
-__global__ __launch_bounds__(1024) void tm_cols_kernel(int H, int W, long long* __restrict__ ii1,
-                                                       long long* __restrict__ ii2) {
-  __shared__ long long t1[kColSeg][kColW], t2[kColSeg][kColW];
+template <typename T>
+__global__ __launch_bounds__(1024) void tm_cols_kernel(int H, int W, T* __restrict__ ii1, T* __restrict__ ii2) {
+  __shared__ T t1[kColSeg][kColW], t2[kColSeg][kColW];
   const int cx = threadIdx.x % kColW, sg = threadIdx.x / kColW;
   const int x = blockIdx.x * kColW + cx;
   const int64_t W1 = W + 1;
   const int per = (H + kColSeg - 1) / kColSeg;
   const int ya = 1 + sg * per, yb = ya + per < H + 1 ? ya + per : H + 1;
-  long long s1 = 0, s2 = 0;
+  T s1 = 0, s2 = 0;
   if (x <= W) {
 #pragma unroll 4
     for (int y = ya; y < yb; ++y) {
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(1024) void tm_cols_kernel(int H, int W, long long* 
   t1[sg][cx] = s1;
   t2[sg][cx] = s2;
   __syncthreads();
-  long long o1 = 0, o2 = 0;
+  T o1 = 0, o2 = 0;
   for (int q = 0; q < sg; ++q) {
     o1 += t1[q][cx];
     o2 += t2[q][cx];
@@ -517,10 +517,10 @@ __device__ __forceinline__ unsigned long long tm_key(float v, unsigned idx) {
 
 // grid (blocks per problem, nprob): score every position (grid-stride), optional map,
 // then one packed-key atomicMin per block for the first raster-order maximum.
+template <typename T>
 __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restrict__ probs,
                                                        const TmStat* __restrict__ st, const int* __restrict__ parts,
-                                                       const long long* __restrict__ ii1,
-                                                       const long long* __restrict__ ii2, int W,
+                                                       const T* __restrict__ ii1, const T* __restrict__ ii2, int W,
                                                        float* __restrict__ maps,
                                                        unsigned long long* __restrict__ keys) {
   const TmProblem pb = probs[blockIdx.y];
@@ -532,20 +532,40 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
   unsigned long long key = ~0ull;
   // rows are strided over the blocks of this problem, columns over the threads (no 64-bit
   // index division per position)
+  // two positions (x, x + 256) per thread per pass: both positions' loads are in flight
+  // before either's fp64 normalisation (the kernel is load-latency bound)
   for (int y = blockIdx.x; y < pb.hr; y += gridDim.x) {
     const int64_t a0 = (int64_t)y * W1, b0 = (int64_t)(y + pb.th) * W1;
-    for (int x = threadIdx.x; x < pb.wr; x += 256) {
-      const int64_t i = (int64_t)y * pb.wr + x;
-      long long P = 0;
-      const int* pp = parts + pb.part_off + i;
-      for (int q = 0; q < pb.nparts; ++q) P += pp[(int64_t)q * npos];
-      const int64_t a = a0 + x, b = b0 + x;
-      const long long sI = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
-      const long long sI2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
-      const float v = tm_score(n * P - ts.sT * sI, n * sI2 - sI * sI, ts.varT, sqT);
-      if (maps) maps[pb.map_off + i] = v;
-      const unsigned long long k = tm_key(v, (unsigned)i);
-      key = k < key ? k : key;
+    const int64_t row = (int64_t)y * pb.wr;
+    for (int x = threadIdx.x; x < pb.wr; x += 512) {
+      const bool two = x + 256 < pb.wr;
+      long long P[2] = {0, 0}, sI[2], sI2[2];
+      const int* pp = parts + pb.part_off + row + x;
+      for (int q = 0; q < pb.nparts; ++q) {
+        P[0] += pp[(int64_t)q * npos];
+        if (two) P[1] += pp[(int64_t)q * npos + 256];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t a = a0 + x + 256 * u, b = b0 + x + 256 * u;
+        T d1 = 0, d2 = 0;
+        if (u == 0 || two) {
+          d1 = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
+          d2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
+        }
+        // uint32: d1 is the two's-complement window sum, d2 the (non-negative) one
+        sI[u] = std::is_same<T, long long>::value ? (long long)d1 : (long long)(int)d1;
+        sI2[u] = (long long)d2;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const int64_t i = row + x + 256 * u;
+        const float v = tm_score(n * P[u] - ts.sT * sI[u], n * sI2[u] - sI[u] * sI[u], ts.varT, sqT);
+        if (maps) maps[pb.map_off + i] = v;
+        const unsigned long long k = tm_key(v, (unsigned)i);
+        key = k < key ? k : key;
+      }
     }
   }
 #pragma unroll
@@ -571,6 +591,7 @@ __global__ void fill_u64_kernel(unsigned long long* p, int n) {
 // ------------------------------------------------------------------ ctx state
 struct TmState {
   int H = 0, W = 0, nprob = 0, nwork = 0;
+  bool ii64 = false;  // int64 integral images (some template area >= 2^18, or EF_TM_II64)
   int64_t pitch = 0, max_pos = 0, map_total = 0;
   std::vector<TmProblem> probs;
   DevBuf raw, scaled, bands, d_probs, d_pieces, d_works, d_stat, parts, f8, ii1, ii2, keys, frame_stage, maps;
@@ -661,6 +682,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
   t->W = frame_w;
   t->nprob = n_problems;
   t->pitch = rup((int64_t)frame_w + 256, 64);
+  t->ii64 = getenv("EF_TM_II64") != nullptr;
   const bool dev = flags & EF_MEM_DEVICE;
 
   int64_t raw_bytes = 0;
@@ -696,6 +718,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     map_total += (int64_t)pb.hr * pb.wr;
     max_pos = std::max<int64_t>(max_pos, (int64_t)pb.hr * pb.wr);
     max_h = std::max(max_h, th);
+    if ((int64_t)th * tw >= (int64_t)1 << 18) t->ii64 = true;
     for (int q = 0; q < npiece; ++q) {
       TmPiece pc{};
       pc.prob = p;
@@ -782,13 +805,20 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
     frame_ld = W;
   }
   int8_t* f8 = static_cast<int8_t*>(t->f8.p);
-  long long* ii1 = static_cast<long long*>(t->ii1.p);
-  long long* ii2 = static_cast<long long*>(t->ii2.p);
   TimerEvt tev;
   timer_begin(c, EF_KERNEL_TMATCH, &tev);
-  hipLaunchKernelGGL(tm_rows_kernel, dim3((unsigned)((H + 1 + 3) / 4)), dim3(256), 0, s, f, H, W, frame_ld, f8,
-                     t->pitch, ii1, ii2);
-  hipLaunchKernelGGL(tm_cols_kernel, dim3((unsigned)((W + 1 + kColW - 1) / kColW)), dim3(1024), 0, s, H, W, ii1, ii2);
+  const dim3 rgrid((unsigned)((H + 1 + 3) / 4)), cgrid((unsigned)((W + 1 + kColW - 1) / kColW));
+  if (t->ii64) {
+    long long* ii1 = static_cast<long long*>(t->ii1.p);
+    long long* ii2 = static_cast<long long*>(t->ii2.p);
+    hipLaunchKernelGGL(tm_rows_kernel<long long>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2);
+    hipLaunchKernelGGL(tm_cols_kernel<long long>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
+  } else {
+    unsigned* ii1 = static_cast<unsigned*>(t->ii1.p);
+    unsigned* ii2 = static_cast<unsigned*>(t->ii2.p);
+    hipLaunchKernelGGL(tm_rows_kernel<unsigned>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2);
+    hipLaunchKernelGGL(tm_cols_kernel<unsigned>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
+  }
   if (t->nprob > 0) {
     unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
     hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((t->nprob + 255) / 256)), dim3(256), 0, s, keys, t->nprob);
@@ -807,9 +837,18 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
       }
     }
     const int64_t sblk = 64;  // row-strided blocks per problem
-    hipLaunchKernelGGL(tm_score_kernel, dim3((unsigned)sblk, (unsigned)t->nprob), dim3(256), 0,
-                       s, static_cast<const TmProblem*>(t->d_probs.p), static_cast<const TmStat*>(t->d_stat.p),
-                       static_cast<const int*>(t->parts.p), ii1, ii2, W, maps, keys);
+    const dim3 sgrid((unsigned)sblk, (unsigned)t->nprob);
+    const TmProblem* dp = static_cast<const TmProblem*>(t->d_probs.p);
+    const TmStat* dst = static_cast<const TmStat*>(t->d_stat.p);
+    const int* dparts = static_cast<const int*>(t->parts.p);
+    if (t->ii64)
+      hipLaunchKernelGGL(tm_score_kernel<long long>, sgrid, dim3(256), 0, s, dp, dst, dparts,
+                         static_cast<const long long*>(t->ii1.p), static_cast<const long long*>(t->ii2.p), W, maps,
+                         keys);
+    else
+      hipLaunchKernelGGL(tm_score_kernel<unsigned>, sgrid, dim3(256), 0, s, dp, dst, dparts,
+                         static_cast<const unsigned*>(t->ii1.p), static_cast<const unsigned*>(t->ii2.p), W, maps,
+                         keys);
     timer_end(c, &tev);
     EF_HIP(c, hipGetLastError(), "template match kernels");
     std::vector<unsigned long long> hk((size_t)t->nprob);

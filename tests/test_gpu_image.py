@@ -99,6 +99,28 @@ def test_match_template_extreme_pixels_and_flat(eng):
     assert np.all(maps[2][:40, :80] == 0)
 
 
+@pytest.mark.parametrize("force64", [False, True])
+@pytest.mark.parametrize("ts", [(511, 512), (520, 510)])
+def test_match_template_integral_width(eng, monkeypatch, ts, force64):
+    """Integral images are wrapping uint32 while every template area is < 2^18 and int64
+    otherwise (or with EF_TM_II64).  (511, 512) is the largest uint32 case: on the
+    all-0 region (I' = -128) the window sum of I'^2 is 16384 * 261632, just below 2^32;
+    (520, 510) has area >= 2^18 and must take the int64 form."""
+    if force64:
+        monkeypatch.setenv("EF_TM_II64", "1")
+    rng = np.random.default_rng(ts[0])
+    frame = (rng.integers(0, 2, (560, 540)) * 255).astype(np.uint8)
+    frame[:530, :525] = 0
+    frame[300:, 200:] = rng.integers(0, 256, (260, 340), dtype=np.uint8)
+    t = frame[25:25 + ts[0], 12:12 + ts[1]].copy()
+    eng.tm_prepare([t], [(0,) + ts], frame.shape)
+    best, xs, ys, maps = eng.tm_match(frame, maps=True)
+    R = io.match_template_ccoeff_normed(frame, t)
+    np.testing.assert_array_equal(maps[0], R)
+    v, (mx, my) = io.min_max_loc_max(R)
+    assert (best[0], xs[0], ys[0]) == (np.float32(v), mx, my) == (np.float32(v), 12, 25)
+
+
 def test_scaled_templates_resized_on_gpu(eng):
     """Problems at 0.8/1.2 scale: the GPU resizes the template (INTER_LINEAR) first."""
     from eigenface.image import scaled_sizes
