@@ -64,12 +64,16 @@ struct HaarStump {
 // One stump with its feature inlined (stump order): what the split cascade kernel stages
 // into LDS per stage, so a stump costs no dependent scalar loads of the stump and feature
 // tables (those miss the scalar cache: the tables are ~180 KB for a frontal-face cascade).
+// src[r - 1][k]: corner k of rect r (0 (x, y), 1 (x + w, y), 2 (x, y + h), 3 (x + w, y + h))
+// equals corner src of rect 0, or -1 (its own gather) — e.g. a half rect sharing the
+// whole rect's right edge; the split kernel reuses rect 0's loaded value.
 struct HaarRec {
   float thr, left, right;
   int nr;
   int x[3], y[3], w[3], h[3];
   float wt[3];
   int pad;
+  signed char src[2][4];
 };
 struct HaarStage {
   int first, count;
@@ -337,6 +341,33 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
   if (k < cap) out[k] = w;
 }
 
+// The feature value of predictOrderedStump (same int box sums, same float operations in
+// the same order) with rect 1/2 corners that coincide with rect 0's taken from rect 0's
+// loads instead of gathered again (the split kernel is gather-bound).
+__device__ __forceinline__ float haar_feature_shared(const int* __restrict__ a1, int64_t W1, int wx, int wy,
+                                                     const HaarRec& f) {
+  const int64_t b0 = (int64_t)(wy + f.y[0]) * W1 + wx + f.x[0], h0 = (int64_t)f.h[0] * W1;
+  const int c[4] = {a1[b0], a1[b0 + f.w[0]], a1[b0 + h0], a1[b0 + h0 + f.w[0]]};
+  float val = __fmul_rn(f.wt[0], (float)(c[3] - c[1] - c[2] + c[0]));
+#pragma unroll
+  for (int r = 1; r < 3; ++r) {
+    if (r == 2 && f.wt[2] == 0.f) break;
+    const int64_t br = (int64_t)(wy + f.y[r]) * W1 + wx + f.x[r], hr = (int64_t)f.h[r] * W1;
+    const int64_t off[4] = {br, br + f.w[r], br + hr, br + hr + f.w[r]};
+    int v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sc = f.src[r - 1][k];
+      if (sc < 0)
+        v[k] = a1[off[k]];
+      else
+        v[k] = sc == 0 ? c[0] : (sc == 1 ? c[1] : (sc == 2 ? c[2] : c[3]));
+    }
+    val = __fadd_rn(val, __fmul_rn(f.wt[r], (float)(v[3] - v[1] - v[2] + v[0])));
+  }
+  return val;
+}
+
 // Pass 3, split form: a workgroup of 4 waves takes 64 windows (lane = window, as above, so
 // each stump's integral-image gathers stay coalesced over neighbouring windows) and wave q
 // evaluates stumps q, q+4, q+8, ... of every stage, read from LDS records (stump + its
@@ -385,10 +416,7 @@ __global__ __launch_bounds__(NQ * 64) void haar_cascade_split_kernel(const HaarL
 #pragma unroll 4
         for (int t = q; t < cn; t += NQ) {  // wave q: every NQ-th stump (the sum is order-free)
           const HaarRec& f = srec[t];
-          float val = __fmul_rn(f.wt[0], (float)box(a1, W1, w.x + f.x[0], w.y + f.y[0], f.w[0], f.h[0]));
-          val = __fadd_rn(val, __fmul_rn(f.wt[1], (float)box(a1, W1, w.x + f.x[1], w.y + f.y[1], f.w[1], f.h[1])));
-          if (f.wt[2] != 0.f)
-            val = __fadd_rn(val, __fmul_rn(f.wt[2], (float)box(a1, W1, w.x + f.x[2], w.y + f.y[2], f.w[2], f.h[2])));
+          float val = haar_feature_shared(a1, W1, w.x, w.y, f);
           val = __fmul_rn(val, vnf);
           tmp = __dadd_rn(tmp, (double)(val < f.thr ? f.left : f.right));
         }
@@ -593,6 +621,24 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
     HaarRec& r = rc[i];
     r.thr = sp[i].thr, r.left = sp[i].left, r.right = sp[i].right, r.nr = q.nr, r.pad = 0;
     for (int k = 0; k < 3; ++k) r.x[k] = q.x[k], r.y[k] = q.y[k], r.w[k] = q.w[k], r.h[k] = q.h[k], r.wt[k] = q.wt[k];
+    auto corner = [&](int rr, int k, int& cx, int& cy) {
+      cx = r.x[rr] + ((k & 1) ? r.w[rr] : 0);
+      cy = r.y[rr] + ((k & 2) ? r.h[rr] : 0);
+    };
+    for (int rr = 1; rr < 3; ++rr)
+      for (int k = 0; k < 4; ++k) {
+        int x1, y1;
+        corner(rr, k, x1, y1);
+        r.src[rr - 1][k] = -1;
+        for (int m = 0; m < 4; ++m) {
+          int x0, y0;
+          corner(0, m, x0, y0);
+          if (x0 == x1 && y0 == y1) {
+            r.src[rr - 1][k] = (signed char)m;
+            break;
+          }
+        }
+      }
   }
   EF_TRY(ensure(c, h->recs, rc.size() * sizeof(HaarRec)));
   EF_HIP(c, hipMemcpy(h->recs.p, rc.data(), rc.size() * sizeof(HaarRec), hipMemcpyHostToDevice), "H2D records");
