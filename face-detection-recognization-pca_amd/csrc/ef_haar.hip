@@ -86,7 +86,8 @@ struct HaarLayer {
   int64_t pix_off, ii_off, res_off;
 };
 struct HaarCand {
-  int layer, y, x, pad;
+  int layer, y, x;
+  float vnf;  // the window's normalisation factor (stage 0's haar_norm), carried along the lists
 };
 
 // ------------------------------------------------------------------ integral images
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
                                                           const unsigned* __restrict__ ii2,
                                                           const HaarStage* __restrict__ stages,
                                                           const HaarRec* __restrict__ recs, int ww, int wh,
-                                                          signed char* __restrict__ res) {
+                                                          signed char* __restrict__ res, float* __restrict__ vn) {
   const HaarLayer ly = L[blockIdx.y];
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= (int64_t)ly.nx * ly.ny) return;
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
   signed char r = -1;
   if (vnf != 0.f) r = haar_stage(a1, W1, x, y, vnf, stages[0], recs) ? 1 : 0;
   res[ly.res_off + p] = r;
+  vn[ly.res_off + p] = vnf;
 }
 
 // Pass 2: the invoker's x walk for each (layer, evaluated row): positions 0, step, ...
@@ -266,6 +268,7 @@ __device__ __forceinline__ unsigned long long haar_walk(unsigned long long rej, 
 __global__ __launch_bounds__(1024) void haar_rows_kernel(const HaarLayer* __restrict__ L, int nlayers,
                                                          const int* __restrict__ row_start,
                                                          const signed char* __restrict__ res,
+                                                         const float* __restrict__ vn,
                                                          HaarCand* __restrict__ work, int* __restrict__ nwork,
                                                          int cap) {
   __shared__ int rs[kHaarMaxLayers + 1];
@@ -311,7 +314,8 @@ __global__ __launch_bounds__(1024) void haar_rows_kernel(const HaarLayer* __rest
     const unsigned long long surv = chunk(c0, v);
     if ((surv >> lane) & 1ull) {
       const int kk = k + __popcll(surv & ((1ull << lane) - 1ull));
-      if (kk < cap) work[kk] = HaarCand{li, y, (c0 + lane) * ly.step, 0};
+      const int x = (c0 + lane) * ly.step;
+      if (kk < cap) work[kk] = HaarCand{li, y, x, vn[ly.res_off + (int64_t)y * ly.nx + x]};
     }
     k += __popcll(surv);
   }
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(256) void haar_cascade_kernel(const HaarLayer* __re
   const HaarLayer ly = L[w.layer];
   const int64_t W1 = ly.w + 1;
   const int* a1 = ii1 + ly.ii_off;
-  const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
+  const float vnf = w.vnf;  // == haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh)
   for (int s = s0; s < s1; ++s)
     if (!haar_stage(a1, W1, w.x, w.y, vnf, stages[s], recs)) return;
   const int k = atomicAdd(nout, 1);
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(NQ * 64) void haar_cascade_split_kernel(const HaarL
   const HaarLayer ly = L[w.layer];
   const int64_t W1 = ly.w + 1;
   const int* a1 = ii1 + ly.ii_off;
-  const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh);
+  const float vnf = w.vnf;  // == haar_norm(a1, ii2 + ly.ii_off, W1, w.x, w.y, ww, wh)
   bool alive = valid;
   __shared__ HaarRec srec[kHaarRecChunk];
   for (int st = s0; st < s1; ++st) {
@@ -444,13 +448,13 @@ struct HaarState {
   int ww = 0, wh = 0, nstages = 0;
   bool order_free = false;  // every stage sum is exact in double in any order (see set_cascade)
   DevBuf stages, recs;
-  DevBuf pix, ii1, ii2, res, layers, rowstart, work, cand, counters, frame, desc;
+  DevBuf pix, ii1, ii2, res, vn, layers, rowstart, work, cand, counters, frame, desc;
 };
 
 void haar_release(ef_ctx* c) {
   if (!c || !c->haar) return;
   HaarState* h = static_cast<HaarState*>(c->haar);
-  DevBuf* bufs[] = {&h->stages, &h->recs, &h->pix, &h->ii1,      &h->ii2,     &h->res,
+  DevBuf* bufs[] = {&h->stages, &h->recs, &h->pix, &h->ii1,      &h->ii2,     &h->res, &h->vn,
                     &h->layers, &h->rowstart, &h->work, &h->cand, &h->counters, &h->frame, &h->desc};
   for (DevBuf* b : bufs) release(*b);
   delete h;
@@ -697,6 +701,7 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   EF_TRY(ensure(c, h->ii1, ii * 4));
   EF_TRY(ensure(c, h->ii2, ii * 4));
   EF_TRY(ensure(c, h->res, std::max<int64_t>(resn, 16)));
+  EF_TRY(ensure(c, h->vn, std::max<int64_t>(resn * 4, 16)));
   EF_TRY(ensure(c, h->layers, layers.size() * sizeof(HaarLayer)));
   EF_TRY(ensure(c, h->rowstart, row_start.size() * sizeof(int)));
   EF_TRY(ensure(c, h->work, (size_t)cap * sizeof(HaarCand)));
@@ -745,13 +750,14 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   const HaarRec* drc = static_cast<const HaarRec*>(h->recs.p);
   signed char* res = static_cast<signed char*>(h->res.p);
   hipLaunchKernelGGL(haar_stage0_kernel, dim3((unsigned)((maxpos + 255) / 256), (unsigned)nl), dim3(256), 0, s, dl, ii1,
-                     ii2, dst, drc, h->ww, h->wh, res);
+                     ii2, dst, drc, h->ww, h->wh, res, static_cast<float*>(h->vn.p));
   int* cnt = static_cast<int*>(h->counters.p);
   HaarCand* work = static_cast<HaarCand*>(h->work.p);
   HaarCand* cand = static_cast<HaarCand*>(h->cand.p);
   hipLaunchKernelGGL(haar_rows_kernel, dim3((unsigned)((row_start[nl] + kHaarRowWaves - 1) / kHaarRowWaves)),
                      dim3(64 * kHaarRowWaves), 0, s, dl, nl,
-                     static_cast<const int*>(h->rowstart.p), res, work, cnt, cap);
+                     static_cast<const int*>(h->rowstart.p), res, static_cast<const float*>(h->vn.p), work, cnt,
+                     cap);
   int hc[16] = {0};
   EF_HIP(c, hipMemcpyAsync(hc, cnt, sizeof(int), hipMemcpyDeviceToHost, s), "D2H work count");
   EF_HIP(c, hipStreamSynchronize(s), "sync");
