@@ -763,7 +763,25 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   EF_HIP(c, hipStreamSynchronize(s), "sync");
   if (hc[0] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: work-list capacity exceeded");
   // stage groups; the lists ping-pong between work and cand, counters cnt[g]
-  const int groups[] = {1, 3, 6, 10, 15, 1 << 30};
+  // EF_HAAR_GROUPS="1,4,8,14" (experiments): first stage of each group, ascending, <= 14.
+  // Default {1, 4, 8, 14} (tools/haar_groups.sh, 640x480 synthetic frontal cascade, ms per
+  // frame): 1,3,6,10,15 0.532; 1,4,8,14 0.490; 1,6,12 0.487; 1,4,9 0.497; eleven or twelve
+  // groups 0.61-0.64 — fewer, longer groups win until the dead lanes of a long group cost
+  // more than a launch and a compaction.
+  static const std::vector<int> groups = [] {
+    std::vector<int> g;
+    if (const char* e = getenv("EF_HAAR_GROUPS")) {
+      for (const char* p = e; *p;) {
+        const int v = atoi(p);
+        if (v >= 1 && (g.empty() || v > g.back()) && g.size() < 14) g.push_back(v);
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    }
+    if (g.empty() || g[0] != 1) g = {1, 4, 8, 14};
+    g.push_back(1 << 30);
+    return g;
+  }();
   // every group takes the split form when the cascade's stage sums are order-free
   // (measured, 640x480 synthetic frontal cascade with LDS stump records and 8 waves: split
   // from group 1 0.637 ms, from stage 3 0.652, from stage 6 0.673 per frame)
