@@ -174,7 +174,10 @@ struct TmStat {
 template <typename T>
 __global__ __launch_bounds__(256) void tm_rows_kernel(const uint8_t* __restrict__ f, int H, int W, int64_t ld,
                                                       int8_t* __restrict__ f8, int64_t pitch,
-                                                      T* __restrict__ ii1, T* __restrict__ ii2) {
+                                                      T* __restrict__ ii1, T* __restrict__ ii2,
+                                                      unsigned long long* __restrict__ keys, int nkeys) {
+  if (blockIdx.x == 0)  // reset the per-problem best keys (consumed by tm_score_kernel)
+    for (int k = threadIdx.x; k < nkeys; k += 256) keys[k] = ~0ull;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row > H) return;
   const int64_t W1 = W + 1;
@@ -583,10 +586,6 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
   }
 }
 
-__global__ void fill_u64_kernel(unsigned long long* p, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = ~0ull;
-}
 
 // ------------------------------------------------------------------ ctx state
 struct TmState {
@@ -805,23 +804,24 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
     frame_ld = W;
   }
   int8_t* f8 = static_cast<int8_t*>(t->f8.p);
+  unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
   TimerEvt tev;
   timer_begin(c, EF_KERNEL_TMATCH, &tev);
   const dim3 rgrid((unsigned)((H + 1 + 3) / 4)), cgrid((unsigned)((W + 1 + kColW - 1) / kColW));
   if (t->ii64) {
     long long* ii1 = static_cast<long long*>(t->ii1.p);
     long long* ii2 = static_cast<long long*>(t->ii2.p);
-    hipLaunchKernelGGL(tm_rows_kernel<long long>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2);
+    hipLaunchKernelGGL(tm_rows_kernel<long long>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2,
+                       keys, t->nprob);
     hipLaunchKernelGGL(tm_cols_kernel<long long>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
   } else {
     unsigned* ii1 = static_cast<unsigned*>(t->ii1.p);
     unsigned* ii2 = static_cast<unsigned*>(t->ii2.p);
-    hipLaunchKernelGGL(tm_rows_kernel<unsigned>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2);
+    hipLaunchKernelGGL(tm_rows_kernel<unsigned>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2,
+                       keys, t->nprob);
     hipLaunchKernelGGL(tm_cols_kernel<unsigned>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
   }
   if (t->nprob > 0) {
-    unsigned long long* keys = static_cast<unsigned long long*>(t->keys.p);
-    hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)((t->nprob + 255) / 256)), dim3(256), 0, s, keys, t->nprob);
     if (t->nwork > 0)
       hipLaunchKernelGGL(tm_corr_kernel, dim3((unsigned)t->nwork), dim3(512), 0, s, f8, t->pitch,
                          static_cast<const uint8_t*>(t->bands.p), static_cast<const TmPiece*>(t->d_pieces.p),
