@@ -106,40 +106,32 @@ __global__ __launch_bounds__(256) void haar_rows_ii_kernel(const uint8_t* __rest
     return;
   }
   const uint8_t* src = pix + ly.pix_off + (int64_t)(row - 1) * ly.w;
-  const int per = (ly.w + 63) / 64, xb = lane * per;
-  int s1 = 0;
-  unsigned s2 = 0;
-  for (int i = 0; i < per; ++i) {
-    const int x = xb + i;
-    if (x < ly.w) {
-      const int v = src[x];
-      s1 += v;
-      s2 += (unsigned)(v * v);
-    }
-  }
-  int e1 = s1;
-  unsigned e2 = s2;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int t1 = __shfl_up(e1, off);
-    const unsigned t2 = __shfl_up(e2, off);
-    if (lane >= off) {
-      e1 += t1;
-      e2 += t2;
-    }
-  }
-  e1 -= s1;
-  e2 -= s2;
+  // 64-pixel chunks, lane = pixel (coalesced), an inclusive wave scan per chunk carried
+  // into the row totals (CV_32S sum / wrapping sqsum: the same values mod 2^32)
   if (lane == 0) r1[0] = r2[0] = 0;
-  for (int i = 0; i < per; ++i) {
-    const int x = xb + i;
+  unsigned c1 = 0, c2 = 0;
+  for (int x0 = 0; x0 < ly.w; x0 += 64) {
+    const int x = x0 + lane;
+    unsigned e1 = 0, e2 = 0;
     if (x < ly.w) {
-      const int v = src[x];
-      e1 += v;
-      e2 += (unsigned)(v * v);
-      r1[x + 1] = e1;
-      r2[x + 1] = e2;
+      const unsigned v = src[x];
+      e1 = v;
+      e2 = v * v;
     }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned t1 = __shfl_up(e1, off), t2 = __shfl_up(e2, off);
+      if (lane >= off) {
+        e1 += t1;
+        e2 += t2;
+      }
+    }
+    if (x < ly.w) {
+      r1[x + 1] = (int)(c1 + e1);
+      r2[x + 1] = c2 + e2;
+    }
+    c1 += __shfl(e1, 63);
+    c2 += __shfl(e2, 63);
   }
 }
 
