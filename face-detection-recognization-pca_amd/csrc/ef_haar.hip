@@ -209,7 +209,7 @@ __device__ __forceinline__ bool haar_stage(const int* ii1, int64_t W1, int x, in
   return !(tmp < (double)st.thr);
 }
 
-// Pass 1: variance + first stage for every window origin of every layer (grid (pos/256,
+// Pass 1: variance + first stage for every visitable window origin of every layer (grid (pos/256,
 // layers)); res = -1 (low variance), 0 (rejected by stage 0), 1 (passed stage 0).
 __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __restrict__ L,
                                                           const int* __restrict__ ii1,
@@ -218,9 +218,14 @@ __global__ __launch_bounds__(256) void haar_stage0_kernel(const HaarLayer* __res
                                                           const HaarRec* __restrict__ recs, int ww, int wh,
                                                           signed char* __restrict__ res, float* __restrict__ vn) {
   const HaarLayer ly = L[blockIdx.y];
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (int64_t)ly.nx * ly.ny) return;
-  const int y = (int)(p / ly.nx), x = (int)(p - (p / ly.nx) * ly.nx);
+  // only the origins the invoker can visit: x and y multiples of the layer's step (a
+  // step-2 layer has a quarter of its origins evaluated; the rest are never read)
+  const int nxs = (ly.nx + ly.step - 1) / ly.step, nys = (ly.ny + ly.step - 1) / ly.step;
+  const int64_t ps = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ps >= (int64_t)nxs * nys) return;
+  const int ys = (int)(ps / nxs);
+  const int y = ys * ly.step, x = (int)(ps - (int64_t)ys * nxs) * ly.step;
+  const int64_t p = (int64_t)y * ly.nx + x;
   const int64_t W1 = ly.w + 1;
   const int* a1 = ii1 + ly.ii_off;
   const float vnf = haar_norm(a1, ii2 + ly.ii_off, W1, x, y, ww, wh);
@@ -731,7 +736,7 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   for (auto& ly : layers) {
     maxh = std::max(maxh, ly.h);
     maxw = std::max(maxw, ly.w);
-    maxpos = std::max<int64_t>(maxpos, (int64_t)ly.nx * ly.ny);
+    maxpos = std::max<int64_t>(maxpos, (int64_t)((ly.nx + ly.step - 1) / ly.step) * ((ly.ny + ly.step - 1) / ly.step));
   }
   const uint8_t* lp = static_cast<const uint8_t*>(h->pix.p);
   hipLaunchKernelGGL(haar_rows_ii_kernel, dim3((unsigned)((maxh + 1 + 3) / 4), (unsigned)nl), dim3(256), 0, s, lp, dl,
