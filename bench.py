@@ -453,7 +453,7 @@ def main():
     match = float((idx == targets).mean())
 
     host_rate = None
-    if world == 1 and not os.environ.get("EF_SEARCH_ABL"):  # PCIe-inclusive rate (never `value`)
+    if world == 1:  # PCIe-inclusive rate (never `value`)
         eng.use_own_stream()
         eng.recognize_keys(P, args.metric)
         t = time.perf_counter()

@@ -2,6 +2,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -67,10 +68,11 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
     if (_e != hipSuccess) return hip_err(ctx, _e, what);  \
   } while (0)
 
-// Search the probes already in ctx->q_pad (bpad rows, kp = ctx->g_kp) into keys_dev.
-static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev) {
+// Search the probes already in ctx->q_pad (bpad rows, kp = ctx->g_kp) of this rank's
+// gallery: keys_dev[b] and, when match_dev is non-null, the fp64 match records.
+static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev, ef_match* match_dev) {
   if (c->n_gallery == 0) {
-    EF_HIP(c, launch_keys_none(c->stream, keys_dev, b), "keys");
+    EF_HIP(c, launch_keys_none(c->stream, keys_dev, b, match_dev), "keys");
     return EF_OK;
   }
   const SearchPlan pl = search_plan(bpad, c->n_gallery, c->g_kp);
@@ -95,6 +97,7 @@ static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long
   ws.cand = reinterpret_cast<int*>(base);
   base += ncand;
   ws.cand_cnt = reinterpret_cast<int*>(base);
+  ws.match = match_dev;
   const float* aux = static_cast<const float*>(metric == EF_METRIC_L2 ? c->gnorm2.p : c->ginv.p);
   EF_HIP(c,
          launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), bpad, b,
@@ -104,9 +107,28 @@ static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long
   return EF_OK;
 }
 
+// Search ctx->q_pad: this rank's shard, then (communicator attached) the exact merge of
+// every rank's match records (ef_comm.hip).  match_dev (optional) receives the records
+// of the (global) winners.
+static int search_qpad(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev, ef_match* match_dev) {
+  if (!c->comm || c->comm_size == 1) return search_local(c, bpad, b, metric, keys_dev, match_dev);
+  EF_TRY(ensure(c, c->match_local, (size_t)b * sizeof(ef_match)));
+  EF_TRY(ensure(c, c->match_all, (size_t)b * c->comm_size * sizeof(ef_match)));
+  ef_match* loc = static_cast<ef_match*>(c->match_local.p);
+  ef_match* all = static_cast<ef_match*>(c->match_all.p);
+  EF_TRY(search_local(c, bpad, b, metric, keys_dev, loc));
+  EF_TRY(comm_allgather(c, loc, all, (size_t)b * sizeof(ef_match)));
+  EF_HIP(c, launch_matches_merge(c->stream, all, c->comm_size, b, keys_dev, match_dev), "matches merge");
+  return EF_OK;
+}
+
 // Project b probes (device pointer P) into ctx->q_pad; optional feature output (device).
-static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t bpad, float* f_dev) {
-  EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->kp * sizeof(float)));
+static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t bpad, float* f_dev, DevBuf* dst) {
+  EF_TRY(ensure(c, *dst, (size_t)bpad * c->kp * sizeof(float)));
+  if (b == 0) {  // this rank's slice of a sharded projection can be empty
+    EF_HIP(c, hipMemsetAsync(dst->p, 0, (size_t)bpad * c->kp * sizeof(float), c->stream), "zero features");
+    return EF_OK;
+  }
   int64_t pps = 0;
   const int ns = c->bf16 ? project_bf16_nsplit(bpad, c->d, c->kpw, &pps) : project_nsplit(bpad, c->d, c->kpw, &pps);
   EF_TRY(ensure(c, c->proj_part, (size_t)ns * bpad * c->kpw * sizeof(float)));
@@ -128,8 +150,35 @@ static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t b
   EF_HIP(c,
          launch_project_reduce(c->stream, static_cast<const float*>(c->proj_part.p), ns, b, bpad, c->kpw,
                                c->k, c->kp, c->bf16 ? static_cast<const float*>(c->corr.p) : nullptr,
-                               static_cast<float*>(c->q_pad.p), f_dev),
+                               static_cast<float*>(dst->p), f_dev),
          "project reduce");
+  return EF_OK;
+}
+
+// Features of the whole batch in ctx->q_pad for the search.  With a communicator attached
+// rank r projects probes [r*cs, (r+1)*cs), cs = ceil(b / ranks), and one all-gather of the
+// (cs x kp) slices assembles the batch (rows past b are zero); otherwise the whole batch.
+// Returns the padded row count of q_pad in *bpad_out.  f_dev (optional) gets this rank's
+// rows only when sharded, so the fused path keeps the unsharded projection for it.
+static int project_for_search(ef_ctx* c, const void* Pd, int dtype, int64_t b, float* f_dev, int64_t* bpad_out) {
+  if (!c->comm || c->comm_size == 1 || f_dev) {
+    const int64_t bpad = round_up(b, kSearchProbeTile);
+    EF_TRY(project_dev(c, Pd, dtype, b, bpad, f_dev, &c->q_pad));
+    *bpad_out = bpad;
+    return EF_OK;
+  }
+  const int64_t R = c->comm_size, cs = (b + R - 1) / R;
+  const int64_t lo = std::min<int64_t>(b, c->comm_rank * cs), hi = std::min<int64_t>(b, (c->comm_rank + 1) * cs);
+  const size_t esz = dtype == EF_U8 ? 1 : 4;
+  const void* Pl = static_cast<const char*>(Pd) + (size_t)lo * c->d * esz;
+  EF_TRY(project_dev(c, Pl, dtype, hi - lo, round_up(cs, kSearchProbeTile), nullptr, &c->q_local));
+  const int64_t rows = R * cs, bpad = round_up(rows, kSearchProbeTile);
+  EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->kp * sizeof(float)));
+  float* q = static_cast<float*>(c->q_pad.p);
+  EF_TRY(comm_allgather(c, c->q_local.p, q, (size_t)cs * c->kp * sizeof(float)));
+  if (bpad > rows)
+    EF_HIP(c, hipMemsetAsync(q + rows * c->kp, 0, (size_t)(bpad - rows) * c->kp * sizeof(float), c->stream), "pad");
+  *bpad_out = bpad;
   return EF_OK;
 }
 
@@ -192,6 +241,7 @@ void ef_destroy(ef_ctx* c) {
                     &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
   for (auto& b : c->fit_pool) release(b);
+  comm_release(c);
   blas_release(c);
   tm_release(c);
   haar_release(c);
@@ -290,7 +340,7 @@ int ef_project(ef_ctx* c, const void* P, int32_t dtype, int64_t b, float* F, uin
     EF_TRY(ensure(c, c->feats_dev, (size_t)b * c->k * sizeof(float)));
     fdev = static_cast<float*>(c->feats_dev.p);
   }
-  EF_TRY(project_dev(c, Pd, dtype, b, bpad, fdev));
+  EF_TRY(project_dev(c, Pd, dtype, b, bpad, fdev, &c->q_pad));
   if (!(flags & EF_MEM_DEVICE)) {
     EF_HIP(c, hipMemcpyAsync(F, fdev, (size_t)b * c->k * sizeof(float), hipMemcpyDeviceToHost, c->stream),
            "D2H features");
@@ -345,17 +395,20 @@ int ef_gallery_set(ef_ctx* c, const float* G, int64_t n, int32_t k, int64_t offs
   return EF_OK;
 }
 
-int ef_search(ef_ctx* c, const float* Q, int64_t b, int32_t metric, int64_t* keys, uint32_t flags) {
+// ef_search / ef_search_matches: keys (and/or match records) of b probe features.
+static int search_impl(ef_ctx* c, const float* Q, int64_t b, int32_t metric, int64_t* keys, ef_match* match,
+                       uint32_t flags, const char* fn) {
   if (!c) return EF_E_INVALID;
-  if (c->g_k == 0) return set_err(c, EF_E_STATE, "ef_search: no gallery (call ef_gallery_set)");
-  if (!Q || !keys || b < 0 || (metric != EF_METRIC_L2 && metric != EF_METRIC_COSINE))
-    return set_err(c, EF_E_INVALID, "ef_search: bad arguments");
+  if (c->g_k == 0) return set_err(c, EF_E_STATE, std::string(fn) + ": no gallery (call ef_gallery_set)");
+  if (!Q || (!keys && !match) || b < 0 || (metric != EF_METRIC_L2 && metric != EF_METRIC_COSINE))
+    return set_err(c, EF_E_INVALID, std::string(fn) + ": bad arguments");
   if (b == 0) return EF_OK;
   (void)hipSetDevice(c->device);
+  const bool dev = flags & EF_MEM_DEVICE;
   const int64_t bpad = round_up(b, kSearchProbeTile);
   EF_TRY(ensure(c, c->q_pad, (size_t)bpad * c->g_kp * sizeof(float)));
   const float* qsrc = Q;
-  if (!(flags & EF_MEM_DEVICE)) {
+  if (!dev) {
     EF_TRY(ensure(c, c->p_stage, (size_t)b * c->g_k * sizeof(float)));
     EF_HIP(c, hipMemcpyAsync(c->p_stage.p, Q, (size_t)b * c->g_k * sizeof(float), hipMemcpyHostToDevice, c->stream),
            "H2D queries");
@@ -363,59 +416,126 @@ int ef_search(ef_ctx* c, const float* Q, int64_t b, int32_t metric, int64_t* key
   }
   EF_HIP(c, launch_pad_rows(c->stream, qsrc, b, c->g_k, bpad, static_cast<float*>(c->q_pad.p), c->g_kp),
          "pad queries");
-  long long* kdev = reinterpret_cast<long long*>(keys);
-  if (!(flags & EF_MEM_DEVICE)) {
-    EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long)));
-    kdev = static_cast<long long*>(c->keys.p);
-  }
-  EF_TRY(search_qpad(c, bpad, b, metric, kdev));
-  if (!(flags & EF_MEM_DEVICE)) {
-    EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
-           "D2H keys");
+  EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long) + (size_t)b * sizeof(ef_match)));
+  long long* kdev = (dev && keys) ? reinterpret_cast<long long*>(keys) : static_cast<long long*>(c->keys.p);
+  ef_match* mdev = nullptr;
+  if (match) mdev = dev ? match : reinterpret_cast<ef_match*>(static_cast<char*>(c->keys.p) + bpad * sizeof(long long));
+  EF_TRY(search_qpad(c, bpad, b, metric, kdev, mdev));
+  if (!dev) {
+    if (keys)
+      EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
+             "D2H keys");
+    if (match)
+      EF_HIP(c, hipMemcpyAsync(match, mdev, (size_t)b * sizeof(ef_match), hipMemcpyDeviceToHost, c->stream),
+             "D2H matches");
     EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
   }
   return EF_OK;
 }
 
-int ef_recognize(ef_ctx* c, const void* P, int32_t dtype, int64_t b, int32_t metric, int64_t* keys,
-                 float* feats, uint32_t flags) {
+static int recognize_impl(ef_ctx* c, const void* P, int32_t dtype, int64_t b, int32_t metric, int64_t* keys,
+                          ef_match* match, float* feats, uint32_t flags, const char* fn) {
   if (!c) return EF_E_INVALID;
-  if (c->d == 0) return set_err(c, EF_E_STATE, "ef_recognize: no model (call ef_model_set)");
-  if (c->g_k == 0) return set_err(c, EF_E_STATE, "ef_recognize: no gallery (call ef_gallery_set)");
-  if (c->g_k != c->k) return set_err(c, EF_E_INVALID, "ef_recognize: gallery k != model k");
-  if (!P || !keys || b < 0 || (dtype != EF_U8 && dtype != EF_F32) ||
+  const std::string f(fn);
+  if (c->d == 0) return set_err(c, EF_E_STATE, f + ": no model (call ef_model_set)");
+  if (c->g_k == 0) return set_err(c, EF_E_STATE, f + ": no gallery (call ef_gallery_set)");
+  if (c->g_k != c->k) return set_err(c, EF_E_INVALID, f + ": gallery k != model k");
+  if (!P || (!keys && !match) || b < 0 || (dtype != EF_U8 && dtype != EF_F32) ||
       (metric != EF_METRIC_L2 && metric != EF_METRIC_COSINE))
-    return set_err(c, EF_E_INVALID, "ef_recognize: bad arguments");
+    return set_err(c, EF_E_INVALID, f + ": bad arguments");
   if (b == 0) return EF_OK;
   (void)hipSetDevice(c->device);
-  const int64_t bpad = round_up(b, kSearchProbeTile);
+  const bool dev = flags & EF_MEM_DEVICE;
   const void* Pd = nullptr;
   EF_TRY(stage_probes(c, P, dtype, b, flags, &Pd));
   float* fdev = nullptr;
   if (feats) {
-    if (flags & EF_MEM_DEVICE) {
+    if (dev) {
       fdev = feats;
     } else {
       EF_TRY(ensure(c, c->feats_dev, (size_t)b * c->k * sizeof(float)));
       fdev = static_cast<float*>(c->feats_dev.p);
     }
   }
-  EF_TRY(project_dev(c, Pd, dtype, b, bpad, fdev));
-  long long* kdev = reinterpret_cast<long long*>(keys);
-  if (!(flags & EF_MEM_DEVICE)) {
-    EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long)));
-    kdev = static_cast<long long*>(c->keys.p);
-  }
-  EF_TRY(search_qpad(c, bpad, b, metric, kdev));
-  if (!(flags & EF_MEM_DEVICE)) {
-    EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
-           "D2H keys");
+  int64_t bpad = 0;
+  EF_TRY(project_for_search(c, Pd, dtype, b, fdev, &bpad));
+  EF_TRY(ensure(c, c->keys, (size_t)bpad * sizeof(long long) + (size_t)b * sizeof(ef_match)));
+  long long* kdev = (dev && keys) ? reinterpret_cast<long long*>(keys) : static_cast<long long*>(c->keys.p);
+  ef_match* mdev = nullptr;
+  if (match) mdev = dev ? match : reinterpret_cast<ef_match*>(static_cast<char*>(c->keys.p) + bpad * sizeof(long long));
+  EF_TRY(search_qpad(c, bpad, b, metric, kdev, mdev));
+  if (!dev) {
+    if (keys)
+      EF_HIP(c, hipMemcpyAsync(keys, kdev, (size_t)b * sizeof(long long), hipMemcpyDeviceToHost, c->stream),
+             "D2H keys");
+    if (match)
+      EF_HIP(c, hipMemcpyAsync(match, mdev, (size_t)b * sizeof(ef_match), hipMemcpyDeviceToHost, c->stream),
+             "D2H matches");
     if (feats)
       EF_HIP(c, hipMemcpyAsync(feats, fdev, (size_t)b * c->k * sizeof(float), hipMemcpyDeviceToHost, c->stream),
              "D2H features");
     EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
   }
   return EF_OK;
+}
+
+int ef_search(ef_ctx* c, const float* Q, int64_t b, int32_t metric, int64_t* keys, uint32_t flags) {
+  if (c && !keys) return set_err(c, EF_E_INVALID, "ef_search: bad arguments");
+  return search_impl(c, Q, b, metric, keys, nullptr, flags, "ef_search");
+}
+
+int ef_search_matches(ef_ctx* c, const float* Q, int64_t b, int32_t metric, ef_match* out, uint32_t flags) {
+  if (c && !out) return set_err(c, EF_E_INVALID, "ef_search_matches: bad arguments");
+  return search_impl(c, Q, b, metric, nullptr, out, flags, "ef_search_matches");
+}
+
+int ef_recognize(ef_ctx* c, const void* P, int32_t dtype, int64_t b, int32_t metric, int64_t* keys, float* feats,
+                 uint32_t flags) {
+  if (c && !keys) return set_err(c, EF_E_INVALID, "ef_recognize: bad arguments");
+  return recognize_impl(c, P, dtype, b, metric, keys, nullptr, feats, flags, "ef_recognize");
+}
+
+int ef_recognize_matches(ef_ctx* c, const void* P, int32_t dtype, int64_t b, int32_t metric, ef_match* out,
+                         float* feats, uint32_t flags) {
+  if (c && !out) return set_err(c, EF_E_INVALID, "ef_recognize_matches: bad arguments");
+  return recognize_impl(c, P, dtype, b, metric, nullptr, out, feats, flags, "ef_recognize_matches");
+}
+
+int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
+  if (!c) return EF_E_INVALID;
+  switch (option) {
+    case EF_OPT_FIT_MAX_ITERS:
+      if (value < 1) return set_err(c, EF_E_INVALID, "EF_OPT_FIT_MAX_ITERS must be >= 1");
+      c->opt_fit_max_iters = value;
+      return EF_OK;
+    case EF_OPT_FIT_FP32_COARSE:
+      c->opt_fit_fp32_coarse = value != 0;
+      return EF_OK;
+    case EF_OPT_COV_SLAB_BYTES:
+      if (value < 1) return set_err(c, EF_E_INVALID, "EF_OPT_COV_SLAB_BYTES must be >= 1");
+      c->opt_cov_slab_bytes = value;
+      return EF_OK;
+    case EF_OPT_TM_INT64_SUMS:
+      c->opt_tm_int64 = value != 0;
+      return EF_OK;
+    case EF_OPT_HAAR_ORDERED:
+      c->opt_haar_ordered = value != 0;
+      return EF_OK;
+    default:
+      return set_err(c, EF_E_INVALID, "ef_set_option: unknown option " + std::to_string(option));
+  }
+}
+
+int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
+  if (!c || !value) return EF_E_INVALID;
+  switch (option) {
+    case EF_OPT_FIT_MAX_ITERS: *value = c->opt_fit_max_iters; return EF_OK;
+    case EF_OPT_FIT_FP32_COARSE: *value = c->opt_fit_fp32_coarse; return EF_OK;
+    case EF_OPT_COV_SLAB_BYTES: *value = c->opt_cov_slab_bytes; return EF_OK;
+    case EF_OPT_TM_INT64_SUMS: *value = c->opt_tm_int64; return EF_OK;
+    case EF_OPT_HAAR_ORDERED: *value = c->opt_haar_ordered; return EF_OK;
+    default: return EF_E_INVALID;
+  }
 }
 
 void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx) {

@@ -383,7 +383,7 @@ int64_t cov_i8_order_bytes(int64_t dim) {
   return t * (t + 1) / 2 * (int64_t)sizeof(int2) + 64;
 }
 
-CovPlan cov_i8_plan(int64_t dim, int64_t K) {
+CovPlan cov_i8_plan(int64_t dim, int64_t K, int64_t slab_budget) {
   CovPlan p;
   p.nst = cov_i8_kpad(K) / YK;
   const int64_t t = (dim + YT - 1) / YT;
@@ -391,11 +391,10 @@ CovPlan cov_i8_plan(int64_t dim, int64_t K) {
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (ncu < 1) ncu = 256;
-  // slab memory budget 8 GiB (8 splits at d = 16384); EF_COV_SLAB_BUDGET (bytes) overrides
-  // it, which the tests use to force the multi-pass schedule on small inputs
+  // slab memory budget (EF_OPT_COV_SLAB_BYTES, default 8 GiB = 8 splits at d = 16384); the
+  // tests lower it to force the multi-pass schedule on small inputs
   const int64_t slab = dim * dim * (int64_t)sizeof(int);
-  int64_t budget = (int64_t)8 << 30;
-  if (const char* env = getenv("EF_COV_SLAB_BUDGET")) budget = std::max<int64_t>(atoll(env), 1);
+  const int64_t budget = std::max<int64_t>(slab_budget, 1);
   int64_t smax = budget / std::max<int64_t>(slab, 1);
   smax = std::min<int64_t>(std::max<int64_t>(smax, 1), 64);
   const int64_t smin_total = (p.nst + kMaxSplitStages - 1) / kMaxSplitStages;

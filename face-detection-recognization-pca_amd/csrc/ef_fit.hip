@@ -69,10 +69,14 @@ struct Bufs {
 // EF_FIT_GEMM=own forces gemm64 everywhere (A/B comparisons).
 hipError_t dense_gemm(ef_ctx* c, hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
                       double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
+#ifdef EF_DIAGNOSTICS
   static const bool own = [] {
     const char* e = getenv("EF_FIT_GEMM");
     return e && std::string(e) == "own";
   }();
+#else
+  constexpr bool own = false;
+#endif
   // rocBLAS for large outputs; small outputs over long K (Y^T.Y, Q^T.Y) keep gemm64's
   // split-K (a 256 x 256 output is only 4 rocBLAS tiles)
   const bool small_out = M * N <= (int64_t)512 * 512 && K >= 4096;
@@ -97,7 +101,6 @@ hipError_t dense_gemm(ef_ctx* c, hipStream_t s, const Operand& A, const Operand&
 }
 
 constexpr int kMaxSweeps = 60;
-constexpr int kMaxIters = 500;
 constexpr int kDirectMax = 1024;                 // direct grid-Jacobi up to this order
 constexpr size_t kWorkElems = size_t(1) << 24;  // split-K slab budget (128 MiB)
 
@@ -256,7 +259,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   // rate); the iteration is self-correcting, and convergence is only declared between two
   // Rayleigh-Ritz steps that both follow fp64 products, so the result is the fp64 one.
   float *C32 = nullptr, *Q32 = nullptr, *Y32 = nullptr;
-  bool coarse = dim >= 4096 && c->blas != nullptr && !getenv("EF_FIT_NO_FP32");
+  bool coarse = dim >= 4096 && c->blas != nullptr && c->opt_fit_fp32_coarse != 0;
   if (coarse) {
     EF_TRY(B.get(c, (size_t)dim * dim, &C32));
     EF_TRY(B.get(c, (size_t)dim * m, &Q32));
@@ -266,7 +269,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   std::vector<double> th(m), prev(m, 0.0);
   bool have_prev = false, prev_fine = false;
   int it = 0;
-  for (it = 1; it <= kMaxIters; ++it) {
+  const int max_iters = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_fit_max_iters, 1 << 20));
+  bool converged = false;
+  double last_worst = 1.0;
+  for (it = 1; it <= max_iters; ++it) {
     const bool fine = !coarse;  // this iteration's product is fp64
     if (coarse) {
       cvt64to32(s, Q, dim * m, Q32);
@@ -281,7 +287,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
     // no iteration count), 8, then every rr_period(dim)
     const bool early = dim < 12288 && (it <= 2 || it == 4);
-    const bool rr = early || it == 8 || it % rr_period(dim) == 0 || it == kMaxIters;
+    const bool rr = early || it == 8 || it % rr_period(dim) == 0 || it == max_iters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
                            work, kWorkElems),
@@ -301,14 +307,22 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
         const double r = std::fabs(th[i] - prev[i]) / std::fmax(std::fabs(th[i]), 1e-300);
         if (r > worst) worst = r, wi = i;
       }
+#ifdef EF_DIAGNOSTICS
       if (getenv("EF_FIT_DEBUG"))
         fprintf(stderr, "[ef_fit] rr it=%d %s sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g\n", it,
                 fine ? "fp64" : "fp32", se.sweeps, worst, wi, th[kk - 1], th[m - 1]);
+#else
+      (void)wi;
+#endif
       if (coarse && worst < 1e-4) coarse = false;  // fp64 products from the next iteration on
       prev = th;
       have_prev = true;
       prev_fine = fine;
-      if (ok || it == kMaxIters) {
+      last_worst = worst;
+      converged = ok;
+      // the iteration cap ends the loop with EF_E_NUMERIC (useless/train.py has no cap:
+      // LAPACK either converges or raises LinAlgError; train-v4.py:114-120 returns False)
+      if (ok || it == max_iters) {
         EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
                              kk, work, kWorkElems),
                "U = Q.V");
@@ -324,11 +338,20 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     }
     EF_TRY(orthonormalise());
   }
-  if (it > kMaxIters) it = kMaxIters;
+  if (it > max_iters) it = max_iters;
+#ifdef EF_DIAGNOSTICS
   if (getenv("EF_FIT_DEBUG"))
     fprintf(stderr, "[ef_fit] wide dim=%lld k=%d m=%d iters=%d jacobi calls=%ld sweeps=%ld\n", (long long)dim, kk, m,
             it, se.calls, se.sweeps);
+#endif
   *iters = it;
+  if (!converged) {
+    char msg[160];
+    snprintf(msg, sizeof msg,
+             "eigensolver did not converge: %d subspace iterations, Ritz values still moving by %.3e (relative)",
+             it, last_worst);
+    return set_err(c, EF_E_NUMERIC, msg);
+  }
   return EF_OK;
 }
 
@@ -353,80 +376,19 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     return EF_OK;
   }
 
-  // Block subspace iteration of width m: Y = C.Q; G = Y^T.Y = W.L.W^T; Q = Y.W.L^-1/2
-  // (orthonormal, Ritz-ordered); k <= 80 keeps the historical m = kJacobiMax (LDS Jacobi),
-  // wider k uses m = 2k (even, <= dim) on the grid Jacobi.
   // Block width m = max(2k, 88) (Ritz values converge as (lambda_{m+1} / lambda_k)^2 per
   // iteration), even, <= dim: CholQR subspace iteration with periodic Rayleigh-Ritz.
   int64_t mm = std::max<int64_t>(2 * (int64_t)kk, kJacobiMax);
   mm = (mm + 7) / 8 * 8;
   if (mm > dim) mm = dim & ~int64_t(1);
   int m = (int)mm;
+#ifdef EF_DIAGNOSTICS
   if (const char* em = getenv("EF_FIT_M")) {  // experiments only
     const int64_t e = atoi(em);
     if (e >= kk + 2 && e <= dim) m = (int)(e & ~int64_t(1));
   }
-  const char* ep = getenv("EF_FIT_PATH");
-  if (!(ep && ep[0] == 'n')) return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
-  SmallEig se;
-  EF_TRY(se.init(c, B, m));
-  double *Q, *Y, *G, *Wm, *W2, *lam;
-  EF_TRY(B.get(c, (size_t)dim * m, &Q));
-  EF_TRY(B.get(c, (size_t)dim * m, &Y));
-  EF_TRY(B.get(c, (size_t)m * m, &G));
-  EF_TRY(B.get(c, (size_t)m * m, &Wm));
-  EF_TRY(B.get(c, (size_t)m * m, &W2));
-  EF_TRY(B.get(c, (size_t)m, &lam));
-  EF_HIP(c, launch_rand_init(s, Q, dim * m, 0x5eedULL), "rand init");
-
-  std::vector<double> th(m), prev(m, 0.0);
-  int stable = 0, it = 0;
-  for (it = 1; it <= kMaxIters; ++it) {
-    EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
-                     work, kWorkElems),
-           "Y = C.Q");
-    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
-                     kWorkElems),
-           "G = Y^T.Y");
-    EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(G)"));
-    EF_HIP(c, launch_scale_cols_rsqrt(s, Wm, m, m, lam, W2), "W.L^-1/2");
-    EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
-                     kWorkElems),
-           "Q = Y.W");
-    EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
-    EF_HIP(c, hipStreamSynchronize(s), "sync");
-    for (auto& t : th) t = std::sqrt(t > 0 ? t : 0.0);
-    // converged when every kept Ritz value is stable to 1e-13 relative (floor 1e-15 of
-    // the largest, for zero eigenvalues of rank-deficient data) twice in a row
-    bool ok = true;
-    for (int i = 0; i < kk; ++i) ok &= std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * th[i], 1e-15 * th[0]);
-    prev = th;
-    if (!(std::isfinite(th[0]))) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
-    if (it > 2 && ok) {
-      if (++stable >= 2) break;
-    } else {
-      stable = 0;
-    }
-  }
-  if (it > kMaxIters) it = kMaxIters;
-  if (getenv("EF_FIT_DEBUG"))
-    fprintf(stderr, "[ef_fit] dim=%lld k=%d m=%d iters=%d jacobi calls=%ld sweeps=%ld\n", (long long)dim, kk, m, it,
-            se.calls, se.sweeps);
-  // Rayleigh-Ritz on C itself: T = Q^T.C.Q, T = V.L.V^T, U = Q.V[:, :kk]
-  EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
-                   kWorkElems),
-         "Y = C.Q");
-  EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
-                   kWorkElems),
-         "T = Q^T.Y");
-  EF_TRY(se.solve(c, G, m, lam, Wm, m, "jacobi(T)"));
-  EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(Wm, m, false), dim, kk, m, 1.0, U_out, kk, work,
-                   kWorkElems),
-         "U = Q.V");
-  EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
-  EF_HIP(c, hipStreamSynchronize(s), "sync");
-  *iters = it;
-  return EF_OK;
+#endif
+  return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
 }
 
 }  // namespace
@@ -489,7 +451,7 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   // pixel scaling commutes with it (covariance path; Gram path without StandardScaler),
   // else the fp64 GEMM with the centring/scaling fused into the operand loads.
   if (int8_path) {
-    const CovPlan plan = cov_i8_plan(dim, gram ? d : n);
+    const CovPlan plan = cov_i8_plan(dim, gram ? d : n, c->opt_cov_slab_bytes);
     int* slabs;
     long long *S64 = nullptr, *cvec, *R;
     unsigned long long* Q2;
@@ -532,7 +494,12 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   // training projection A.E (projected_data / fit_transform output)
   if (proj_out) {
     EF_TRY(B.get(c, (size_t)n * kk, &proj));
-    if (proj_i8_supported(Xd, n, d, kk) && !getenv("EF_FIT_PROJ_F64")) {  // exact int8 digits (ef_proj_i8.hip)
+#ifdef EF_DIAGNOSTICS
+    const bool f64proj = getenv("EF_FIT_PROJ_F64") != nullptr;
+#else
+    constexpr bool f64proj = false;
+#endif
+    if (proj_i8_supported(Xd, n, d, kk) && !f64proj) {  // exact int8 digits (ef_proj_i8.hip)
       uint8_t* pw;
       EF_TRY(B.get(c, proj_i8_work_bytes(n, d, kk), &pw));
       EF_HIP(c, launch_proj_i8(s, Xd, n, d, mean, wp, En, kk, pw, proj), "F = A.E (int8 digits)");

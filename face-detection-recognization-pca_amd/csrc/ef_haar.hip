@@ -30,6 +30,7 @@
 // float (no contraction), times the float normalisation factor, compared with the stump
 // threshold; the stage sum accumulates the float leaves in double.
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -613,7 +614,7 @@ int ef_haar_set_cascade(ef_ctx* c, int32_t win_w, int32_t win_h, int32_t n_featu
   h->ww = win_w;
   h->wh = win_h;
   h->nstages = n_stages;
-  h->order_free = order_free && !getenv("EF_HAAR_ORDERED");
+  h->order_free = order_free && !c->opt_haar_ordered;
   EF_TRY(ensure(c, h->stages, st.size() * sizeof(HaarStage)));
   EF_HIP(c, hipMemcpy(h->stages.p, st.data(), st.size() * sizeof(HaarStage), hipMemcpyHostToDevice), "H2D stages");
   std::vector<HaarRec> rc((size_t)n_stumps);
@@ -693,7 +694,14 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
                                         " pyramid layers (scale factor too close to 1)");
   std::vector<int> row_start(nl + 1, 0);
   for (int i = 0; i < nl; ++i) row_start[i + 1] = row_start[i] + (layers[i].ny + layers[i].step - 1) / layers[i].step;
-  const int cap = 1 << 20;  // candidate / work-list capacity (windows surviving stage 0)
+  // candidate / work-list capacity: every window origin the invoker can visit (a 1080p
+  // frame at minSize 30 has ~3.5 M; a cascade whose stage 0 passes most of them must not
+  // overflow a fixed list)
+  int64_t visitable = 0;
+  for (const auto& ly : layers)
+    visitable += (int64_t)((ly.nx + ly.step - 1) / ly.step) * ((ly.ny + ly.step - 1) / ly.step);
+  if (visitable > INT_MAX / 2) return set_err(c, EF_E_INVALID, "ef_haar_detect: frame too large");
+  const int cap = (int)std::max<int64_t>(visitable, 1024);
   EF_TRY(ensure(c, h->pix, pix));
   EF_TRY(ensure(c, h->ii1, ii * 4));
   EF_TRY(ensure(c, h->ii2, ii * 4));
@@ -767,6 +775,7 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   // more than a launch and a compaction.
   static const std::vector<int> groups = [] {
     std::vector<int> g;
+#ifdef EF_DIAGNOSTICS
     if (const char* e = getenv("EF_HAAR_GROUPS")) {
       for (const char* p = e; *p;) {
         const int v = atoi(p);
@@ -775,6 +784,7 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
         if (*p == ',') ++p;
       }
     }
+#endif
     if (g.empty() || g[0] != 1) g = {1, 4, 8, 14};
     g.push_back(1 << 30);
     return g;
@@ -782,15 +792,16 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   // every group takes the split form when the cascade's stage sums are order-free
   // (measured, 640x480 synthetic frontal cascade with LDS stump records and 8 waves: split
   // from group 1 0.637 ms, from stage 3 0.652, from stage 6 0.673 per frame)
-  static const int kHaarSplitFrom = [] {  // first stage group run in split form (EF_HAAR_SPLIT_FROM: experiments)
-    const char* e = getenv("EF_HAAR_SPLIT_FROM");
-    return e ? atoi(e) : 1;
-  }();
-  static const int split_waves = [] {  // EF_HAAR_SPLITW: waves per split workgroup (experiments)
+#ifdef EF_DIAGNOSTICS  // experiments: first split-form stage group, waves per split workgroup
+  static const int kHaarSplitFrom = [] { const char* e = getenv("EF_HAAR_SPLIT_FROM"); return e ? atoi(e) : 1; }();
+  static const int split_waves = [] {
     const char* e = getenv("EF_HAAR_SPLITW");
     const int v = e ? atoi(e) : 8;
     return v == 4 || v == 16 ? v : 8;
   }();
+#else
+  constexpr int kHaarSplitFrom = 1, split_waves = 8;
+#endif
   int gi = 0;
   const int live = hc[0];  // upper bound of every group's input
   HaarCand* bin = work;
@@ -817,11 +828,13 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
   EF_HIP(c, hipGetLastError(), "haar kernels");
   EF_HIP(c, hipMemcpyAsync(hc, cnt, 16 * sizeof(int), hipMemcpyDeviceToHost, s), "D2H counts");
   EF_HIP(c, hipStreamSynchronize(s), "sync");
+#ifdef EF_DIAGNOSTICS
   if (getenv("EF_HAAR_DEBUG")) {
     fprintf(stderr, "[ef_haar] stage-group inputs:");
     for (int g = 0; g <= gi; ++g) fprintf(stderr, " %d", hc[g]);
     fprintf(stderr, "\n");
   }
+#endif
   hc[1] = hc[gi];  // survivors of the last group (all of stage 0's when the cascade has 1 stage)
   cand = bin;
   if (hc[1] > cap) return set_err(c, EF_E_INVALID, "ef_haar_detect: candidate capacity exceeded");

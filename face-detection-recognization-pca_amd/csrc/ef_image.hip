@@ -681,7 +681,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
   t->W = frame_w;
   t->nprob = n_problems;
   t->pitch = rup((int64_t)frame_w + 256, 64);
-  t->ii64 = getenv("EF_TM_II64") != nullptr;
+  t->ii64 = c->opt_tm_int64 != 0;
   const bool dev = flags & EF_MEM_DEVICE;
 
   int64_t raw_bytes = 0;

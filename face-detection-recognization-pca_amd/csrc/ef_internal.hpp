@@ -42,6 +42,7 @@ struct SearchWs {
   float* thr;           // [bpad] fp32 score threshold of each slot
   int* cand;            // [bpad][kCandMax] candidate rows
   int* cand_cnt;        // [bpad]
+  ef_match* match;      // [b] exact merge records (fp64 winner score), may be null
 };
 
 struct SearchPlan {
@@ -66,6 +67,12 @@ struct TimerEvt {
 
 struct ef_ctx {
   int device = 0;
+  // tunables set with ef_set_option (include/eigenface.h EF_OPT_*)
+  int64_t opt_fit_max_iters = 500;
+  int64_t opt_fit_fp32_coarse = 1;
+  int64_t opt_cov_slab_bytes = (int64_t)8 << 30;
+  int64_t opt_tm_int64 = 0;
+  int64_t opt_haar_ordered = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -103,6 +110,13 @@ struct ef_ctx {
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
   void* blas = nullptr;  // rocBLAS handle (fit's plain dense products), lazily created
 
+  // multi-GPU: RCCL communicator (ef_comm_init), null when single-rank
+  void* comm = nullptr;
+  int comm_size = 1, comm_rank = 0;
+  ef::DevBuf match_local;  // ef_match[b] this rank's records
+  ef::DevBuf match_all;    // ef_match[comm_size][b] gathered records
+  ef::DevBuf q_local;      // float[cpad][kp] this rank's slice of the projected probes
+
   bool timing = false;
   std::vector<ef::TimerEvt> pending;
   double t_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -126,7 +140,13 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp);
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
                          int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
                          float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
-hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b);
+hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b, ef_match* match);
+// keys[b] (+ merged[b]) <- exact arg-best over parts x b match records (ef_comm.hip)
+hipError_t launch_matches_merge(hipStream_t s, const ef_match* parts, int nparts, int64_t b, long long* keys,
+                                ef_match* merged);
+void comm_release(ef_ctx* c);
+// all-gather over the attached communicator on ctx->stream (bytes per rank)
+int comm_allgather(ef_ctx* c, const void* send, void* recv, size_t bytes_per_rank);
 hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,
                            float* dst, int kp);
 hipError_t launch_gallery_aux(hipStream_t s, const float* G, int64_t n, int kp, float* gnorm2,

@@ -98,7 +98,7 @@ struct CovPlan {
 };
 int64_t cov_i8_kpad(int64_t K);
 int64_t cov_i8_order_bytes(int64_t dim);  // device scratch for the tile order list
-CovPlan cov_i8_plan(int64_t dim, int64_t K);
+CovPlan cov_i8_plan(int64_t dim, int64_t K, int64_t slab_budget);
 bool cov_i8_fused_stats(const uint8_t* X, int64_t d);  // covariance-path prep can produce S1/S2
 // Gram path: At = X' (K = d).  Covariance path: At = X'^T (K = n); with S1/S2 non-null
 // (requires cov_i8_fused_stats) also S1 += sum x, S2 += sum x^2 per pixel.

@@ -364,7 +364,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
     kmin = o < kmin ? o : kmin;
   }
   if (kmin == LLONG_MAX) {  // empty gallery
-    if (lane == 0) keys[p] = LLONG_MAX;
+    if (lane == 0) {
+      keys[p] = LLONG_MAX;
+      if (ws.match) ws.match[p] = ef_match{__builtin_inf(), 0.0, LLONG_MAX};
+    }
     return;
   }
   float r2 = __builtin_inff();
@@ -396,8 +399,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
     delta = 2.f * ((KP + 8) * u * 1.01f * qn) + 1e-30f;
   }
   delta *= 2.f;  // safety factor
+  double qq64 = 0.0;  // tie-tolerance scale of the fp64 resolution (resolve_kernel)
+  if (METRIC == EF_METRIC_L2 && ws.match) {
+    for (int c = lane; c < KP; c += 64) qq64 = fma((double)q[c], (double)q[c], qq64);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) qq64 += __shfl_xor(qq64, off);
+  }
   if (lane == 0) {
     keys[p] = pack_key((float)v, (unsigned)(row + g_offset));
+    if (ws.match)
+      ws.match[p] = ef_match{v, METRIC == EF_METRIC_L2 ? qq64 + (double)gmax2 : 1.0,
+                             pack_key((float)v, (unsigned)(row + g_offset))};
     if (r2 - b1 <= delta) {
       const int slot = atomicAdd(ws.amb_count, 1);
       ws.amb_list[slot] = (int)p;
@@ -440,7 +452,14 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
     const double v = score64<KP, METRIC>(q, G + r * KP, lane);
     if (v <= vmin + tol && r < best_row) { best_row = r; best_v = v; }
   }
-  if (lane == 0 && best_row != LLONG_MAX) keys[p] = pack_key((float)best_v, (unsigned)(best_row + g_offset));
+  if (lane == 0 && best_row != LLONG_MAX) {
+    const long long key = pack_key((float)best_v, (unsigned)(best_row + g_offset));
+    keys[p] = key;
+    if (ws.match) {
+      ws.match[p].score = best_v;
+      ws.match[p].key = key;
+    }
+  }
 }
 
 // dst[rows_pad][kp] <- src[rows][k] with zero padding.
@@ -499,7 +518,11 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
   // workgroup that starts at launch, so there is no tail round (measured: 90.1 % vs 89.6 %
   // at 1M rows, 82 % vs 80.5 % at 125k rows for 2048); the chunk count is a multiple of 8
   // so the XCD remap is a bijection.  EF_SEARCH_WGS overrides (experiments).
+#ifdef EF_DIAGNOSTICS
   static const int64_t target = [] { const char* e = getenv("EF_SEARCH_WGS"); return e ? atoll(e) : 512; }();
+#else
+  constexpr int64_t target = 512;
+#endif
   int64_t want = (target + pl.n_ptiles - 1) / pl.n_ptiles;
   if (want > tiles) want = tiles;
   if (want < 1) want = 1;
@@ -534,11 +557,17 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
     const hipError_t e = launch_search_wide(s, KP, M, false, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
+#ifdef EF_DIAGNOSTICS
   static const int abl = [] { const char* e = getenv("EF_SEARCH_ABL"); return e ? atoi(e) : 0; }();
-  if (KP == 128 && M == EF_METRIC_L2 && abl > 0) {  // diagnostic ablations (timing only)
+#else
+  constexpr int abl = 0;
+#endif
+  if (KP == 128 && M == EF_METRIC_L2 && abl > 0) {  // diagnostic build only: ablations (timing, wrong results)
+#ifdef EF_DIAGNOSTICS
     auto k = abl == 1 ? search_kernel<KP, M, false, 1> : abl == 4 ? search_kernel<KP, M, false, 4>
                                                                    : search_kernel<KP, M, false, 5>;
     hipLaunchKernelGGL(k, grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles, pl.tiles_per_chunk, bpad, ws);
+#endif
   } else {
     hipLaunchKernelGGL((search_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, bpad, ws);
@@ -589,13 +618,16 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
 #undef EF_SEARCH_CASE
 }
 
-__global__ void keys_fill_kernel(long long* keys, int64_t b) {
+__global__ void keys_fill_kernel(long long* keys, int64_t b, ef_match* match) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < b) keys[i] = LLONG_MAX;
+  if (i < b) {
+    keys[i] = LLONG_MAX;
+    if (match) match[i] = ef_match{__builtin_inf(), 0.0, LLONG_MAX};
+  }
 }
 
-hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b) {
-  hipLaunchKernelGGL(keys_fill_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, s, keys, b);
+hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b, ef_match* match) {
+  hipLaunchKernelGGL(keys_fill_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, s, keys, b, match);
   return hipGetLastError();
 }
 

@@ -5,17 +5,21 @@ Drop-in for the PCA / recognition hot path of saladbkp/face-detection-recognizat
 hand-written gfx950 HIP kernels in ``_lib/libeigenface.so`` (no CPU fallback).
 """
 from ._native import EigenfaceError, NativeLibraryError, LIB_PATH  # noqa: F401
-from .engine import Engine, FitResult, decode_keys, device_count  # noqa: F401
+from .engine import Engine, FitResult, decode_keys, device_count, merge_matches_host  # noqa: F401
 from .pca import (  # noqa: F401
     EigenfacePCA,
     get_engine,
     manual_pca,
     recognize_face,
+    recognize_face_dual_model,
     recognize_face_with_model,
+    recognize_faces,
+    recognize_faces_dual_model,
 )
 
 __all__ = [
     "Engine", "FitResult", "decode_keys", "device_count", "EigenfacePCA", "get_engine",
-    "manual_pca", "recognize_face", "recognize_face_with_model", "EigenfaceError",
+    "manual_pca", "recognize_face", "recognize_face_with_model", "recognize_faces",
+    "recognize_face_dual_model", "recognize_faces_dual_model", "merge_matches_host", "EigenfaceError",
     "NativeLibraryError", "LIB_PATH",
 ]

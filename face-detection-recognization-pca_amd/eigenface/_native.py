@@ -23,6 +23,19 @@ EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
 EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR = 0, 1, 2, 3, 4
 EF_KEY_NONE = (1 << 63) - 1
+EF_UNIQUE_ID_BYTES = 128
+EF_OPT_FIT_MAX_ITERS, EF_OPT_FIT_FP32_COARSE, EF_OPT_COV_SLAB_BYTES, EF_OPT_TM_INT64_SUMS, EF_OPT_HAAR_ORDERED = \
+    1, 2, 3, 4, 5
+EF_E_NUMERIC = -5
+
+
+class ef_match(C.Structure):
+    """include/eigenface.h ef_match: fp64 winner score, tie-tolerance scale, packed key."""
+    _fields_ = [("score", C.c_double), ("scale", C.c_double), ("key", C.c_int64)]
+
+
+# numpy view of an ef_match array
+MATCH_DTYPE = [("score", "<f8"), ("scale", "<f8"), ("key", "<i8")]
 
 _ERRNAMES = {-1: "EF_E_INVALID", -2: "EF_E_HIP", -3: "EF_E_STATE", -4: "EF_E_NOMEM", -5: "EF_E_NUMERIC"}
 
@@ -59,6 +72,15 @@ _SIGS = {
     "ef_search": ([vp, vp, i64, i32, vp, u32], C.c_int),
     "ef_recognize": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
     "ef_keys_decode": ([vp, i64, i32, vp, vp], None),
+    "ef_search_matches": ([vp, vp, i64, i32, vp, u32], C.c_int),
+    "ef_recognize_matches": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
+    "ef_matches_merge": ([vp, vp, i32, i64, vp, vp, u32], C.c_int),
+    "ef_comm_unique_id": ([vp], C.c_int),
+    "ef_comm_init": ([vp, i32, i32, vp], C.c_int),
+    "ef_comm_destroy": ([vp], C.c_int),
+    "ef_comm_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+    "ef_set_option": ([vp, i32, i64], C.c_int),
+    "ef_get_option": ([vp, i32, C.POINTER(i64)], C.c_int),
     "ef_preprocess": ([vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, u32], C.c_int),
     "ef_tm_prepare": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, u32], C.c_int),
     "ef_tm_match": ([vp, vp, i64, vp, vp, vp, vp, u32], C.c_int),
@@ -94,7 +116,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 1:
+        if h.ef_api_version() != 2:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

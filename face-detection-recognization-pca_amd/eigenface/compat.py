@@ -25,7 +25,8 @@ from datetime import datetime
 
 import numpy as np
 
-from .pca import EigenfacePCA, get_engine
+from ._native import EigenfaceError
+from .pca import EigenfacePCA, _model_engine, get_engine
 
 
 # ----------------------------------------------------------------------- images
@@ -183,7 +184,11 @@ class FaceTrainer:
         if len(self.face_labels) == 0:
             print("Error: No face labels assigned!")
             return False
-        m = EigenfacePCA(self.n_components, standardize=True, device=self.device).fit(self.face_images)
+        try:
+            m = EigenfacePCA(self.n_components, standardize=True, device=self.device).fit(self.face_images)
+        except EigenfaceError as e:  # e.g. EF_E_NUMERIC: eigensolver did not converge
+            print(f"Error: PCA training failed: {e}")
+            return False
         self.model = m
         self.mean_face = m.mean_face_
         self.scaler, self.pca = sklearn_objects(m)
@@ -326,33 +331,150 @@ def _model_projection(md):
     return mu.astype(np.float32), np.ascontiguousarray(w, dtype=np.float32)
 
 
+_fold_cache: dict = {}
+
+
+def _folded(md):
+    """(mean, W) of a model dict, folded once per model (the cache keeps the dict and the
+    estimator arrays it was folded from, so a replaced or refitted estimator re-folds)."""
+    pca = md.get("pca", md.get("pca_model"))
+    sc = md["scaler"]
+    src = (pca.components_, pca.mean_, sc.mean_, sc.scale_)
+    hit = _fold_cache.get(id(md))
+    if hit is not None and hit[0] is md and all(x is y for x, y in zip(hit[1], src)):
+        return hit[2], hit[3]
+    mu, w = _model_projection(md)
+    if len(_fold_cache) > 64:
+        _fold_cache.clear()
+    _fold_cache[id(md)] = (md, src, mu, w)
+    return mu, w
+
+
+def preprocess_faces(face_imgs, device=0):
+    """Grey 64x64 rows of a batch of face crops (scan-template-v4.py:257-263): one GPU
+    launch (ef_preprocess) for the whole batch."""
+    return get_engine(device).preprocess([np.asarray(f, dtype=np.uint8) for f in face_imgs], (64, 64))
+
+
+def extract_faces_features(face_rows, model_data, device=0):
+    """scan-template-v4.py:253-268 for a batch: ``face_rows`` (b, 4096) uint8 from
+    :func:`preprocess_faces` -> (b, k) features (one projection launch)."""
+    mu, w = _folded(model_data)
+    eng = _model_engine(mu, w, device)
+    return eng.project(np.asarray(face_rows)).astype(np.float64)
+
+
 def extract_face_features(face_img, model_data, device=0):
-    """scan-template-v4.py:253-268 on the GPU: grey 64x64 face -> model features."""
-    eng = get_engine(device)
-    g = eng.preprocess([np.asarray(face_img, dtype=np.uint8)], (64, 64))  # grey + resize on the GPU
-    mu, w = _model_projection(model_data)
-    eng.set_model(mu, w)
-    return eng.project(g)[0].astype(np.float64)
+    """scan-template-v4.py:253-268 on the GPU: grey face crop -> model features."""
+    return extract_faces_features(preprocess_faces([face_img], device), model_data, device)[0]
 
 
-def recognize_face_all_models(face_img, models, threshold=0.8, device=0):
-    """Best match over per-person models (scan-template-v4.py:289-319): strict '>' over
-    models in iteration order, recognised name or the model's person name."""
-    from .pca import recognize_face_with_model
+def recognize_faces_all_models(face_imgs, models, threshold=0.8, device=0):
+    """recognize_face_all_models (scan-template-v4.py:289-319) for every detection of a
+    frame at once: the crops are preprocessed in one launch, then per model one projection
+    and one cosine search over all of them.  Per face: strict '>' over models in
+    iteration order, the recognised name or the model's person name; (-1, "unknown", 0.0)
+    when no model scores above 0."""
+    from .pca import _gallery_engine
 
-    best = None
-    best_conf = 0.0
+    n = len(face_imgs)
+    best = [None] * n
+    best_conf = np.zeros(n)
+    if n == 0:
+        return []
+    rows = preprocess_faces(face_imgs, device)
     for person_name, info in models.items():
         md = info["model_data"] if "model_data" in info else info
         if md is None:
             continue
         try:
-            f = extract_face_features(face_img, md, device)
-            pid, name, conf = recognize_face_with_model(f, md, threshold, device)
+            f = extract_faces_features(rows, md, device)
+            eng = _gallery_engine(md["face_features"], device)
+            idx, sim = eng.search(f.astype(np.float32), "cosine")
         except Exception as e:  # reference: print and continue (:312-314)
             print(f"Error recognizing with model {person_name}: {e}")
             continue
-        if conf > best_conf:
-            best_conf = conf
-            best = (pid, name if name != "unknown" else person_name, conf)
-    return best if best else (-1, "unknown", 0.0)
+        labels, pmap = md["face_labels"], md["person_id_map"]
+        for i in range(n):
+            conf = float(sim[i])
+            if not conf > best_conf[i]:
+                continue
+            pid, name = -1, "unknown"
+            if idx[i] >= 0 and conf >= threshold:  # recognize_face_with_model (:278-284)
+                pid = labels[idx[i]]
+                for nm, v in pmap.items():
+                    if v == pid:
+                        name = nm
+                        break
+            best_conf[i] = conf
+            best[i] = (pid, name if name != "unknown" else person_name, conf)
+    return [b if b else (-1, "unknown", 0.0) for b in best]
+
+
+def recognize_face_all_models(face_img, models, threshold=0.8, device=0):
+    """Best match over per-person models for one face (scan-template-v4.py:289-319)."""
+    return recognize_faces_all_models([face_img], models, threshold, device)[0]
+
+
+def load_all_models(root="."):
+    """``MultiModelFaceScanner.load_all_models`` (scan-template-v4.py:17-74): every
+    ``faces/lock_version/*/face_model.pkl`` under ``root`` (glob order, sorted here for
+    determinism), keyed by the person directory name, each entry
+    ``{model_data, detection_data, template_images, model_path}`` with up to 5 templates
+    ``{image (grey, IMREAD_GRAYSCALE), width, height}`` from the first faces of
+    ``{person}_faces_detection.json`` whose ``image_path`` exists (:48-58).  Models that
+    fail to load are reported and skipped (:70-71).  Pickles execute code when loaded:
+    only load model files you trust."""
+    import glob
+
+    models = {}
+    pattern = os.path.join(root, "faces", "lock_version", "*", "face_model.pkl")
+    paths = sorted(glob.glob(pattern))
+    if not paths:
+        print(f"No models found matching pattern: {pattern}")
+        return models
+    print(f"Found {len(paths)} model(s):")
+    for model_path in paths:
+        person_name = os.path.basename(os.path.dirname(model_path))
+        try:
+            with open(model_path, "rb") as f:
+                md = pickle.load(f)
+            json_path = os.path.join(os.path.dirname(model_path), f"{person_name}_faces_detection.json")
+            det = None
+            if os.path.exists(json_path):
+                with open(json_path, "r", encoding="utf-8") as f:
+                    det = json.load(f)
+            templates = []
+            if det and det.get("faces"):
+                for face in det["faces"][:5]:
+                    path = face["image_path"]
+                    if os.path.exists(path):
+                        img = decode_gray(path)
+                        if img is not None:
+                            templates.append({"image": img, "width": face["width"], "height": face["height"]})
+            models[person_name] = {"model_data": md, "detection_data": det, "template_images": templates,
+                                   "model_path": model_path}
+            print(f"  - {person_name}: {len(md['face_features']) if md else 0} faces")
+        except Exception as e:  # noqa: BLE001 - the reference prints and continues
+            print(f"  - Failed to load {person_name}: {e}")
+    print(f"Successfully loaded {len(models)} model(s)")
+    return models
+
+
+def decode_gray(path):
+    """cv2.imread(path, IMREAD_GRAYSCALE): libjpeg's grey output (OpenCV when importable,
+    else Pillow's draft('L') — the decode pinned by the reference models' EVR); None if
+    unreadable."""
+    try:
+        import cv2
+    except ImportError:
+        cv2 = None
+    if cv2 is not None:
+        return cv2.imread(path, cv2.IMREAD_GRAYSCALE)
+    try:
+        from PIL import Image
+        im = Image.open(path)
+        im.draft("L", im.size)
+        return np.asarray(im.convert("L"), dtype=np.uint8)
+    except (OSError, ValueError):
+        return None

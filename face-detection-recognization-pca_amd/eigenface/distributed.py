@@ -1,21 +1,31 @@
 """Gallery row sharding across GPUs (one process per GPU, torch.distributed).
 
-Rank r owns gallery rows [lo_r, hi_r) and searches them with global row offsets, so
-its per-probe packed key (order-preserving score << 32 | global row) is directly
-comparable with every other rank's.  One all-reduce(MIN) over the B int64 keys (RCCL
-over xGMI with backend "nccl"; gloo on CPU) yields the global arg-best with the
-lowest-index tie-break.  The projection model is replicated; the
-probe batch's projection is split by rows across ranks and the (B x k) fp32 features
-are all-gathered (2 MiB at B = 4096, k = 128), so no rank repeats another's projection
-work — at 8 ranks a replicated projection would be ~20 % of each rank's step.
+Rank r owns gallery rows [lo_r, hi_r) and searches them with global row offsets.  Its
+search returns one *match record* per probe (include/eigenface.h ``ef_match``: the
+winner's fp64 score, the tie-tolerance scale and the packed key), and one all-gather of
+the records (24 B per probe and rank: 96 KiB per rank at B = 4096 — latency-bound; RCCL
+over xGMI with backend "nccl", gloo on CPU) lets every rank merge them exactly with
+``ef_matches_merge``: the lowest global index among the ranks whose fp64 score is within
+1e-12 of the best.  A MIN over the packed fp32 keys alone would order two ranks' winners
+only to fp32 resolution and break sub-ulp differences by index; the fp64 record makes the
+sharded arg-best equal the single-engine one.
+
+The projection model is replicated; the probe batch's projection is split by rows across
+ranks and the (B x k) fp32 features are all-gathered (2 MiB at B = 4096, k = 128), so no
+rank repeats another's projection work.
+
+The same exchange also exists inside the library (``Engine.comm_init`` /
+``ef_comm_init``: RCCL driven from C, for callers of the C ABI); this module is the
+torch.distributed form.
 
 This is the logical analogue of recognize_face_all_models' best-over-models loop
-(scan-template-v4.py:297-319), made exact: a MIN over keys instead of a strict '>'
-scan, so the result does not depend on shard order.
+(scan-template-v4.py:297-319), made exact and independent of shard order.
 """
 from __future__ import annotations
 
 import numpy as np
+
+from . import _native as N
 
 
 def shard_range(n_total: int, rank: int, world: int):
@@ -32,14 +42,36 @@ def pack_keys(values, idx):
     return (s << 32) | (np.asarray(idx, dtype=np.int64) & 0xFFFFFFFF)
 
 
+def make_matches(score, scale, idx):
+    """Host match records (N.MATCH_DTYPE) from fp64 scores (L2 squared distance or
+    -cosine; +inf = no row), tie scales and global row indices."""
+    score = np.asarray(score, dtype=np.float64)
+    m = np.empty(score.shape[0], dtype=N.MATCH_DTYPE)
+    m["score"] = score
+    m["scale"] = scale
+    fin = np.isfinite(score)
+    keys = pack_keys(np.where(fin, score, 0.0).astype(np.float32), idx)
+    m["key"] = np.where(fin, keys, N.EF_KEY_NONE)
+    return m
+
+
+def _as_records_tensor(m):
+    """(b, 3) int64 tensor view of match records (numpy structured array or tensor)."""
+    import torch
+    if isinstance(m, torch.Tensor):
+        return m
+    a = np.ascontiguousarray(m, dtype=N.MATCH_DTYPE)
+    return torch.from_numpy(a.view(np.int64).reshape(-1, 3).copy())
+
+
 class ShardedGallery:
     """One rank's shard of a row-partitioned gallery.
 
-    ``local_search(Q, metric) -> int64 keys`` defaults to the rank's
-    :class:`eigenface.Engine` (device tensors in, device keys out)."""
+    ``local_matches(Q, metric) -> match records`` defaults to the rank's
+    :class:`eigenface.Engine` (device tensors in, a (b, 3) int64 device tensor out)."""
 
     def __init__(self, engine, gallery_local, n_total: int, rank: int, world: int, group=None,
-                 local_search=None, local_project=None):
+                 local_matches=None, local_project=None):
         self.rank, self.world, self.n_total, self.group = rank, world, n_total, group
         self.lo, self.hi = shard_range(n_total, rank, world)
         if gallery_local is not None and len(gallery_local) != self.hi - self.lo:
@@ -47,33 +79,46 @@ class ShardedGallery:
         self.engine = engine
         if engine is not None and gallery_local is not None:
             engine.set_gallery(gallery_local, global_offset=self.lo)
-        self._local = local_search or (lambda q, m, keys=None: engine.search_keys(q, m, keys=keys))
+        self._local = local_matches or (lambda q, m: engine.search_matches(q, m))
         self._project = local_project or (lambda p, out=None: engine.project(p, out=out))
         self._fbuf = {}
+        self._rbuf = {}
 
-    def _allreduce_min(self, k):
+    # ---------------------------------------------------------------- exchange
+    def _gather_merge(self, rec, b, keys=None):
+        """All-gather every rank's records and merge them exactly -> int64 keys[b]."""
         import torch
         import torch.distributed as dist
 
+        rec = _as_records_tensor(rec)
         if self.world == 1:
-            return k
-        if not isinstance(k, torch.Tensor):
-            k = torch.from_numpy(np.ascontiguousarray(k))
-        if k.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: reduce on host
-            h = k.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.MIN, group=self.group)
-            k.copy_(h)
-        else:  # RCCL over xGMI, stream-ordered on torch's current stream
-            dist.all_reduce(k, op=dist.ReduceOp.MIN, group=self.group)
-        return k
+            parts = rec
+        else:
+            key = (b, str(rec.device))
+            if key not in self._rbuf:
+                self._rbuf[key] = torch.empty((self.world * b, 3), dtype=torch.int64, device=rec.device)
+            parts = self._rbuf[key]
+            if rec.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: gather on host
+                chunks = [torch.empty((b, 3), dtype=torch.int64) for _ in range(self.world)]
+                dist.all_gather(chunks, rec.cpu(), group=self.group)
+                parts.copy_(torch.cat(chunks))
+            elif rec.is_cuda:  # RCCL over xGMI, stream-ordered on torch's current stream
+                dist.all_gather_into_tensor(parts, rec, group=self.group)
+            else:
+                dist.all_gather(list(parts.chunk(self.world)), rec, group=self.group)
+        if parts.is_cuda and self.engine is not None:
+            return self.engine.merge_matches(parts, b, keys)
+        from .engine import merge_matches_host
+        out = torch.from_numpy(merge_matches_host(parts.cpu().numpy(), b))
+        if keys is not None:
+            keys.copy_(out)
+            return keys
+        return out
 
     def search_keys(self, Q, metric="l2", keys=None):
-        import torch
-
-        k = self._local(Q, metric, keys=keys) if keys is not None else self._local(Q, metric)
-        if not isinstance(k, torch.Tensor):
-            k = torch.from_numpy(np.ascontiguousarray(k))
-        return self._allreduce_min(k)
+        """Global packed keys of the best row per probe (all ranks get the same keys)."""
+        b = int(Q.shape[0])
+        return self._gather_merge(self._local(Q, metric), b, keys)
 
     def _allgather_rows(self, loc, out):
         """out[(world*c), k] <- concat over ranks of loc[c, k] (rank order)."""
@@ -122,15 +167,13 @@ class ShardedGallery:
         return full[:b]
 
     def recognize_keys(self, P, metric="l2", keys=None, shard_projection=True):
-        """Projection + local search + all-reduce.  world > 1 with a device (or CPU
-        tensor) batch: the projection is split across ranks (project_sharded);
-        otherwise the engine's fused ef_recognize runs the whole batch."""
+        """Projection + local search + exact merge.  world > 1 with a device (or CPU
+        tensor) batch: the projection is split across ranks (project_sharded); otherwise
+        the engine's fused ef_recognize_matches runs the whole batch."""
         import torch
 
+        b = int(P.shape[0])
         if self.world == 1 or not shard_projection or not isinstance(P, torch.Tensor):
-            return self._allreduce_min(self.engine.recognize_keys(P, metric, keys=keys))
+            return self._gather_merge(self.engine.recognize_matches(P, metric), b, keys)
         q = self.project_sharded(P)
-        k = self._local(q, metric, keys=keys) if keys is not None else self._local(q, metric)
-        if not isinstance(k, torch.Tensor):
-            k = torch.from_numpy(np.ascontiguousarray(k))
-        return self._allreduce_min(k)
+        return self._gather_merge(self._local(q, metric), b, keys)

@@ -33,6 +33,15 @@ def _dev(x, torch_dtype):
     return x, x.data_ptr()
 
 
+_OPTIONS = {"fit_max_iters": N.EF_OPT_FIT_MAX_ITERS, "fit_fp32_coarse": N.EF_OPT_FIT_FP32_COARSE,
+            "cov_slab_bytes": N.EF_OPT_COV_SLAB_BYTES, "tm_int64_sums": N.EF_OPT_TM_INT64_SUMS,
+            "haar_ordered": N.EF_OPT_HAAR_ORDERED}
+
+
+def _option(o):
+    return _OPTIONS[o] if isinstance(o, str) else int(o)
+
+
 def _metric(m):
     if isinstance(m, str):
         return METRICS[m.lower()]
@@ -77,6 +86,11 @@ class Engine:
         self.model_d = None
         self.gallery_n = 0
         self.gallery_k = None
+        # Owner tokens of the resident model / gallery: whoever uploads them last owns them.
+        # Callers that cache "my model is resident" (EigenfacePCA, recognize_face_with_model)
+        # compare their token with these instead of assuming nobody else replaced it.
+        self.model_owner = None
+        self.gallery_owner = None
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -114,6 +128,42 @@ class Engine:
     def trim(self):
         """Free the fit workspaces the context keeps between fits (ef_trim)."""
         self._chk(self._lib.ef_trim(self._h))
+
+    def set_option(self, option, value):
+        """Context tunable (include/eigenface.h EF_OPT_*): "fit_max_iters",
+        "fit_fp32_coarse", "cov_slab_bytes", "tm_int64_sums", "haar_ordered" or the code."""
+        self._chk(self._lib.ef_set_option(self._h, _option(option), int(value)))
+
+    def get_option(self, option):
+        v = C.c_int64(0)
+        self._chk(self._lib.ef_get_option(self._h, _option(option), C.byref(v)))
+        return int(v.value)
+
+    # --------------------------------------------------------------- multi-GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """A fresh RCCL unique id (rank 0 creates it; broadcast it to the other ranks)."""
+        buf = C.create_string_buffer(N.EF_UNIQUE_ID_BYTES)
+        rc = N.lib().ef_comm_unique_id(buf)
+        if rc != N.EF_OK:
+            raise N.EigenfaceError(rc, "ef_comm_unique_id failed (RCCL unavailable?)")
+        return bytes(buf.raw)
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        """Attach an in-library RCCL communicator (ef_comm_init): from now on search /
+        recognize return the global result over the row-sharded gallery."""
+        if len(unique_id) != N.EF_UNIQUE_ID_BYTES:
+            raise ValueError("unique_id must be EF_UNIQUE_ID_BYTES bytes")
+        buf = C.create_string_buffer(bytes(unique_id), N.EF_UNIQUE_ID_BYTES)
+        self._chk(self._lib.ef_comm_init(self._h, int(nranks), int(rank), buf))
+
+    def comm_destroy(self):
+        self._chk(self._lib.ef_comm_destroy(self._h))
+
+    def comm_info(self):
+        n, r = C.c_int32(0), C.c_int32(0)
+        self._chk(self._lib.ef_comm_info(self._h, C.byref(n), C.byref(r)))
+        return int(n.value), int(r.value)
 
     # ------------------------------------------------------------------------ fit
     def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
@@ -159,7 +209,7 @@ class Engine:
         return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
 
     # ----------------------------------------------------------------- projection
-    def set_model(self, mean, W, precision="fp32"):
+    def set_model(self, mean, W, precision="fp32", owner=None):
         """Resident recognition model f = (p - mean) . W, W is d x k (k <= 512).
 
         precision="bf16" projects on bf16 MFMA (BASELINE.json config 5):
@@ -181,21 +231,39 @@ class Engine:
             raise ValueError("mean and W disagree on d")
         if precision == "bf16":
             flags |= N.EF_MODEL_BF16
+        self.model_owner = None  # a failed upload leaves no valid owner
         self._chk(self._lib.ef_model_set(self._h, mp, wp, d, k, flags))
         if flags:
             self.synchronize()
         self.model_d, self.model_k = int(d), int(k)
+        self.model_owner = owner if owner is not None else object()
+
+    def _dev_pixels(self, P):
+        """Validated device probe pixels: (b, model_d) uint8 or float32, contiguous."""
+        import torch
+        if P.dtype not in (torch.uint8, torch.float32):
+            raise TypeError(f"probe pixels must be uint8 or float32, got {P.dtype}")
+        if P.ndim != 2 or P.shape[1] != self.model_d:
+            raise ValueError(f"P must be (b, {self.model_d}), got {tuple(P.shape)}")
+        p, pp = _dev(P, P.dtype)
+        return p, pp, (N.EF_U8 if P.dtype == torch.uint8 else N.EF_F32)
+
+    @staticmethod
+    def _dev_out(t, shape, dtype, what):
+        if t.dtype != dtype or tuple(t.shape) != tuple(shape) or not t.is_contiguous():
+            raise ValueError(f"{what} must be a contiguous {dtype} tensor of shape {tuple(shape)}")
+        return t
 
     def project(self, P, out=None):
         if self.model_k is None:
             raise RuntimeError("no model: call set_model first")
         if _is_dev(P):
             import torch
-            dtype = N.EF_U8 if P.dtype == torch.uint8 else N.EF_F32
-            p, pp = _dev(P, P.dtype if P.dtype in (torch.uint8, torch.float32) else torch.float32)
+            p, pp, dtype = self._dev_pixels(P)
             b = p.shape[0]
             if out is None:
                 out = torch.empty((b, self.model_k), dtype=torch.float32, device=p.device)
+            self._dev_out(out, (b, self.model_k), torch.float32, "out")
             self._chk(self._lib.ef_project(self._h, pp, dtype, b, out.data_ptr(), N.EF_MEM_DEVICE))
             return out
         p = np.asarray(P)
@@ -209,7 +277,7 @@ class Engine:
         return f
 
     # --------------------------------------------------------------------- search
-    def set_gallery(self, G, global_offset: int = 0):
+    def set_gallery(self, G, global_offset: int = 0, owner=None):
         if _is_dev(G):
             import torch
             g, gp = _dev(G, torch.float32)
@@ -217,22 +285,33 @@ class Engine:
         else:
             g, gp = _host(G, np.float32)
             flags = 0
+        if g.ndim != 2:
+            raise ValueError("gallery must be 2-D (n, k)")
         n, k = g.shape
+        self.gallery_owner = None
         self._chk(self._lib.ef_gallery_set(self._h, gp, n, k, int(global_offset), flags))
         self.gallery_n, self.gallery_k = int(n), int(k)
+        self.gallery_owner = owner if owner is not None else object()
 
     def search_keys(self, Q, metric="l2", keys=None):
         """Packed keys (int64) of the best gallery row per probe."""
         mt = _metric(metric)
+        if self.gallery_k is None:
+            raise RuntimeError("no gallery: call set_gallery first")
         if _is_dev(Q):
             import torch
             q, qp = _dev(Q, torch.float32)
+            if q.ndim != 2 or q.shape[1] != self.gallery_k:
+                raise ValueError(f"Q must be (b, {self.gallery_k}), got {tuple(q.shape)}")
             b = q.shape[0]
             if keys is None:
                 keys = torch.empty(b, dtype=torch.int64, device=q.device)
+            self._dev_out(keys, (b,), torch.int64, "keys")
             self._chk(self._lib.ef_search(self._h, qp, b, mt, keys.data_ptr(), N.EF_MEM_DEVICE))
             return keys
         q, qp = _host(Q, np.float32)
+        if q.ndim != 2 or q.shape[1] != self.gallery_k:
+            raise ValueError(f"Q must be (b, {self.gallery_k}), got {q.shape}")
         b = q.shape[0]
         k = np.empty(b, dtype=np.int64)
         self._chk(self._lib.ef_search(self._h, qp, b, mt, k.ctypes.data, 0))
@@ -248,27 +327,91 @@ class Engine:
     def recognize_keys(self, P, metric="l2", keys=None, feats=None):
         """Fused projection + search (device or host)."""
         mt = _metric(metric)
+        if self.model_k is None or self.gallery_k is None:
+            raise RuntimeError("recognize needs a model and a gallery")
         if _is_dev(P):
             import torch
-            dtype = N.EF_U8 if P.dtype == torch.uint8 else N.EF_F32
-            p = P if P.is_contiguous() else P.contiguous()
+            p, pp, dtype = self._dev_pixels(P)
             b = p.shape[0]
             if keys is None:
                 keys = torch.empty(b, dtype=torch.int64, device=p.device)
-            fp = feats.data_ptr() if feats is not None else None
-            self._chk(self._lib.ef_recognize(self._h, p.data_ptr(), dtype, b, mt, keys.data_ptr(), fp,
-                                             N.EF_MEM_DEVICE))
+            self._dev_out(keys, (b,), torch.int64, "keys")
+            fp = None
+            if feats is not None:
+                fp = self._dev_out(feats, (b, self.model_k), torch.float32, "feats").data_ptr()
+            self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, keys.data_ptr(), fp, N.EF_MEM_DEVICE))
             return keys
         p = np.asarray(P)
         dtype = N.EF_U8 if p.dtype == np.uint8 else N.EF_F32
         p, pp = _host(p, np.uint8 if dtype == N.EF_U8 else np.float32)
+        if p.ndim != 2 or p.shape[1] != self.model_d:
+            raise ValueError(f"P must be (b, {self.model_d}), got {p.shape}")
         b = p.shape[0]
         k = np.empty(b, dtype=np.int64)
         fp = None
         if feats is not None:
+            if not (isinstance(feats, np.ndarray) and feats.dtype == np.float32 and feats.shape == (b, self.model_k)
+                    and feats.flags.c_contiguous):
+                raise ValueError(f"feats must be a contiguous float32 array of shape {(b, self.model_k)}")
             fp = feats.ctypes.data
         self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, k.ctypes.data, fp, 0))
         return k
+
+    # ------------------------------------------------------- exact match records
+    def search_matches(self, Q, metric="l2", out=None):
+        """ef_search_matches: per-probe (fp64 score, scale, key) records (numpy structured
+        array of N.MATCH_DTYPE on the host; an (b, 3) int64 tensor for device input)."""
+        return self._matches(Q, metric, out, search=True)
+
+    def recognize_matches(self, P, metric="l2", out=None):
+        """ef_recognize_matches: projection + search, returning match records."""
+        return self._matches(P, metric, out, search=False)
+
+    def _matches(self, X, metric, out, search):
+        mt = _metric(metric)
+        if _is_dev(X):
+            import torch
+            if search:
+                x, xp = _dev(X, torch.float32)
+                if x.ndim != 2 or x.shape[1] != self.gallery_k:
+                    raise ValueError(f"Q must be (b, {self.gallery_k})")
+            else:
+                x, xp, dtype = self._dev_pixels(X)
+            b = x.shape[0]
+            if out is None:
+                out = torch.empty((b, 3), dtype=torch.int64, device=x.device)
+            self._dev_out(out, (b, 3), torch.int64, "out")
+            if search:
+                self._chk(self._lib.ef_search_matches(self._h, xp, b, mt, out.data_ptr(), N.EF_MEM_DEVICE))
+            else:
+                self._chk(self._lib.ef_recognize_matches(self._h, xp, dtype, b, mt, out.data_ptr(), None,
+                                                         N.EF_MEM_DEVICE))
+            return out
+        if search:
+            x, xp = _host(X, np.float32)
+        else:
+            x = np.asarray(X)
+            dtype = N.EF_U8 if x.dtype == np.uint8 else N.EF_F32
+            x, xp = _host(x, np.uint8 if dtype == N.EF_U8 else np.float32)
+        b = x.shape[0]
+        res = np.empty(b, dtype=N.MATCH_DTYPE)
+        if search:
+            self._chk(self._lib.ef_search_matches(self._h, xp, b, mt, res.ctypes.data, 0))
+        else:
+            self._chk(self._lib.ef_recognize_matches(self._h, xp, dtype, b, mt, res.ctypes.data, None, 0))
+        return res
+
+    def merge_matches(self, parts, b, keys=None):
+        """Device merge (ef_matches_merge, EF_MEM_DEVICE) of gathered records: ``parts`` is
+        an (nparts*b, 3) int64 tensor (part-major) -> int64 keys[b]."""
+        import torch
+        nparts = parts.shape[0] // b if b else 0
+        if keys is None:
+            keys = torch.empty(b, dtype=torch.int64, device=parts.device)
+        if b:
+            self._chk(self._lib.ef_matches_merge(self._h, parts.data_ptr(), nparts, b, keys.data_ptr(), None,
+                                                 N.EF_MEM_DEVICE))
+        return keys
 
     def recognize(self, P, metric="l2", return_features=False):
         """Project probes P (uint8/float32 pixels) and return (idx, best[, feats])."""
@@ -279,6 +422,8 @@ class Engine:
         return (idx, best, feats) if return_features else (idx, best)
 
     # ---------------------------------------------------------------------- images
+    PREPROCESS_CHUNK = 65535
+
     def preprocess(self, images, size=(64, 64), rgb=False, out=None):
         """Grey + INTER_LINEAR resize of a ragged batch (include/eigenface.h
         ef_preprocess): ``images`` is a list of uint8 arrays (h, w) or (h, w, 3|4)
@@ -288,6 +433,14 @@ class Engine:
         n = len(images)
         if n == 0:
             return np.empty((0, oh * ow), np.uint8)
+        if n > self.PREPROCESS_CHUNK:  # ef_preprocess takes at most 65535 images per call
+            res = np.empty((n, oh * ow), np.uint8) if out is None else None
+            for a in range(0, n, self.PREPROCESS_CHUNK):
+                e = min(n, a + self.PREPROCESS_CHUNK)
+                part = self.preprocess(images[a:e], size, rgb, None if out is None else out[a:e])
+                if res is not None:
+                    res[a:e] = part
+            return out if out is not None else res
         arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
         hs = np.array([a.shape[0] for a in arrs], np.int32)
         ws = np.array([a.shape[1] for a in arrs], np.int32)
@@ -386,6 +539,21 @@ def decode_keys(keys, metric="l2"):
     best = np.empty(b, dtype=np.float32)
     N.lib().ef_keys_decode(k.ctypes.data, b, _metric(metric), best.ctypes.data, idx.ctypes.data)
     return idx, best
+
+
+def merge_matches_host(parts, b):
+    """Host merge (ef_matches_merge without a context; no GPU needed): ``parts`` is an
+    array of N.MATCH_DTYPE (nparts*b, part-major) or its (nparts*b, 3) int64 view."""
+    p = np.ascontiguousarray(parts)
+    if p.dtype != np.dtype(N.MATCH_DTYPE):
+        p = np.ascontiguousarray(p, dtype=np.int64).view(N.MATCH_DTYPE).reshape(-1)
+    nparts = p.shape[0] // b if b else 0
+    keys = np.empty(b, dtype=np.int64)
+    if b:
+        rc = N.lib().ef_matches_merge(None, p.ctypes.data, nparts, b, keys.ctypes.data, None, 0)
+        if rc != N.EF_OK:
+            raise N.EigenfaceError(rc, "ef_matches_merge failed")
+    return keys
 
 
 def device_count() -> int:

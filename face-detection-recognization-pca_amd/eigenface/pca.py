@@ -86,8 +86,12 @@ class EigenfacePCA:
         self.fit_iters_ = r.iters
         self._W = np.ascontiguousarray(w, dtype=np.float32)
         self._mu = np.ascontiguousarray(r.mean, dtype=np.float32)
-        self._model_on = None
-        self._gallery_on = None
+        # owner tokens: the engine's resident model / gallery are ours only while the
+        # engine still carries these exact tokens (another estimator or a drop-in function
+        # may have replaced them in between)
+        self._model_token = object()
+        self._gallery_token = None
+        self._gallery_src = None
         return self
 
     def fit_transform(self, X, y=None):
@@ -95,9 +99,8 @@ class EigenfacePCA:
 
     # --------------------------------------------------------------- transform
     def _ensure_model(self, eng):
-        if self._model_on is not eng:
-            eng.set_model(self._mu, self._W)
-            self._model_on = eng
+        if eng.model_owner is not self._model_token:
+            eng.set_model(self._mu, self._W, owner=self._model_token)
 
     def transform(self, X):
         """(p - mean) . W on the GPU (fp32 MFMA), returned as float64."""
@@ -110,10 +113,11 @@ class EigenfacePCA:
 
     # --------------------------------------------------------------- recognize
     def set_gallery(self, features=None):
+        """Gallery rows for ``recognize`` (default: the training features)."""
         eng = get_engine(self.device)
-        g = self.face_features_ if features is None else features
-        eng.set_gallery(np.asarray(g, dtype=np.float32))
-        self._gallery_on = (eng, id(g))
+        self._gallery_src = self.face_features_ if features is None else np.asarray(features)
+        self._gallery_token = object()
+        eng.set_gallery(np.asarray(self._gallery_src, dtype=np.float32), owner=self._gallery_token)
         return self
 
     def recognize(self, P, metric="cosine", threshold=None):
@@ -121,8 +125,10 @@ class EigenfacePCA:
         only) idx is -1 where score < threshold (scan-template-v4.py:278)."""
         eng = get_engine(self.device)
         self._ensure_model(eng)
-        if self._gallery_on is None or self._gallery_on[0] is not eng:
+        if self._gallery_token is None:
             self.set_gallery()
+        elif eng.gallery_owner is not self._gallery_token:  # replaced by someone else: re-upload
+            eng.set_gallery(np.asarray(self._gallery_src, dtype=np.float32), owner=self._gallery_token)
         idx, best = eng.recognize(P, metric)
         if threshold is not None:
             idx = np.where(best >= threshold, idx, -1)
@@ -144,15 +150,42 @@ def manual_pca(data_matrix, n_components=None, device=0):
 
 
 # ------------------------------------------------------------------ recognize
-_gallery_cache: dict = {}
+class _ArrayToken:
+    """Owner token of an uploaded host array: the array itself (kept alive, so its id
+    cannot be reused) plus a digest of its bytes (so in-place edits re-upload)."""
+
+    def __init__(self, a):
+        self.a = a
+        self.shape, self.dtype = a.shape, a.dtype
+        self.digest = _digest(a)
+
+    def matches(self, a):
+        return a is self.a and a.shape == self.shape and a.dtype == self.dtype and _digest(a) == self.digest
+
+
+def _digest(a):
+    import hashlib
+    return hashlib.blake2b(np.ascontiguousarray(a).view(np.uint8), digest_size=16).digest()
 
 
 def _gallery_engine(features, device):
+    """Engine whose resident gallery holds ``features`` (uploaded when the engine's owner
+    token is not this array's token)."""
     eng = get_engine(device)
-    key = (id(features), np.asarray(features).shape, device)
-    if _gallery_cache.get(device) != key:
-        eng.set_gallery(np.asarray(features, dtype=np.float32))
-        _gallery_cache[device] = key
+    a = features if isinstance(features, np.ndarray) else np.asarray(features)
+    tok = eng.gallery_owner
+    if not (isinstance(tok, _ArrayToken) and tok.matches(a)):
+        eng.set_gallery(np.asarray(a, dtype=np.float32), owner=_ArrayToken(a))
+    return eng
+
+
+def _model_engine(mean, W, device):
+    """Engine whose resident model is (mean, W) (same owner-token rule)."""
+    eng = get_engine(device)
+    tok = eng.model_owner
+    if not (isinstance(tok, tuple) and len(tok) == 2 and tok[0].matches(mean) and tok[1].matches(W)):
+        eng.set_model(np.asarray(mean, dtype=np.float32), np.asarray(W, dtype=np.float32),
+                      owner=(_ArrayToken(mean), _ArrayToken(W)))
     return eng
 
 
@@ -178,13 +211,40 @@ def recognize_face(face_vector, model_data, similarity_threshold=0.7, device=0):
     """Drop-in for ``recognize_face`` on a ``models/*_pca_model.pkl`` dict
     (useless/scan.py:100-132): returns ``(person_name, max_similarity,
     is_recognized)``."""
-    eng = get_engine(device)
-    ef = np.asarray(model_data["eigenfaces"], dtype=np.float32)
-    eng.set_model(np.asarray(model_data["mean_face"], dtype=np.float32), ef)
-    _gallery_cache.pop(device, None)
-    eng.set_gallery(np.asarray(model_data["projected_data"], dtype=np.float32))
-    p = np.asarray(face_vector).reshape(1, -1)
+    return recognize_faces(np.asarray(face_vector).reshape(1, -1), model_data, similarity_threshold, device)[0]
+
+
+def recognize_faces(face_vectors, model_data, similarity_threshold=0.7, device=0):
+    """Batched ``recognize_face``: one GPU projection + cosine arg-best for all rows of
+    ``face_vectors`` (b, d) — the loop useless/scan.py:168-215 runs per detection."""
+    mean, ef = _as_array(model_data["mean_face"]), _as_array(model_data["eigenfaces"])
+    eng = _model_engine(mean, ef, device)
+    _gallery_engine(_as_array(model_data["projected_data"]), device)
+    p = np.asarray(face_vectors)
     p = p if p.dtype == np.uint8 else p.astype(np.float32)
     _, best = eng.recognize(p, "cosine")
-    sim = float(best[0])
-    return model_data["person_name"], sim, sim >= similarity_threshold
+    name = model_data["person_name"]
+    return [(name, float(s), bool(s >= similarity_threshold)) for s in best]
+
+
+def recognize_face_dual_model(face_vector, dark_model_data, light_model_data, similarity_threshold=0.7, device=0):
+    """Drop-in for ``recognize_face_dual_model`` (useless/scan.py:134-166): the face is
+    recognised by the dark and the light model, OR-combined; the confidence is the
+    larger similarity and the name comes from the dark model on ties (``>=``).  Returns
+    ``(person_name, best_confidence, is_recognized, dark_similarity, light_similarity)``."""
+    return recognize_faces_dual_model(np.asarray(face_vector).reshape(1, -1), dark_model_data, light_model_data,
+                                      similarity_threshold, device)[0]
+
+
+def recognize_faces_dual_model(face_vectors, dark_model_data, light_model_data, similarity_threshold=0.7, device=0):
+    """Batched :func:`recognize_face_dual_model`: one GPU pass per model over all rows."""
+    dark = recognize_faces(face_vectors, dark_model_data, similarity_threshold, device)
+    light = recognize_faces(face_vectors, light_model_data, similarity_threshold, device)
+    out = []
+    for (dn, ds, dr), (ln, ls, lr) in zip(dark, light):
+        out.append((dn if ds >= ls else ln, max(ds, ls), dr or lr, ds, ls))
+    return out
+
+
+def _as_array(a):
+    return a if isinstance(a, np.ndarray) else np.asarray(a)

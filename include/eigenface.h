@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 1
+#define EF_API_VERSION 2
 
 /* status codes */
 #define EF_OK 0
@@ -134,6 +134,62 @@ int ef_recognize(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, int32_t
 /* Host-side key decoding: L2 -> squared distance, COSINE -> similarity;
  * EF_KEY_NONE -> idx -1, best NaN. */
 void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx);
+
+/* ------------------------------------------------ exact cross-shard arg-best
+ * A key's fp32 score cannot order two shards' winners whose fp64 scores differ by less
+ * than one fp32 ulp, and a MIN over keys would then fall back to the lower index.  The
+ * match record of a probe carries the winner's fp64 score, so shards merge exactly:
+ *   score  fp64 score of the winning row (L2: squared distance; COSINE: -similarity;
+ *          +inf with key == EF_KEY_NONE for an empty shard)
+ *   scale  tie-tolerance scale (L2: |q|^2 + max |g|^2 of the shard; COSINE: 1)
+ *   key    the packed key of ef_search (global row index in the low 32 bits)
+ * Merging picks, per probe, the lowest global index among the parts whose score is within
+ * 1e-12 * (|min score| + max scale) of the minimum — the rule a single engine applies to
+ * its fp32-ambiguous candidates (np.argmin / np.argmax first-index semantics,
+ * scan-template-v4.py:274-275). */
+typedef struct ef_match {
+  double score;
+  double scale;
+  int64_t key;
+} ef_match;
+int ef_search_matches(ef_ctx* ctx, const float* Q, int64_t b, int32_t metric, ef_match* out, uint32_t flags);
+int ef_recognize_matches(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, int32_t metric, ef_match* out,
+                         float* feats, uint32_t flags);
+/* parts: nparts x b records (part-major) -> keys_out[b] (and merged records in merged_out,
+ * optional).  Host pointers: computed on the host, ctx may be NULL (usable without a GPU).
+ * EF_MEM_DEVICE: device pointers, stream-ordered on ctx's stream. */
+int ef_matches_merge(ef_ctx* ctx, const ef_match* parts, int32_t nparts, int64_t b, int64_t* keys_out,
+                     ef_match* merged_out, uint32_t flags);
+
+/* ------------------------------------------------------------- multi-GPU (RCCL)
+ * Row-sharded gallery across the ranks of one job, one process per GPU:
+ * rank r sets its shard with ef_gallery_set(..., global_offset = first global row).
+ * Once a communicator is attached, ef_search / ef_recognize (and the _matches forms) on
+ * every rank return the GLOBAL result: each rank searches its shard, the match records
+ * are all-gathered over RCCL (xGMI) and merged exactly (ef_matches_merge) on the ctx's
+ * stream.  ef_recognize additionally splits the projection: rank r projects probes
+ * [r*c, (r+1)*c), c = ceil(b / nranks), and the features are all-gathered.  Every rank
+ * must make the same calls with the same b and metric (collectives).  RCCL is loaded at
+ * run time (librccl.so.1); EF_E_STATE if it is unavailable.
+ * ef_comm_unique_id: rank 0 creates the id (EF_UNIQUE_ID_BYTES bytes) and the caller
+ * broadcasts it (e.g. over torch.distributed or MPI). */
+#define EF_UNIQUE_ID_BYTES 128
+int ef_comm_unique_id(void* id_out);
+int ef_comm_init(ef_ctx* ctx, int32_t nranks, int32_t rank, const void* unique_id);
+int ef_comm_destroy(ef_ctx* ctx);
+int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
+
+/* ------------------------------------------------------------------ options
+ * Per-context tunables (defaults in brackets). */
+#define EF_OPT_FIT_MAX_ITERS 1   /* subspace-iteration cap [500]; reaching it unconverged -> EF_E_NUMERIC */
+#define EF_OPT_FIT_FP32_COARSE 2 /* 1 [default]: fp32 C.Q products while the Ritz values still move by
+                                    > 1e-4 (self-correcting); 0: fp64 products throughout */
+#define EF_OPT_COV_SLAB_BYTES 3  /* device budget of the int32 covariance partial sums [8 GiB];
+                                    smaller budgets run the multi-pass int64 schedule */
+#define EF_OPT_TM_INT64_SUMS 4   /* 1: int64 integral images in the template localiser [0: auto] */
+#define EF_OPT_HAAR_ORDERED 5    /* 1: sequential stage sums even when reassociation is exact [0] */
+int ef_set_option(ef_ctx* ctx, int32_t option, int64_t value);
+int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 
 /* ------------------------------------------------------------------ ingest
  * Replaces the per-image cv2.cvtColor(img, COLOR_BGR2GRAY) + cv2.resize(gray, (w, h))

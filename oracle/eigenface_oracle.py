@@ -38,6 +38,8 @@ __all__ = [
     "recognize_face_manual",
     "manual_model_info_evr",
     "synth_faces",
+    "int_synth_faces",
+    "pca_cov_fit",
     "synth_basis",
     "synth_mean_face",
     "planted_probes",
@@ -154,6 +156,55 @@ def pca_full_fit(z, n_components):
         "n_samples_": n,
         "total_var": float(total),
         "fit_transform": u[:, :k] * s[:k],
+    }
+
+
+def pca_cov_fit(x, n_components, standardize=True, chunk=2048):
+    """``train_pca_model``'s StandardScaler + PCA for n >= d through the covariance
+    branch of manual_pca (useless/train.py:97-103: ``np.cov`` + ``eigh``) instead of
+    an SVD of the n x d matrix — the same estimator (``components_`` = top
+    eigenvectors of the covariance of the standardised data, ``explained_variance_``
+    = its eigenvalues, sklearn's svd_flip sign rule, extmath.py:946-952), affordable
+    at the C3 shape (d = 16384).  Only the top ``n_components`` pairs are computed
+    (LAPACK dsyevr through scipy).  Returns the dict of :func:`pca_full_fit` plus
+    ``scaler``."""
+    import scipy.linalg as sla
+
+    x = np.asarray(x)
+    n, d = x.shape
+    k = int(n_components)
+    if standardize:
+        s_mean, s_var, s_scale = standard_scaler_fit(x)
+    else:
+        s_mean = x.astype(np.float64).mean(axis=0)
+        s_var = s_scale = np.ones(d)
+    # z = (x - mu)/sigma; PCA centres z again (mean ~1e-17) — _pca.py:741-743
+    zmean = np.zeros(d)
+    for a in range(0, n, chunk):
+        zmean += ((x[a:a + chunk].astype(np.float64) - s_mean) / s_scale).sum(axis=0)
+    zmean /= n
+    cov = np.zeros((d, d))
+    for a in range(0, n, chunk):
+        zc = (x[a:a + chunk].astype(np.float64) - s_mean) / s_scale - zmean
+        cov += zc.T @ zc
+    cov /= n - 1
+    total = float(np.trace(cov))
+    lam, vec = sla.eigh(cov, subset_by_index=[d - k, d - 1], driver="evr", overwrite_a=True)
+    del cov
+    order = np.argsort(lam)[::-1]
+    lam = lam[order]
+    vt, _ = _svd_flip_rows(vec[:, order].T)
+    feats = np.empty((n, k))
+    for a in range(0, n, chunk):
+        feats[a:a + chunk] = ((x[a:a + chunk].astype(np.float64) - s_mean) / s_scale - zmean) @ vt.T
+    return {
+        "scaler": (s_mean, s_var, s_scale),
+        "mean_": zmean,
+        "components_": vt,
+        "explained_variance_": lam,
+        "explained_variance_ratio_": lam / total,
+        "total_var": total,
+        "fit_transform": feats,
     }
 
 
@@ -311,6 +362,48 @@ def synth_faces(n, side, r=64, seed=0, noise=2.0, basis=None, coeffs=None):
         coeffs = rng.standard_normal((n, r)) * synth_spectrum(r)[None, :]
     x = synth_mean_face(side)[None, :] + coeffs @ b.T + noise * rng.standard_normal((n, d))
     return np.clip(np.rint(x), 0, 255).astype(np.uint8), coeffs
+
+
+INT_SYNTH_BLOCK = 2048
+
+
+def int_synth_spectrum(r):
+    """Integer factor weights floor(4096 / sqrt(j+1)) (pure integer arithmetic)."""
+    import math
+    return np.array([math.isqrt(4096 * 4096 // (j + 1)) for j in range(r)], dtype=np.int64)
+
+
+def int_synth_faces(n, side, r=160, seed=0, rows=None):
+    """Bit-reproducible synthetic faces for fit-parity fixtures at large shapes.
+
+    ``X = clip(M + rint((Z.diag(s)).Bq / 2^20) + eps, 0, 255)`` with integer-valued
+    operands only: ``Bq`` uniform integers in [-128, 128) (r x d), ``Z`` sums of four
+    uniform integers in [-32, 32) per factor, ``s`` :func:`int_synth_spectrum`,
+    ``eps`` uniform in {-2..2}, ``M`` an integer radial face-like mean.  Every partial
+    sum of ``Z.diag(s).Bq`` is an integer below 2^53, so the float64 product is exact
+    whatever BLAS kernel or summation order the host uses: the same seed gives the same
+    pixels on the build container and on the GPU box.  Rows come in blocks of
+    INT_SYNTH_BLOCK, each from its own seeded stream, so ``rows=(lo, hi)`` regenerates
+    any slice.  The spectrum (eigenvalues ~ 1/(j+1) for r factors, noise floor far
+    below) keeps the top-128 eigen-gaps meaningful for eigenvector parity.
+    """
+    d = side * side
+    lo, hi = (0, n) if rows is None else rows
+    bq = np.random.default_rng([seed, 0]).integers(-128, 128, size=(r, d)).astype(np.float64)
+    s = int_synth_spectrum(r).astype(np.float64)
+    yy, xx = np.mgrid[0:side, 0:side]
+    dy, dx = yy - side // 2, xx - side // 2
+    m = (170 - (dx * dx + dy * dy) * 80 // max(side * side // 2, 1)).ravel().astype(np.float64)
+    out = np.empty((hi - lo, d), dtype=np.uint8)
+    for blk in range(lo // INT_SYNTH_BLOCK, (hi - 1) // INT_SYNTH_BLOCK + 1 if hi > lo else 0):
+        a, e = blk * INT_SYNTH_BLOCK, min(n, (blk + 1) * INT_SYNTH_BLOCK)
+        rng = np.random.default_rng([seed, 1, blk])
+        z = rng.integers(-32, 32, size=(4, e - a, r)).sum(axis=0).astype(np.float64) * s
+        eps = rng.integers(-2, 3, size=(e - a, d)).astype(np.float64)
+        px = np.clip(m + np.rint((z @ bq) * (1.0 / 1048576.0)) + eps, 0, 255).astype(np.uint8)
+        ca, ce = max(a, lo), min(e, hi)
+        out[ca - lo:ce - lo] = px[ca - a:ce - a]
+    return out
 
 
 def planted_probes(gallery_pixels_fn, targets, noise=4.0, seed=7):

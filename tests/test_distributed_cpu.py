@@ -1,7 +1,8 @@
-"""The N>1 path on CPU: world_size-2 gloo, row-sharded gallery, all-reduce(MIN) over
-packed keys == unsharded arg-best with lowest-index ties.  The per-rank search here is
-the oracle (the GPU kernel's key format is checked separately against the library's
-decoder and on the GPU by test_gpu_search.test_sharded_keys_min_equals_full)."""
+"""The N>1 path on CPU: world_size-2/3 gloo, row-sharded gallery, all-gather of the
+per-rank fp64 match records + the library's exact merge (ef_matches_merge, host form) ==
+unsharded arg-best with lowest-index ties — including winners in different shards whose
+fp64 scores differ by less than one fp32 ulp.  The per-rank search here is the oracle
+(the GPU kernel's records are checked on the GPU by tests/test_gpu_distributed.py)."""
 import os
 import socket
 
@@ -22,20 +23,47 @@ def _free_port():
     return p
 
 
-def _oracle_keys(q, g_local, lo, metric):
+def _paths():
     import sys
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
-    from eigenface.distributed import pack_keys
-    from oracle import eigenface_oracle as orc
-    if len(g_local) == 0:
-        return np.full(len(q), (1 << 63) - 1, dtype=np.int64)
+
+
+def _scores64(q, g, metric):
+    q = np.asarray(q, np.float64)
+    g = np.asarray(g, np.float64)
     if metric == "l2":
-        idx, d2 = orc.l2_argmin(q, g_local)
-        return pack_keys(d2.astype(np.float32), idx + lo)
-    idx, s = orc.cosine_argmax(q, g_local)
-    return pack_keys(-s.astype(np.float32), idx + lo)
+        return ((q[:, None, :] - g[None, :, :]) ** 2).sum(-1)
+    qn = np.linalg.norm(q, axis=1)
+    gn = np.linalg.norm(g, axis=1)
+    dots = q @ g.T
+    with np.errstate(invalid="ignore", divide="ignore"):
+        sim = dots / (qn[:, None] * gn[None, :])
+    sim[(qn[:, None] == 0) | (gn[None, :] == 0)] = 0.0
+    return -sim
+
+
+def _oracle_matches(q, g_local, lo, metric):
+    """One shard's records by the single-engine rule: lowest index among rows whose fp64
+    score is within 1e-12 * (|min| + scale) of the shard's minimum."""
+    _paths()
+    from eigenface.distributed import make_matches
+    q = np.asarray(q)
+    if len(g_local) == 0:
+        return make_matches(np.full(len(q), np.inf), np.zeros(len(q)), np.zeros(len(q), np.int64))
+    s = _scores64(q, g_local, metric)
+    g64 = np.asarray(g_local, np.float64)
+    scale = ((np.asarray(q, np.float64) ** 2).sum(1) + (g64 ** 2).sum(1).max()) if metric == "l2" \
+        else np.ones(len(q))
+    vmin = s.min(axis=1)
+    tol = 1e-12 * (np.abs(vmin) + scale)
+    idx = np.argmax(s <= (vmin + tol)[:, None], axis=1)
+    return make_matches(s[np.arange(len(q)), idx], scale, idx + lo)
+
+
+def _oracle_keys(q, g, metric):
+    return _oracle_matches(q, g, 0, metric)["key"]
 
 
 def _worker(rank, world, port, g, q, metric, out):
@@ -49,7 +77,7 @@ def _worker(rank, world, port, g, q, metric, out):
     from eigenface.distributed import ShardedGallery, shard_range
     lo, hi = shard_range(len(g), rank, world)
     sg = ShardedGallery(None, g[lo:hi], len(g), rank, world,
-                        local_search=lambda qq, m, keys=None: _oracle_keys(qq, g[lo:hi], lo, m))
+                        local_matches=lambda qq, m: _oracle_matches(qq, g[lo:hi], lo, m))
     keys = sg.search_keys(q, metric)
     out[rank] = keys.numpy().copy()
     dist.destroy_process_group()
@@ -75,7 +103,7 @@ def test_sharded_allreduce_matches_unsharded(metric, world):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    full = _oracle_keys(q, g, 0, metric)
+    full = _oracle_keys(q, g, metric)
     for r in range(world):
         np.testing.assert_array_equal(out[r], full)
     from eigenface import decode_keys
@@ -125,7 +153,7 @@ def _proj_worker(rank, world, port, g, P, mean, W, metric, out):
         return torch.from_numpy(orc.project(p.numpy(), mean, W).astype(np.float32))
 
     sg = ShardedGallery(None, g[lo:hi], len(g), rank, world, local_project=proj,
-                        local_search=lambda qq, m, keys=None: _oracle_keys(qq.numpy(), g[lo:hi], lo, m))
+                        local_matches=lambda qq, m: _oracle_matches(qq.numpy(), g[lo:hi], lo, m))
     keys = sg.recognize_keys(torch.from_numpy(P), metric)
     out[rank] = (keys.numpy().copy(), sum(seen))
     dist.destroy_process_group()
@@ -157,8 +185,86 @@ def test_sharded_projection_allgather_matches_unsharded(world, b):
         p.join(120)
         assert p.exitcode == 0
     q = orc.project(P, mean, W).astype(np.float32)
-    full = _oracle_keys(q, g, 0, "l2")
+    full = _oracle_keys(q, g, "l2")
     c = (b + world - 1) // world
     for r in range(world):
         np.testing.assert_array_equal(out[r][0], full)
         assert out[r][1] == max(0, min(b, (r + 1) * c) - min(b, r * c))
+
+
+def sub_ulp_case(k=24, n=400, seed=0):
+    """Gallery + probes where the true winner sits in a later shard and beats a row of an
+    earlier shard by ~1e-9 relative — below fp32 resolution of the score, far above the
+    1e-12 tie tolerance.  A MIN over packed fp32 keys would return the earlier row.
+    Returns (g, q, rows_a, rows_b, metric_of_probe)."""
+    rng = np.random.default_rng(seed)
+    g = (rng.standard_normal((n, k)) * 4.0).astype(np.float32)
+    q = np.zeros((4, k), np.float32)
+    # L2 probes 0, 1: g_a = q + 0.5 e0 (d^2 = 0.25); g_b = q + x e1 + y e2 with
+    # x = 0.5 - 2^-24, x^2 + y^2 = 0.25 - 1e-9 (both round to the same fp32 distance)
+    x = np.float32(0.5) - np.float32(2.0 ** -24)
+    y = np.float32(np.sqrt(0.25 - 1e-9 - float(x) ** 2))
+    rows_a, rows_b = [], []
+    for j, (ra, rb) in enumerate([(10, 390), (150, 260)]):
+        base = (np.rint(rng.standard_normal(k) * 20) / 64).astype(np.float32)
+        base[:3] = 0  # the offsets below are then exact in fp32
+        q[j] = base
+        g[ra] = base
+        g[ra, 0] += np.float32(0.5)
+        g[rb] = base
+        g[rb, 1] += x
+        g[rb, 2] += y
+        rows_a.append(ra)
+        rows_b.append(rb)
+    # cosine probes 2, 3: q = e0; g_a = (1, a), g_b = (1, b) with 1/sqrt(1+b^2) - 1/sqrt(1+a^2) ~ 1e-9
+    a = np.float32(1e-3)
+    bb = np.float32(np.sqrt(float(a) ** 2 - 2e-9))
+    for j, (ra, rb), ax in zip((2, 3), [(20, 380), (100, 200)], (0, 5)):
+        q[j] = 0
+        q[j, ax] = 1
+        g[ra] = 0
+        g[ra, ax], g[ra, ax + 3] = 1, a
+        g[rb] = 0
+        g[rb, ax], g[rb, ax + 4] = 1, bb
+        rows_a.append(ra)
+        rows_b.append(rb)
+    return g, q, rows_a, rows_b
+
+
+def test_sub_ulp_case_is_a_real_fp32_tie():
+    g, q, ra, rb = sub_ulp_case()
+    s_l2 = _scores64(q[:2], g, "l2")
+    s_cos = _scores64(q[2:], g, "cosine")
+    for s, a, b in ((s_l2, ra[:2], rb[:2]), (s_cos, ra[2:], rb[2:])):
+        for i in range(2):
+            va, vb = s[i, a[i]], s[i, b[i]]
+            assert vb < va and (va - vb) / abs(va) > 1e-10        # b is strictly better in fp64
+            assert np.float32(va) == np.float32(vb)                 # ... but ties in fp32
+            assert np.argmin(s[i]) == b[i]
+    # the fp32 key MIN across shards would pick the earlier row
+    from eigenface.distributed import pack_keys
+    ka = pack_keys(np.float32(s_l2[0, ra[0]]), ra[0])
+    kb = pack_keys(np.float32(s_l2[0, rb[0]]), rb[0])
+    assert min(ka, kb) == ka
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merge_is_fp64_exact_across_shards(world):
+    g, q, ra, rb = sub_ulp_case()
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    res = {}
+    for metric, qs in (("l2", q[:2]), ("cosine", q[2:])):
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, g, qs, metric, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+        res[metric] = [out[r] for r in range(world)]
+    from eigenface import decode_keys
+    for metric, want in (("l2", rb[:2]), ("cosine", rb[2:])):
+        for r in range(world):
+            idx, _ = decode_keys(res[metric][r], metric)
+            np.testing.assert_array_equal(idx, want)

@@ -103,3 +103,33 @@ def test_read_faces_gpu_ingest_matches_oracle(tmp_path):
     np.testing.assert_array_equal(rows, np.stack(ref))
     np.testing.assert_array_equal(read_face(paths[0]).ravel(), ref[0])
     assert read_face(paths[2]) is None
+
+
+def test_engine_owner_tokens_interleaved_models():
+    """Two EigenfacePCA instances and the drop-in functions share one engine per device:
+    each must re-upload its model / gallery when another caller replaced it (owner
+    tokens), never silently use someone else's."""
+    from eigenface import EigenfacePCA, recognize_face_with_model
+    xa, _ = orc.synth_faces(300, 32, r=24, seed=41)
+    xb, _ = orc.synth_faces(300, 32, r=24, seed=42)
+    a = EigenfacePCA(12, standardize=True).fit(xa)
+    b = EigenfacePCA(12, standardize=True).fit(xb)
+    fa = a.transform(xa[:5])
+    fb = b.transform(xb[:5])
+    ia, _ = a.recognize(xa[:5])
+    ib, _ = b.recognize(xb[:5])
+    for _ in range(2):  # interleave: each call must see its own model and gallery
+        np.testing.assert_allclose(a.transform(xa[:5]), fa, rtol=1e-6, atol=1e-6)
+        np.testing.assert_array_equal(b.recognize(xb[:5])[0], ib)
+        np.testing.assert_allclose(b.transform(xb[:5]), fb, rtol=1e-6, atol=1e-6)
+        np.testing.assert_array_equal(a.recognize(xa[:5])[0], ia)
+    np.testing.assert_array_equal(ia, np.arange(5))
+    # a drop-in recognise with another gallery in between
+    g = np.random.default_rng(3).standard_normal((50, 12))
+    md = {"face_features": g, "face_labels": np.arange(50), "person_id_map": {f"p{i}": i for i in range(50)}}
+    pid, _, _ = recognize_face_with_model(g[7], md, threshold=0.5)
+    assert pid == 7
+    np.testing.assert_array_equal(a.recognize(xa[:5])[0], ia)
+    g[7] = -g[7]  # in-place edit of the same array: the digest forces a re-upload
+    pid, _, _ = recognize_face_with_model(g[7], md, threshold=0.5)
+    assert pid == 7

@@ -119,13 +119,19 @@ def test_standardized_covariance_path_vs_oracle():
                                atol=1e-7 * np.abs(o["face_features"]).max())
 
 
-def test_covariance_multi_pass(monkeypatch):
-    """Force the int8 covariance into several syrk passes (slab budget of one split):
-    the int64 slab accumulation between passes must keep the product exact."""
-    from eigenface import manual_pca
-    monkeypatch.setenv("EF_COV_SLAB_BUDGET", str(64 * 64 * 4))
+def test_covariance_multi_pass():
+    """Force the int8 covariance into several syrk passes (slab budget of one split,
+    EF_OPT_COV_SLAB_BYTES): the int64 slab accumulation between passes must keep the
+    product exact."""
+    from eigenface import get_engine, manual_pca
     x, _ = orc.synth_faces(140_000, 8, r=32, seed=5)  # K = 140000 > 2047 * 64 samples per split
-    eig, mean, proj, lam = manual_pca(x, 8)
+    e = get_engine(0)
+    default = e.get_option("cov_slab_bytes")
+    e.set_option("cov_slab_bytes", 64 * 64 * 4)
+    try:
+        eig, mean, proj, lam = manual_pca(x, 8)
+    finally:
+        e.set_option("cov_slab_bytes", default)
     o_eig, o_mean, _, o_lam = orc.manual_pca(x, 8)
     np.testing.assert_allclose(mean, o_mean, rtol=1e-14)
     np.testing.assert_allclose(lam, o_lam, rtol=1e-9)
@@ -133,20 +139,14 @@ def test_covariance_multi_pass(monkeypatch):
 
 
 @pytest.mark.parametrize("n,side,k,std", [(3000, 16, 12, False), (700, 32, 40, True), (5000, 8, 64, True)])
-def test_training_projection_int8_digits(monkeypatch, n, side, k, std):
-    """F = ((X - mu) w) E through the int8 digit GEMM (ef_proj_i8.hip) equals the fp64 GEMM
-    path (EF_FIT_PROJ_F64) and the oracle to fp64 rounding (useless/train.py:122,
+def test_training_projection_int8_digits(n, side, k, std):
+    """F = ((X - mu) w) E through the int8 digit GEMM (ef_proj_i8.hip) equals the fp64
+    CPU restatement of the centred, scaled product to fp64 rounding (useless/train.py:122,
     train-v4.py:134)."""
     from eigenface import EigenfacePCA
     x, _ = orc.synth_faces(n, side, r=min(48, side * side), seed=n + side)
     m = EigenfacePCA(k, standardize=std).fit(x)
     f8 = m.face_features_
-    monkeypatch.setenv("EF_FIT_PROJ_F64", "1")
-    m64 = EigenfacePCA(k, standardize=std).fit(x)
-    np.testing.assert_array_equal(m.components_, m64.components_)
-    scale = np.abs(m64.face_features_).max()
-    np.testing.assert_allclose(f8, m64.face_features_, rtol=0, atol=1e-12 * scale)
-    # and against the CPU restatement of the centred, scaled product
     z = (x - m.scaler_mean_) / m.scaler_scale_ if std else x - m.mean_face_
     ref = z @ m.components_.T
     np.testing.assert_allclose(f8, ref, rtol=0, atol=1e-11 * np.abs(ref).max())
@@ -170,3 +170,73 @@ def test_pooled_workspaces_refit_and_trim():
     np.testing.assert_array_equal(ra1.components, ra3.components)
     np.testing.assert_array_equal(rb1.components, rb2.components)
     np.testing.assert_array_equal(ra1.projection, ra3.projection)
+
+
+def test_eigensolver_non_convergence_is_reported():
+    """The subspace iteration's cap (EF_OPT_FIT_MAX_ITERS) ends an unconverged solve with
+    EF_E_NUMERIC instead of returning partial eigenpairs; FaceTrainer.train_pca_model
+    maps it to False with a message, as train-v4.py:114-120 does for a failed fit."""
+    from eigenface import EigenfaceError, get_engine
+    from eigenface._native import EF_E_NUMERIC
+    from eigenface.compat import FaceTrainer
+    x, _ = orc.synth_faces(600, 64, r=256, seed=31)  # Gram path, order 600 > 88: subspace iteration
+    e = get_engine(0)
+    e.set_option("fit_max_iters", 2)
+    try:
+        with pytest.raises(EigenfaceError) as ei:
+            e.fit(x, 40)
+        assert ei.value.code == EF_E_NUMERIC and "did not converge" in str(ei.value)
+        tr = FaceTrainer(n_components=40)
+        tr.face_images = x
+        tr.face_labels = np.zeros(len(x), np.int64)
+        assert tr.train_pca_model() is False and not tr.is_trained
+    finally:
+        e.set_option("fit_max_iters", 500)
+    r = e.fit(x, 40)  # default cap: converges
+    assert r.iters > 2
+
+
+def _c3_fixture():
+    g = golden("fit_c3.npz")
+    x = orc.int_synth_faces(int(g["n"]), int(g["side"]), r=int(g["r"]), seed=int(g["seed"]))
+    return g, x
+
+
+@pytest.mark.parametrize("coarse_fp32", [1, 0])
+def test_fit_c3_shape_vs_oracle(coarse_fp32):
+    """The C3 fit shape (d = 128 x 128 = 16384, k = 128, n = 20000 >= d, StandardScaler):
+    covariance branch at order 16384, the order >= 12288 Rayleigh-Ritz schedule and (for
+    coarse_fp32 = 1, the default) the fp32 coarse phase, against the oracle's
+    covariance-branch fit (tests/golden/make_fit_c3.py; exact-integer generator, so the
+    box regenerates the same pixels).  Eigenvalues rtol 1e-9, components 1e-4 relative
+    (north star), fp32 coarse phase == fp64 throughout to 1e-9."""
+    from eigenface import get_engine
+    g, x = _c3_fixture()
+    e = get_engine(0)
+    e.set_option("fit_fp32_coarse", coarse_fp32)
+    try:
+        r = e.fit(x, int(g["k"]), standardize=True)
+    finally:
+        e.set_option("fit_fp32_coarse", 1)
+    assert r.k == 128 and r.iters > 0  # subspace iteration, not the direct Jacobi
+    np.testing.assert_allclose(r.mean, g["scaler_mean"], rtol=1e-14)
+    np.testing.assert_allclose(r.scale, g["scaler_scale"], rtol=1e-12)
+    np.testing.assert_allclose(r.total_var, float(g["total_var"]), rtol=1e-12)
+    np.testing.assert_allclose(r.eigenvalues, g["eigenvalues"], rtol=1e-9)
+    R, px = _c3_probe_matrices(x.shape[1])
+    np.testing.assert_array_equal(px, g["px"])
+    cr = r.components @ R
+    s = np.sign((cr * g["comps_R"]).sum(axis=1))  # sign-align, then count rule flips
+    assert (s > 0).mean() >= 0.95  # svd_flip rule reproduced except near-tied max entries
+    cr *= s[:, None]
+    # unit rows against +-1 columns: |c.R| ~ 1, so atol 1e-4 is the 1e-4 relative bar
+    np.testing.assert_allclose(cr, g["comps_R"], atol=1e-4)
+    np.testing.assert_allclose(r.components[:, px] * s[:, None], g["comps_px"], atol=1e-4 * np.abs(g["comps_px"]).max())
+    f = r.projection[:64] * s[None, :]
+    np.testing.assert_allclose(f, g["features"], rtol=0, atol=1e-4 * np.abs(g["features"]).max())
+
+
+def _c3_probe_matrices(d):
+    r = np.random.default_rng([5]).integers(0, 2, size=(d, 8)).astype(np.float64) * 2.0 - 1.0
+    px = np.sort(np.random.default_rng([6]).choice(d, size=256, replace=False))
+    return r, px

@@ -103,18 +103,20 @@ def test_match_template_extreme_pixels_and_flat(eng):
 @pytest.mark.parametrize("ts", [(511, 512), (520, 510)])
 def test_match_template_integral_width(eng, monkeypatch, ts, force64):
     """Integral images are wrapping uint32 while every template area is < 2^18 and int64
-    otherwise (or with EF_TM_II64).  (511, 512) is the largest uint32 case: on the
+    otherwise (or with the EF_OPT_TM_INT64_SUMS option).  (511, 512) is the largest uint32 case: on the
     all-0 region (I' = -128) the window sum of I'^2 is 16384 * 261632, just below 2^32;
     (520, 510) has area >= 2^18 and must take the int64 form."""
-    if force64:
-        monkeypatch.setenv("EF_TM_II64", "1")
+    eng.set_option("tm_int64_sums", 1 if force64 else 0)
     rng = np.random.default_rng(ts[0])
     frame = (rng.integers(0, 2, (560, 540)) * 255).astype(np.uint8)
     frame[:530, :525] = 0
     frame[300:, 200:] = rng.integers(0, 256, (260, 340), dtype=np.uint8)
     t = frame[25:25 + ts[0], 12:12 + ts[1]].copy()
-    eng.tm_prepare([t], [(0,) + ts], frame.shape)
-    best, xs, ys, maps = eng.tm_match(frame, maps=True)
+    try:
+        eng.tm_prepare([t], [(0,) + ts], frame.shape)
+        best, xs, ys, maps = eng.tm_match(frame, maps=True)
+    finally:
+        eng.set_option("tm_int64_sums", 0)
     R = io.match_template_ccoeff_normed(frame, t)
     np.testing.assert_array_equal(maps[0], R)
     v, (mx, my) = io.min_max_loc_max(R)

@@ -46,7 +46,7 @@ def test_library_is_gfx950_code_object():
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
-    assert lib.ef_api_version() == 1
+    assert lib.ef_api_version() == 2
     n = ctypes.c_int(-1)
     assert lib.ef_device_count(ctypes.byref(n)) == 0
     if n.value == 0:  # build container: creating a context must fail cleanly, not crash
@@ -96,3 +96,43 @@ def test_product_package_does_not_import_oracle():
     for f in os.listdir(pkg):
         if f.endswith(".py"):
             assert "oracle" not in open(os.path.join(pkg, f)).read().replace("no oracle", ""), f
+
+
+def test_product_library_reads_no_environment_knobs():
+    """Experiment knobs and ablations live in the diagnostic build (make diag,
+    -DEF_DIAGNOSTICS) only: the product library never calls getenv, so no environment
+    variable can change its numerics or kernel choice."""
+    from eigenface import _native
+    out = subprocess.run(["nm", "-D", "--undefined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    assert not re.search(r"\bgetenv\b", out)
+
+
+def test_host_match_merge_is_exact():
+    """ef_matches_merge on the host (no GPU): fp64 scores decide across parts even when
+    their fp32 keys tie; exact ties and near-ties within 1e-12 go to the lowest index;
+    empty parts are ignored; all-empty gives EF_KEY_NONE."""
+    from eigenface import _native as N, decode_keys, merge_matches_host
+    from eigenface.distributed import pack_keys
+
+    b = 5
+    inf = np.inf
+    none = N.EF_KEY_NONE
+    # part 0 rows 0..99, part 1 rows 100..199
+    s0 = np.array([1.0, 2.0, 3.0, inf, 5.0])
+    s1 = np.array([1.0 - 1e-9, 2.0, 3.0 + 1e-13, inf, 4.0])
+    i0 = np.array([7, 8, 9, 0, 11])
+    i1 = np.array([107, 5, 109, 0, 111])
+    recs = np.zeros(2 * b, dtype=N.MATCH_DTYPE)
+    for r, (s, i) in enumerate([(s0, i0), (s1, i1)]):
+        recs["score"][r * b:(r + 1) * b] = s
+        recs["scale"][r * b:(r + 1) * b] = 1.0
+        keys = pack_keys(np.where(np.isinf(s), 0, s).astype(np.float32), i)
+        keys[np.isinf(s)] = none
+        recs["key"][r * b:(r + 1) * b] = keys
+    # fp32 keys of probe 0 tie (1 - 1e-9 rounds to 1.0f): the key MIN would pick row 7
+    assert np.float32(1.0 - 1e-9) == np.float32(1.0)
+    out = merge_matches_host(recs, b)
+    idx, best = decode_keys(out, "l2")
+    np.testing.assert_array_equal(idx, [107, 5, 9, -1, 111])
+    assert best[4] == np.float32(4.0)
+    assert out[3] == none
