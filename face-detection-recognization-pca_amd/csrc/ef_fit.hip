@@ -391,6 +391,68 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
   return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
 }
 
+// Numerically null components.  With k = n (train-v5.py:540-545 sets n_components to the
+// face count) the centred data has rank n - 1 and the last eigenvalue is rounding noise:
+// the Gram path's back-projection A^T.u of its eigenvector is itself rounding noise, and
+// normalising it would give an arbitrary direction with large projections.  In exact
+// arithmetic any unit vector orthogonal to the data span is a valid component (sklearn's
+// full SVD returns LAPACK's choice); this takes a fixed one: a seeded vector, made
+// orthogonal (two Gram-Schmidt passes) to every other component, unit length, svd_flip
+// sign rule.  Rare and small (k x d), so on the host.
+int complete_null_components(ef_ctx* c, int64_t n, int64_t d, int kk, const double* lam_dev, double* comps_dev,
+                             double* En_dev) {
+  hipStream_t s = c->stream;
+  std::vector<double> lam(kk);
+  EF_HIP(c, hipMemcpyAsync(lam.data(), lam_dev, kk * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  const double tol = 1e-14 * (double)std::max(n, d) * std::fabs(lam[0]);
+  std::vector<int> null_cols;
+  for (int j = 0; j < kk; ++j)
+    if (!(lam[j] > tol)) null_cols.push_back(j);
+  if (null_cols.empty() || (int)null_cols.size() == kk) return EF_OK;
+  std::vector<double> C((size_t)kk * d);
+  EF_HIP(c, hipMemcpyAsync(C.data(), comps_dev, C.size() * sizeof(double), hipMemcpyDeviceToHost, s), "D2H comps");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  std::vector<char> done(kk, 0);
+  for (int j = 0; j < kk; ++j) done[j] = lam[j] > tol;
+  unsigned long long st = 0x9e3779b97f4a7c15ULL;
+  for (int j : null_cols) {
+    double* v = &C[(size_t)j * d];
+    for (int64_t i = 0; i < d; ++i) {  // splitmix64 -> uniform(-1, 1)
+      st += 0x9e3779b97f4a7c15ULL;
+      unsigned long long z = st;
+      z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+      z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+      z ^= z >> 31;
+      v[i] = (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    }
+    for (int pass = 0; pass < 2; ++pass)
+      for (int q = 0; q < kk; ++q) {
+        if (!done[q]) continue;
+        const double* u = &C[(size_t)q * d];
+        double dot = 0.0;
+        for (int64_t i = 0; i < d; ++i) dot += u[i] * v[i];
+        for (int64_t i = 0; i < d; ++i) v[i] -= dot * u[i];
+      }
+    double nrm = 0.0, mx = -1.0;
+    int64_t mi = 0;
+    for (int64_t i = 0; i < d; ++i) {
+      nrm += v[i] * v[i];
+      if (std::fabs(v[i]) > mx) mx = std::fabs(v[i]), mi = i;
+    }
+    const double f = (v[mi] < 0 ? -1.0 : 1.0) / std::sqrt(nrm);
+    for (int64_t i = 0; i < d; ++i) v[i] *= f;
+    done[j] = 1;
+  }
+  std::vector<double> T((size_t)d * kk);
+  for (int j = 0; j < kk; ++j)
+    for (int64_t i = 0; i < d; ++i) T[(size_t)i * kk + j] = C[(size_t)j * d + i];
+  EF_HIP(c, hipMemcpyAsync(comps_dev, C.data(), C.size() * sizeof(double), hipMemcpyHostToDevice, s), "H2D comps");
+  EF_HIP(c, hipMemcpyAsync(En_dev, T.data(), T.size() * sizeof(double), hipMemcpyHostToDevice, s), "H2D En");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  return EF_OK;
+}
+
 }  // namespace
 
 extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint32_t flags,
@@ -491,6 +553,7 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   } else {
     EF_HIP(c, launch_normalize_sign(s, U, d, kk, kk, comps, En), "normalize");
   }
+  EF_TRY(complete_null_components(c, n, d, kk, lam, comps, En));
   // training projection A.E (projected_data / fit_transform output)
   if (proj_out) {
     EF_TRY(B.get(c, (size_t)n * kk, &proj));

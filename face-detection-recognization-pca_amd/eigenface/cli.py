@@ -8,9 +8,11 @@
         useless/train.py train_single_model (:225-276): sorted images of DIR ->
         models/NAME[_V]_pca_model.pkl + _model_info.json + JPGs
 
-To drop into a reference checkout, a two-line ``train-v4.py`` shim is enough:
-``import sys; sys.path.insert(0, "<repo>/face-detection-recognization-pca_amd")`` and
-``from eigenface.cli import main_train_v4 as main; main()``.
+    python -m eigenface.cli train-v5 [--base-dir faces/lock_version]
+        train-v5.py main (:570-610): one full-rank model per person directory
+
+The reference-named entry files ``face-detection-recognization-pca_amd/dropin/train-v4.py``
+and ``train-v5.py`` wrap these for unchanged callers (run_pipeline.py:234).
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ import numpy as np
 
 
 def train_v4(person, root="."):
+    """train-v4.py main (:268-312); returns True when a model was written."""
     from .compat import FaceTrainer
 
     json_path = os.path.join(root, f"faces/lock_version/{person}/{person}_faces_detection.json")
@@ -30,19 +33,22 @@ def train_v4(person, root="."):
     if not os.path.exists(json_path):
         print(f"Error: JSON file {json_path} not found!")
         print("Please run detection-v2.py first to generate face data.")
-        return 1
+        return False
     tr = FaceTrainer(n_components=50)
     if tr.load_face_images(json_path, face_dir) == 0:
         print("No valid face images found!")
-        return 1
-    tr.assign_labels_interactive(person)
+        return False
+    if len(tr.assign_labels_interactive(person)) == 0:
+        print("No faces labeled, training cancelled.")
+        return False
     if not tr.train_pca_model():
         print("Training failed!")
-        return 1
+        return False
     tr.save_eigenfaces(face_dir, person)
     tr.save_model(model_path)
     print(f"\nTraining completed successfully!\nModel saved to: {model_path}")
-    return 0
+    print(f"Eigenfaces and mean face saved to: {face_dir}")
+    return True
 
 
 def train_manual(faces_dir, person, model_dir="models", version=None, n_components=50):
@@ -83,16 +89,24 @@ def main(argv=None):
     m.add_argument("--model-dir", default="models")
     m.add_argument("--version", default=None)
     m.add_argument("--k", type=int, default=50)
+    v5 = sub.add_parser("train-v5", help="train-v5.py drop-in (every person directory)")
+    v5.add_argument("--base-dir", default="faces/lock_version")
     a = ap.parse_args(argv)
     if a.cmd == "train":
-        return train_v4(a.person, a.root)
+        return 0 if train_v4(a.person, a.root) else 1
+    if a.cmd == "train-v5":
+        from .multi_person import main as v5_main
+        ok, failed = v5_main(a.base_dir)
+        return 0 if ok and not failed else 1
     return train_manual(a.faces_dir, a.person, a.model_dir, a.version, a.k)
 
 
 def main_train_v4():
+    """train-v4.py's command line; like the reference's main it exits 0 after printing
+    an error (run_pipeline.py:41 only sees crashes)."""
     ap = argparse.ArgumentParser(description="Train face recognition model using PCA")
     ap.add_argument("--person", required=True, help="Person name for training model")
-    sys.exit(train_v4(ap.parse_args().person))
+    train_v4(ap.parse_args().person)
 
 
 if __name__ == "__main__":

@@ -82,11 +82,16 @@ def _save_bgr_jpg(path, bgr):
         Image.fromarray(a[..., ::-1] if a.ndim == 3 else a).save(path, quality=95)
 
 
-def _save_jpg(path, arr2d):
-    """cv2.normalize(NORM_MINMAX, 0..255, CV_8U) + imwrite (train-v4.py:164-177)."""
+def _save_jpg(path, arr2d, truncate=False):
+    """cv2.normalize(NORM_MINMAX, 0..255, CV_8U) + imwrite (train-v4.py:164-177); with
+    ``truncate`` the float normalize + astype(uint8) of useless/train.py:205-216."""
     a = np.asarray(arr2d, dtype=np.float64)
     lo, hi = a.min(), a.max()
-    u8 = np.zeros(a.shape, np.uint8) if hi == lo else np.rint((a - lo) * (255.0 / (hi - lo))).astype(np.uint8)
+    if hi == lo:
+        u8 = np.zeros(a.shape, np.uint8)
+    else:
+        v = (a - lo) * (255.0 / (hi - lo))
+        u8 = (np.floor(v) if truncate else np.rint(v)).astype(np.uint8)
     try:
         import cv2
         cv2.imwrite(path, u8)
@@ -313,10 +318,11 @@ def save_pca_model(eigenfaces, mean_face, projected_data, eigenvalues, filenames
 def visualize_eigenfaces(eigenfaces, mean_face, output_dir, person_name, n_display=10):
     """Mean face + top eigenfaces as min-max JPGs (useless/train.py:194-223)."""
     side = int(np.sqrt(len(mean_face)))
-    _save_jpg(os.path.join(output_dir, f"{person_name}_mean_face.jpg"), np.asarray(mean_face).reshape(side, side))
+    _save_jpg(os.path.join(output_dir, f"{person_name}_mean_face.jpg"), np.asarray(mean_face).reshape(side, side),
+              truncate=True)
     for i in range(min(n_display, eigenfaces.shape[1])):
         _save_jpg(os.path.join(output_dir, f"{person_name}_eigenface_{i + 1:02d}.jpg"),
-                  eigenfaces[:, i].reshape(side, side))
+                  eigenfaces[:, i].reshape(side, side), truncate=True)
 
 
 # ------------------------------------------------------------------ scanner

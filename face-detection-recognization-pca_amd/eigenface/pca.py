@@ -146,7 +146,9 @@ def manual_pca(data_matrix, n_components=None, device=0):
     if n_components is None:
         n_components = min(n - 1, d)
     r = get_engine(device).fit(x, n_components, standardize=False)
-    return np.ascontiguousarray(r.components.T), r.mean, r.projection, r.eigenvalues
+    # (d, k) Fortran-ordered like the reference's faces[:, order][:, :k] (the layout of
+    # the committed models/*_pca_model.pkl)
+    return r.components.T, r.mean, r.projection, r.eigenvalues
 
 
 # ------------------------------------------------------------------ recognize

@@ -196,7 +196,69 @@ def main():
 
     for k_, v in out.items():
         print(f"{k_}: {v:.3e}")
+    make_c1_synth(ref_train, ref_mscan)
+
+
+def make_c1_synth(ref_train=None, ref_mscan=None):
+    """G7: config 1 without photographs — an exact-integer synthetic stand-in of
+    faces/Light_version (229 x 100 x 100, so the GPU box regenerates identical pixels)
+    through the reference's own ``manual_pca`` (useless/train.py:56-128),
+    ``save_pca_model`` (:130-192: the pickle dict is captured in memory — nothing is
+    unpickled — and the info JSON read back) and ``recognize_face`` (useless/scan.py:
+    100-132)."""
+    import tempfile
+    sys.modules.setdefault("cv2", _cv2_placeholder())
+    ref_train = ref_train or _load("ref_manual_train", "useless/train.py")
+    ref_mscan = ref_mscan or _load("ref_manual_scan", "useless/scan.py")
+    n, side, r, seed, k = 229, 100, 160, 7, 50
+    X = orc.int_synth_faces(n, side, r=r, seed=seed)
+    eig, mean, proj, lam = ref_train.manual_pca(X.astype(np.float64), n_components=k)
+    captured = {}
+
+    class _Pickle:
+        @staticmethod
+        def dump(obj, f, *a, **kw):
+            captured["md"] = obj
+
+    real_pickle = ref_train.pickle
+    ref_train.pickle = _Pickle
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            names = [f"img_{i:03d}.png" for i in range(n)]
+            ref_train.save_pca_model(eig, mean, proj, lam, names, "synth", td, "light")
+            info = json.load(open(os.path.join(td, "synth_light_model_info.json")))
+    finally:
+        ref_train.pickle = real_pickle
+    md = captured["md"]
+
+    def describe(v):
+        if isinstance(v, np.ndarray):
+            return {"type": "ndarray", "dtype": str(v.dtype), "shape": list(v.shape),
+                    "f_contiguous": bool(v.flags.f_contiguous), "c_contiguous": bool(v.flags.c_contiguous)}
+        return {"type": type(v).__name__}
+
+    layout = {"pkl": {key: describe(v) for key, v in md.items()}, "info_keys": sorted(info)}
+    # probes: training rows, rows + integer noise, a flat face, the mean face (~0 projection)
+    rng = np.random.default_rng([seed, 2])
+    noisy = np.clip(X[[10, 200]].astype(np.int64) + rng.integers(-12, 13, (2, X.shape[1])), 0, 255)
+    flat = np.full((1, X.shape[1]), 128)
+    probes = np.concatenate([X[[0, 50, 100]], noisy, flat, np.rint(mean)[None, :]]).astype(np.uint8)
+    res = [ref_mscan.recognize_face(v.astype(np.float64), md, 0.7) for v in probes]
+    R = np.random.default_rng([5]).integers(0, 2, size=(X.shape[1], 8)).astype(np.float64) * 2.0 - 1.0
+    sgn = np.sign(eig[np.argmax(np.abs(eig), axis=0), np.arange(k)])  # max-|.|-positive storage convention
+    np.savez_compressed(
+        os.path.join(HERE, "c1_synth.npz"),
+        n=n, side=side, r=r, seed=seed, k=k,
+        eigenvalues=lam, eigenfaces_R=(eig * sgn[None, :]).T @ R, projected=proj * sgn[None, :],
+        mean_sum=mean.sum(), evr_json=np.array(info["explained_variance_ratio"]),
+        layout=json.dumps(layout), probes=probes,
+        sim=np.array([float(x[1]) for x in res]), recognized=np.array([bool(x[2]) for x in res]),
+    )
+    print("c1_synth: eigenvalues", lam[:3], "sims", [round(float(x[1]), 6) for x in res])
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "c1":
+        make_c1_synth()
+    else:
+        main()

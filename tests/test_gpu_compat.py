@@ -33,8 +33,8 @@ def test_train_v4_cli_and_pickle(tmp_path):
     from eigenface import recognize_face_with_model
     xa = _person_dir(str(tmp_path), "alice", 120, 1)
     xb = _person_dir(str(tmp_path), "bob", 90, 2)
-    assert train_v4("alice", str(tmp_path)) == 0
-    assert train_v4("bob", str(tmp_path)) == 0
+    assert train_v4("alice", str(tmp_path)) is True
+    assert train_v4("bob", str(tmp_path)) is True
     base = tmp_path / "faces" / "lock_version"
     for p in ("alice", "bob"):
         assert (base / p / "face_model.pkl").exists()
@@ -133,3 +133,84 @@ def test_engine_owner_tokens_interleaved_models():
     g[7] = -g[7]  # in-place edit of the same array: the digest forces a re-upload
     pid, _, _ = recognize_face_with_model(g[7], md, threshold=0.5)
     assert pid == 7
+
+
+def _describe(v):
+    if isinstance(v, np.ndarray):
+        return {"type": "ndarray", "dtype": str(v.dtype), "shape": list(v.shape),
+                "f_contiguous": bool(v.flags.f_contiguous), "c_contiguous": bool(v.flags.c_contiguous)}
+    return {"type": type(v).__name__}
+
+
+def test_config1_synthetic_manual_path_vs_reference(tmp_path):
+    """BASELINE config 1 without photographs: an exact-integer synthetic stand-in of
+    faces/Light_version (229 faces, 100 x 100) through cli.train_manual (useless/train.py
+    train_single_model: sorted files -> manual_pca k=50 -> models/*_pca_model.pkl +
+    *_model_info.json) and recognize_face, against the reference's own manual_pca,
+    save_pca_model and recognize_face outputs (tests/golden/make_goldens.py c1)."""
+    from PIL import Image
+    from conftest import golden
+    from eigenface import recognize_face, recognize_faces
+    from eigenface.cli import train_manual
+    g = golden("c1_synth.npz")
+    X = orc.int_synth_faces(int(g["n"]), int(g["side"]), r=int(g["r"]), seed=int(g["seed"]))
+    d = tmp_path / "Light_version"
+    d.mkdir()
+    side = int(g["side"])
+    for i, row in enumerate(X):
+        Image.fromarray(row.reshape(side, side), mode="L").save(d / f"img_{i:03d}.png")
+    assert train_manual(str(d), "synth", str(tmp_path / "models"), "light", int(g["k"])) == 0
+    md = pickle.load(open(tmp_path / "models" / "synth_light_pca_model.pkl", "rb"))  # written by this package
+    info = json.load(open(tmp_path / "models" / "synth_light_model_info.json"))
+    layout = json.loads(str(g["layout"]))
+    assert {k: _describe(v) for k, v in md.items()} == layout["pkl"]
+    assert sorted(info) == layout["info_keys"]
+    assert md["training_filenames"][:2] == ["img_000.png", "img_001.png"] and md["version"] == "light"
+    np.testing.assert_allclose(md["eigenvalues"], g["eigenvalues"], rtol=1e-9)
+    np.testing.assert_allclose(info["explained_variance_ratio"], g["evr_json"], rtol=1e-9)
+    np.testing.assert_allclose(md["mean_face"].sum(), float(g["mean_sum"]), rtol=1e-14)
+    R = np.random.default_rng([5]).integers(0, 2, size=(X.shape[1], 8)).astype(np.float64) * 2.0 - 1.0
+    er = md["eigenfaces"].T @ R
+    s = np.sign((er * g["eigenfaces_R"]).sum(axis=1))
+    np.testing.assert_allclose(er * s[:, None], g["eigenfaces_R"], atol=1e-4)
+    proj = md["projected_data"] * s[None, :]
+    np.testing.assert_allclose(proj, g["projected"], atol=1e-6 * np.abs(g["projected"]).max())
+    # recognise (useless/scan.py:100-132) one by one and batched
+    sims = []
+    for p, want_sim, want_ok in zip(g["probes"], g["sim"], g["recognized"]):
+        name, sim, ok = recognize_face(p.astype(np.float64), md, 0.7)
+        assert name == "synth" and ok == bool(want_ok)
+        sims.append(sim)
+    # fp32 projection: |f32 - f| <= 2e-6 * sum|p - mu||w| per component (the K6 bound,
+    # tests/test_gpu_project.py); the cosine moves by at most 2 |df| / |f| — large only for
+    # the mean-face probe, whose projection is nearly all cancellation
+    P = g["probes"].astype(np.float64) - md["mean_face"]
+    f = P @ md["eigenfaces"]
+    df = 2e-6 * (np.abs(P) @ np.abs(md["eigenfaces"]))
+    tol = 2 * np.linalg.norm(df, axis=1) / np.linalg.norm(f, axis=1) + 1e-6
+    assert np.all(np.abs(np.array(sims) - g["sim"]) <= tol)
+    batch = recognize_faces(g["probes"], md, 0.7)
+    np.testing.assert_allclose([b[1] for b in batch], sims, atol=1e-6)
+
+
+def test_dual_model_recognition_matches_reference_rule():
+    """recognize_face_dual_model (useless/scan.py:134-166): OR of the two models'
+    decisions, max similarity, the dark model's name on ties; against the oracle's
+    single-model recognise per model."""
+    from eigenface import manual_pca, recognize_face_dual_model
+    xd = orc.int_synth_faces(120, 24, r=40, seed=11)
+    xl = orc.int_synth_faces(140, 24, r=40, seed=12)
+    models = []
+    for nm, x in (("dark", xd), ("light", xl)):
+        e, m, p, lam = manual_pca(x, 20)
+        models.append({"eigenfaces": e, "mean_face": m, "projected_data": p, "person_name": f"joe_{nm}"})
+    rng = np.random.default_rng(1)
+    probes = np.concatenate([xd[:3], xl[:3], rng.integers(0, 256, (2, xd.shape[1]))]).astype(np.uint8)
+    for v in probes:
+        got = recognize_face_dual_model(v, models[0], models[1], 0.7)
+        rd = orc.recognize_face_manual(v, models[0], 0.7)
+        rl = orc.recognize_face_manual(v, models[1], 0.7)
+        assert got[2] == (rd[2] or rl[2])
+        assert got[0] == (rd[0] if rd[1] >= rl[1] else rl[0]) or abs(rd[1] - rl[1]) < 1e-6
+        np.testing.assert_allclose(got[3:], [rd[1], rl[1]], atol=2e-6)
+        np.testing.assert_allclose(got[1], max(rd[1], rl[1]), atol=2e-6)
