@@ -242,7 +242,6 @@ void ef_destroy(ef_ctx* c) {
   for (DevBuf* b : bufs) release(*b);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
-  blas_release(c);
   tm_release(c);
   haar_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -15,8 +15,6 @@
 //     — the top-k pairs are all manual_pca keeps (:114-116) and all sklearn reports
 //     (explained_variance_ratio_ uses trace(C) as the total, _pca.py:644-646);
 //   * eigenfaces: E = A^T.U (:91), unit columns (:94-95), sklearn svd_flip sign rule.
-#include <rocblas/rocblas.h>
-
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -24,13 +22,6 @@
 #include <vector>
 
 #include "ef_linalg.hpp"
-
-namespace ef {
-void blas_release(ef_ctx* c) {
-  if (c->blas) (void)rocblas_destroy_handle(static_cast<rocblas_handle>(c->blas));
-  c->blas = nullptr;
-}
-}  // namespace ef
 
 namespace {
 
@@ -64,38 +55,21 @@ struct Bufs {
     if (_e != hipSuccess) return hip_err(ctx, _e, what); \
   } while (0)
 
-// Plain dense fp64 products of the subspace iteration (C.Q, Y^T.Y, Y.W: no operand
-// transformation to fuse) go to rocBLAS dgemm; the pixel-operand products keep gemm64.
-// EF_FIT_GEMM=own forces gemm64 everywhere (A/B comparisons).
+// Plain dense fp64 products of the subspace iteration with a large output (C.Q, Y.V, Q.V)
+// run on the tall matrix-core GEMM (ef_dgemm.hip), which takes B transposed: B^T is
+// written into bt_scratch (>= K x N doubles) first — at most dim x m, 32 MiB at C3, a few
+// microseconds.  Products with a small output over a long K (Y^T.Y, Q^T.Y) and the
+// pixel-operand products keep gemm64's split-K.
 hipError_t dense_gemm(ef_ctx* c, hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
-                      double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
-#ifdef EF_DIAGNOSTICS
-  static const bool own = [] {
-    const char* e = getenv("EF_FIT_GEMM");
-    return e && std::string(e) == "own";
-  }();
-#else
-  constexpr bool own = false;
-#endif
-  // rocBLAS for large outputs; small outputs over long K (Y^T.Y, Q^T.Y) keep gemm64's
-  // split-K (a 256 x 256 output is only 4 rocBLAS tiles)
+                      double alpha, double* C, int64_t ldc, double* work, size_t work_elems,
+                      double* bt_scratch = nullptr) {
+  (void)c;
   const bool small_out = M * N <= (int64_t)512 * 512 && K >= 4096;
-  if (!own && !A.u8 && !B.u8 && !small_out) {
-    if (!c->blas) {
-      rocblas_handle h = nullptr;
-      if (rocblas_create_handle(&h) == rocblas_status_success) c->blas = h;
-    }
-    if (c->blas) {
-      rocblas_handle h = static_cast<rocblas_handle>(c->blas);
-      const double beta = 0.0;
-      // row-major C = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
-      if (rocblas_set_stream(h, s) == rocblas_status_success &&
-          rocblas_dgemm(h, B.trans ? rocblas_operation_transpose : rocblas_operation_none,
-                        A.trans ? rocblas_operation_transpose : rocblas_operation_none, (rocblas_int)N,
-                        (rocblas_int)M, (rocblas_int)K, &alpha, B.p, (rocblas_int)B.ld, A.p, (rocblas_int)A.ld, &beta,
-                        C, (rocblas_int)ldc) == rocblas_status_success)
-        return hipGetLastError();
-    }
+  if (bt_scratch && !A.u8 && !B.u8 && !A.trans && !B.trans && !small_out && tall_gemm_supported(A.ld, A.p, 8) &&
+      tall_gemm_supported(K, bt_scratch, 8)) {
+    hipError_t e = launch_transpose_f64(s, B.p, B.ld, K, N, bt_scratch, K);
+    if (e != hipSuccess) return e;
+    return tall_gemm_f64(s, A.p, A.ld, false, bt_scratch, K, C, ldc, M, N, K, alpha, work, work_elems);
   }
   return gemm64(s, A, B, M, N, K, alpha, C, ldc, work, work_elems);
 }
@@ -142,34 +116,6 @@ struct SmallEig {
   }
 };
 
-// Y[r][:] <- Y[r][:] L^-T (forward substitution per row; used only without rocBLAS).
-__global__ void trsm_rows_kernel(double* __restrict__ Y, int64_t rows, int m, const double* __restrict__ L) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= rows) return;
-  double* y = Y + r * m;
-  for (int j = 0; j < m; ++j) {
-    double v = y[j];
-    for (int l = 0; l < j; ++l) v -= y[l] * L[(int64_t)j * m + l];
-    y[j] = v / L[(int64_t)j * m + j];
-  }
-}
-
-// Q <- Y L^-T in place (row-major Y: dim x m; L row-major lower m x m).
-hipError_t tri_solve_right(ef_ctx* c, hipStream_t s, double* Y, int64_t dim, int m, const double* L) {
-  if (c->blas) {
-    rocblas_handle h = static_cast<rocblas_handle>(c->blas);
-    const double one = 1.0;
-    // column-major view: Y^T (m x dim); L row-major lower == column-major upper L^T
-    if (rocblas_set_stream(h, s) == rocblas_status_success &&
-        rocblas_dtrsm(h, rocblas_side_left, rocblas_fill_upper, rocblas_operation_transpose,
-                      rocblas_diagonal_non_unit, (rocblas_int)m, (rocblas_int)dim, &one, L, (rocblas_int)m, Y,
-                      (rocblas_int)m) == rocblas_status_success)
-      return hipGetLastError();
-  }
-  hipLaunchKernelGGL(trsm_rows_kernel, dim3((unsigned)((dim + 255) / 256)), dim3(256), 0, s, Y, dim, m, L);
-  return hipGetLastError();
-}
-
 // Wide-block subspace iteration (m > kJacobiMax): orthonormalise by CholQR every
 // iteration (G = Y^T.Y = L.L^T, Q = Y.L^-T — one small Cholesky instead of an m x m
 // eigensolve), Rayleigh-Ritz (H = Q^T.C.Q, block Jacobi) at iterations (1, 2, 4,) 8 and every
@@ -197,24 +143,16 @@ static void cvt32to64(hipStream_t s, const float* a, int64_t n, double* b) {
   hipLaunchKernelGGL(f32_to_f64_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
                      b);
 }
-// Y32 (dim x m) = C32 (dim x dim) . Q32 (dim x m), row-major, rocBLAS sgemm.
-static bool sgemm_cq(ef_ctx* c, hipStream_t s, const float* C32, const float* Q32, int64_t dim, int m, float* Y32) {
-  if (!c->blas) return false;
-  rocblas_handle h = static_cast<rocblas_handle>(c->blas);
-  const float one = 1.f, zero = 0.f;
-  return rocblas_set_stream(h, s) == rocblas_status_success &&
-         rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, (rocblas_int)m, (rocblas_int)dim,
-                       (rocblas_int)dim, &one, Q32, (rocblas_int)m, C32, (rocblas_int)dim, &zero, Y32,
-                       (rocblas_int)m) == rocblas_status_success;
-}
 
 int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int m, double* work, double* U_out,
                   double* lam_out, int* iters) {
   hipStream_t s = c->stream;
   SmallEig se;
   EF_TRY(se.init(c, B, m));
-  double *Q, *Y, *Y2, *G, *V, *W2, *lam;
+  double *Q, *Y, *Y2, *G, *V, *W2, *Li, *Bt, *lam;
   int* cinfo;
+  EF_TRY(B.get(c, (size_t)m * m, &Li));
+  EF_TRY(B.get(c, (size_t)dim * m, &Bt));
   EF_TRY(B.get(c, (size_t)dim * m, &Q));
   EF_TRY(B.get(c, (size_t)dim * m, &Y));
   EF_TRY(B.get(c, (size_t)dim * m, &Y2));
@@ -236,9 +174,16 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       EF_HIP(c, hipMemcpyAsync(&hinfo, cinfo, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
     }
-    if (hinfo == 0) {
-      EF_HIP(c, tri_solve_right(c, s, Y, dim, m, G), "Q = Y.L^-T");
-      std::swap(Q, Y);
+    if (hinfo == 0) {  // Q = Y . L^-T: explicit inverse of the m x m factor (it IS (L^-T)^T), one GEMM
+      EF_HIP(c, launch_tri_inv(s, G, m, Li), "L^-1");
+      if (tall_gemm_supported(m, Y, 8)) {
+        EF_HIP(c, tall_gemm_f64(s, Y, m, false, Li, m, Q, m, dim, m, m, 1.0, work, kWorkElems), "Q = Y.L^-T");
+      } else {  // odd row pitch: generic GEMM on L^-T written out
+        EF_HIP(c, launch_transpose_f64(s, Li, m, m, m, Bt, m), "L^-T");
+        EF_HIP(c, gemm64(s, Operand::dense(Y, m, false), Operand::dense(Bt, m, false), dim, m, m, 1.0, Q, m, work,
+                         kWorkElems),
+               "Q = Y.L^-T");
+      }
       return EF_OK;
     }
     // rank-deficient block: eigen-orthonormalisation with a floored spectrum
@@ -248,7 +193,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(G)"));
     EF_HIP(c, launch_scale_cols_rsqrt(s, V, m, m, lam, W2), "W.L^-1/2");
     EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(W2, m, false), dim, m, m, 1.0, Q, m, work,
-                         kWorkElems),
+                         kWorkElems, Bt),
            "Q = Y.W");
     return EF_OK;
   };
@@ -259,10 +204,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   // rate); the iteration is self-correcting, and convergence is only declared between two
   // Rayleigh-Ritz steps that both follow fp64 products, so the result is the fp64 one.
   float *C32 = nullptr, *Q32 = nullptr, *Y32 = nullptr;
-  bool coarse = dim >= 4096 && c->blas != nullptr && c->opt_fit_fp32_coarse != 0;
+  bool coarse = dim >= 4096 && c->opt_fit_fp32_coarse != 0 && tall_gemm_supported(dim, C, 8);
   if (coarse) {
     EF_TRY(B.get(c, (size_t)dim * dim, &C32));
-    EF_TRY(B.get(c, (size_t)dim * m, &Q32));
+    EF_TRY(B.get(c, (size_t)dim * m, &Q32));  // Q^T in fp32 (the GEMM's transposed B)
     EF_TRY(B.get(c, (size_t)dim * m, &Y32));
     cvt64to32(s, C, dim * dim, C32);
   }
@@ -275,12 +220,14 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   for (it = 1; it <= max_iters; ++it) {
     const bool fine = !coarse;  // this iteration's product is fp64
     if (coarse) {
-      cvt64to32(s, Q, dim * m, Q32);
-      if (!sgemm_cq(c, s, C32, Q32, dim, m, Y32)) return set_err(c, EF_E_HIP, "Y = C.Q (sgemm)");
+      EF_HIP(c, launch_transpose_f64_to_f32(s, Q, m, dim, m, Q32, dim), "Q^T (fp32)");
+      EF_HIP(c, tall_gemm_f32(s, C32, dim, false, Q32, dim, Y32, m, dim, m, dim, 1.f, reinterpret_cast<float*>(work),
+                              kWorkElems * 2),
+             "Y = C.Q (fp32)");
       cvt32to64(s, Y32, dim * m, Y);
     } else {
-      EF_HIP(c, dense_gemm(c, s, Operand::dense(C, dim, false), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m,
-                           work, kWorkElems),
+      EF_HIP(c, dense_gemm(c, s, Operand::symmetric(C, dim), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
+                           kWorkElems, Bt),
              "Y = C.Q");
     }
     // Rayleigh-Ritz at iterations 1, 2, 4 (small orders only: there they re-order the block
@@ -324,7 +271,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       // LAPACK either converges or raises LinAlgError; train-v4.py:114-120 returns False)
       if (ok || it == max_iters) {
         EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
-                             kk, work, kWorkElems),
+                             kk, work, kWorkElems, Bt),
                "U = Q.V");
         EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
         EF_HIP(c, hipStreamSynchronize(s), "sync");
@@ -332,7 +279,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       }
       // continue from the Ritz basis: C.(Q.V) = Y.V
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(V, m, false), dim, m, m, 1.0, Y2, m,
-                           work, kWorkElems),
+                           work, kWorkElems, Bt),
              "Y.V");
       std::swap(Y, Y2);
     }

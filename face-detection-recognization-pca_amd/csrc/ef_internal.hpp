@@ -108,7 +108,6 @@ struct ef_ctx {
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
-  void* blas = nullptr;  // rocBLAS handle (fit's plain dense products), lazily created
 
   // multi-GPU: RCCL communicator (ef_comm_init), null when single-rank
   void* comm = nullptr;
@@ -126,7 +125,6 @@ struct ef_ctx {
 namespace ef {
 
 int set_err(ef_ctx* c, int code, const std::string& msg);
-void blas_release(ef_ctx* c);
 void tm_release(ef_ctx* c);
 void haar_release(ef_ctx* c);
 int hip_err(ef_ctx* c, hipError_t e, const char* what);

@@ -41,8 +41,14 @@ struct Operand {
   const uint8_t* x = nullptr;
   int64_t ld = 0;
   int trans = 0;
+  bool sym = false;  // symmetric: either orientation may be read (tall GEMM walks its rows)
   const double* mu = nullptr;
   const double* w = nullptr;
+  static Operand symmetric(const double* p, int64_t ld) {
+    Operand o = dense(p, ld, false);
+    o.sym = true;
+    return o;
+  }
   static Operand dense(const double* p, int64_t ld, bool trans) {
     Operand o;
     o.p = p;
@@ -67,6 +73,26 @@ hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, 
                   double alpha, double* C, int64_t ldc, double* work, size_t work_elems);
 
 size_t jacobi_lds_bytes(int m);
+
+// Tall dense GEMMs on the matrix cores (ef_dgemm.hip): C[M x N] = alpha A[M x K] B[K x N]
+// with B given TRANSPOSED (Bt: N x K, row-major, ldbt) and A row-major or, with a_trans,
+// stored transposed (element (i, k) at A[k * lda + i]; a symmetric A either way); N <= 512
+// intended; work: split-K slabs (M*N*splits elements, may be null).  Rows of A (a_trans:
+// of A^T) and of Bt must be 16-byte aligned (tall_gemm_supported).
+bool tall_gemm_supported(int64_t ld, const void* p, int elem_bytes);
+hipError_t tall_gemm_f64(hipStream_t s, const double* A, int64_t lda, bool a_trans, const double* Bt, int64_t ldbt,
+                         double* C, int64_t ldc, int64_t M, int64_t N, int64_t K, double alpha, double* work,
+                         size_t work_elems);
+hipError_t tall_gemm_f32(hipStream_t s, const float* A, int64_t lda, bool a_trans, const float* Bt, int64_t ldbt,
+                         float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float* work,
+                         size_t work_elems);
+// out (cols x rows, ldout) = in (rows x cols, ldin)^T; the second also converts to fp32
+hipError_t launch_transpose_f64(hipStream_t s, const double* in, int64_t ldin, int64_t rows, int64_t cols, double* out,
+                                int64_t ldout);
+hipError_t launch_transpose_f64_to_f32(hipStream_t s, const double* in, int64_t ldin, int64_t rows, int64_t cols,
+                                       float* out, int64_t ldout);
+// Li = L^-1 for a lower-triangular m x m L (m <= 512), row-major
+hipError_t launch_tri_inv(hipStream_t s, const double* L, int m, double* Li);
 hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, double* evals, double* evecs,
                          int64_t ldv, int max_sweeps, int* info);
 // Grid-parallel Jacobi for any order (ef_jacobi_big.hip): one hipGraph per sweep, built
