@@ -130,14 +130,17 @@ static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t b
     return EF_OK;
   }
   int64_t pps = 0;
-  const int ns = c->bf16 ? project_bf16_nsplit(bpad, c->d, c->kpw, &pps) : project_nsplit(bpad, c->d, c->kpw, &pps);
+  const uint8_t* mu8 = c->mean_u8_ok ? static_cast<const uint8_t*>(c->mean_u8.p) : nullptr;
+  const int ns = c->bf16 ? project_bf16_nsplit(dtype, P, mu8, bpad, c->d, c->kpw, &pps)
+                         : project_nsplit(bpad, c->d, c->kpw, &pps);
   EF_TRY(ensure(c, c->proj_part, (size_t)ns * bpad * c->kpw * sizeof(float)));
   TimerEvt t;
   timer_begin(c, EF_KERNEL_PROJECT, &t);
   if (c->bf16) {
     EF_HIP(c,
            launch_project_bf16(c->stream, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean_r.p),
-                               static_cast<const unsigned short*>(c->W16.p), c->kpw,
+                               mu8, static_cast<const unsigned short*>(c->W16.p),
+                               c->kpw,
                                static_cast<float*>(c->proj_part.p), ns, pps),
            "project kernel (bf16)");
   } else {
@@ -236,7 +239,7 @@ void ef_destroy(ef_ctx* c) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
-  DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->corr,      &c->G,
+  DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->mean_u8,   &c->corr,      &c->G,
                     &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev};
   for (DevBuf* b : bufs) release(*b);
@@ -312,9 +315,23 @@ int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_
     e = launch_bf16_model(c->stream, static_cast<const float*>(c->W.p), static_cast<const float*>(c->mean.p), d, ldw,
                           static_cast<unsigned short*>(c->W16.p), static_cast<float*>(c->mean_r.p),
                           static_cast<float*>(c->corr.p), static_cast<double*>(cp.p), nchunk);
+    int bad = 1;
+    int* bad_dev = reinterpret_cast<int*>(static_cast<char*>(c->mean_u8.p));
+    if (e == hipSuccess) {
+      const size_t off = ((size_t)d + 255) & ~size_t(255);
+      const int rc = ensure(c, c->mean_u8, off + 16);
+      if (rc != EF_OK) { release(cp); return rc; }
+      bad_dev = reinterpret_cast<int*>(static_cast<char*>(c->mean_u8.p) + off);
+      e = hipMemsetAsync(bad_dev, 0, sizeof(int), c->stream);
+      if (e == hipSuccess)
+        e = launch_mean_u8(c->stream, static_cast<const float*>(c->mean_r.p), d, static_cast<uint8_t*>(c->mean_u8.p),
+                           bad_dev);
+      if (e == hipSuccess) e = hipMemcpyAsync(&bad, bad_dev, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     release(cp);
     if (e != hipSuccess) return hip_err(c, e, "bf16 model");
+    c->mean_u8_ok = bad == 0;
   }
   c->bf16 = bf16;
   c->d = d;

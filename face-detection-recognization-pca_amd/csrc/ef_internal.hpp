@@ -85,6 +85,8 @@ struct ef_ctx {
   bool bf16 = false;   // EF_MODEL_BF16: project with W16 on bf16 MFMA
   ef::DevBuf W16;      // bf16[kpw][d]
   ef::DevBuf mean_r;   // float[d] round(mean)
+  ef::DevBuf mean_u8;  // uint8[d] round(mean) (wide bf16 kernel) + int counter
+  bool mean_u8_ok = false;  // every round(mean) in 0..255
   ef::DevBuf corr;     // float[kpw] (mean - round(mean)).W
 
   // gallery
@@ -160,9 +162,11 @@ hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, i
 // bf16 model (EF_MODEL_BF16): W16 [kpw][d] bf16, round(mean), fp64-derived correction row
 hipError_t launch_bf16_model(hipStream_t s, const float* W, const float* mean, int64_t d, int ldw,
                              unsigned short* Wt16, float* mean_r, float* corr, double* corr_part, int nchunk);
-int project_bf16_nsplit(int64_t bpad, int64_t d, int ldw, int64_t* pix_per_split);
+int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int64_t bpad, int64_t d, int ldw,
+                        int64_t* pix_per_split);
 hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_t b, int64_t bpad, int64_t d,
-                               const float* mean_r, const unsigned short* Wt16, int ldw, float* part, int nsplit,
-                               int64_t pps);
+                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16, int ldw,
+                               float* part, int nsplit, int64_t pps);
+hipError_t launch_mean_u8(hipStream_t s, const float* mean_r, int64_t d, uint8_t* out, int* bad);
 
 }  // namespace ef

@@ -149,6 +149,163 @@ __global__ __launch_bounds__(256, 2) void project_bf16_kernel(const void* __rest
       }
 }
 
+// ---------------------------------------------------------------------------------
+// Wide form for uint8 probes (the config-5 shape: 4096 probes x 65536 pixels x k = 512).
+// The 128 x 128 kernel above converts every pixel once per 128-column tile with ~6 VALU
+// instructions per pixel and re-reads W for every 128 probes: it runs VALU-bound at ~9 %
+// of the bf16 peak.  Here a workgroup of 8 waves owns 256 probes x NT components (NT =
+// 256: each wave 64 x 128, eight 32x32 accumulators = 128 AGPRs), so each (probe, pixel)
+// is converted at most ldw / 256 times and each W element is read once per 256 probes:
+//   per 32-pixel stage: 8 KiB of uint8 pixels + NT x 64 B of W16 from L2 for 2 x 8
+//   MFMAs per wave (512 cycles per SIMD at 2 waves/SIMD) = 24 B/clk/CU at NT = 256;
+//   conversion p - round(mean) -> bf16 is exact for uint8 (|p - mr| <= 255) and costs
+//   ~2 VALU instructions per pixel: v_cvt_f32_ubyte, a packed subtract, a v_perm of the
+//   two high halves (bf16 truncation of an exactly representable value).
+// K splits over gridDim.y (fp32 slabs, the project_reduce_kernel contract); the grid is
+// XCD-aware: the workgroups of one K split are dealt to one XCD so that split's W and
+// probe slices stream through that XCD's L2 once.
+constexpr int WM = 256;  // probes per workgroup (wide form)
+constexpr int WKS = 64;  // pixels per stage (wide form)
+
+template <int NT, int WK>
+__global__ __launch_bounds__(512, 1) void project_bf16_wide_kernel(const uint8_t* __restrict__ P, int64_t b, int64_t d,
+                                                                   const uint8_t* __restrict__ mean_u8,
+                                                                   const unsigned short* __restrict__ Wt16, int ldw,
+                                                                   float* __restrict__ part, int64_t bpad,
+                                                                   int64_t pps, int mt, int nt, int ns) {
+  constexpr int WN = NT / 2;       // components per wave (4 x 2 waves)
+  constexpr int JB = WN / 32;      // 32-column blocks per wave
+  constexpr int WS = WK + 8;       // LDS row stride (bf16): 16-B pad keeps ds_read_b128 conflict-free
+  constexpr int PT = WK / 2;       // pixels per thread per stage (two threads per row)
+  constexpr int NV = PT / 16;      // uint4 of raw pixels per thread per stage
+  __shared__ __attribute__((aligned(16))) unsigned short sA[2][WM * WS];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[2][NT * WS];
+
+  // XCD-aware deal: consecutive block ids go round-robin over the 8 XCDs; give XCD x the
+  // contiguous run [x * per, (x + 1) * per) of (split, m-tile, n-tile) items, split-major
+  const int total = mt * nt * ns;
+  const int per = total / 8;  // host guarantees total % 8 == 0
+  const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int split = item / (mt * nt);
+  const int rem = item - split * (mt * nt);
+  const int mi = rem / nt, ni = rem - (rem / nt) * nt;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)mi * WM;
+  const int col0 = ni * NT;
+  const int64_t k_beg = (int64_t)split * pps;
+  const int64_t k_end = k_beg + pps < d ? k_beg + pps : d;
+  const int nsteps = (int)((k_end - k_beg) / WK);  // host guarantees whole stages
+
+  // staging: A: thread -> (probe row tid >> 1, 16-pixel half); B: NT / 256 (row, half) pairs.
+  // Register pipeline two stages deep: the raw pixels, round(mean) bytes and W16 of stage
+  // st + 2 are loaded while stage st's MFMAs run and stage st + 1 is converted into LDS,
+  // so each global load has two stages of MFMA time (~2k cycles) to arrive.
+  const int sr = tid >> 1, sh = (tid & 1) * PT;
+  const int64_t arow = m0 + sr;
+  const bool arow_ok = arow < b;
+  const uint8_t* pa = P + (arow_ok ? arow : 0) * d + sh;
+  constexpr int BR = NT >= 256 ? NT / 256 : 1;  // W (row, half) pairs per thread
+  const bool bload = NT >= 256 || tid < 2 * NT;   // NT = 128: the first 256 threads
+  struct Raw {
+    uint4 p[NV], m[NV], w[BR][2 * NV];
+  };
+  auto load_raw = [&](int step, Raw& r) {
+    const int64_t px0 = k_beg + (int64_t)step * WK;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      r.p[v] = arow_ok ? *reinterpret_cast<const uint4*>(pa + px0 + 16 * v) : make_uint4(0, 0, 0, 0);
+      r.m[v] = *reinterpret_cast<const uint4*>(mean_u8 + px0 + sh + 16 * v);
+    }
+    if (bload) {
+#pragma unroll
+      for (int q = 0; q < BR; ++q) {
+        const unsigned short* wrow = Wt16 + (int64_t)(col0 + sr + 256 * q) * d + px0 + sh;
+#pragma unroll
+        for (int v = 0; v < 2 * NV; ++v) r.w[q][v] = *reinterpret_cast<const uint4*>(wrow + 8 * v);
+      }
+    }
+  };
+  // p - round(mean) -> bf16 (exact: |p - mr| <= 255), the bf16 being the high half of the
+  // exactly representable fp32 value; stored with W16 into LDS buffer buf
+  auto convert_store = [&](const Raw& r, int buf) {
+#pragma unroll
+   for (int v = 0; v < NV; ++v) {
+    const unsigned pw[4] = {r.p[v].x, r.p[v].y, r.p[v].z, r.p[v].w};
+    const unsigned mw[4] = {r.m[v].x, r.m[v].y, r.m[v].z, r.m[v].w};
+    unsigned pk[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned w = pw[q], m = mw[q];
+      const float f0 = (float)(w & 0xffu) - (float)(m & 0xffu);
+      const float f1 = (float)((w >> 8) & 0xffu) - (float)((m >> 8) & 0xffu);
+      const float f2 = (float)((w >> 16) & 0xffu) - (float)((m >> 16) & 0xffu);
+      const float f3 = (float)(w >> 24) - (float)(m >> 24);
+      pk[2 * q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+      pk[2 * q + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+    }
+    // padded rows past b must be zero (their slab rows are summed like the others)
+    const uint4 a0 = arow_ok ? make_uint4(pk[0], pk[1], pk[2], pk[3]) : make_uint4(0, 0, 0, 0);
+    const uint4 a1 = arow_ok ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(&sA[buf][sr * WS + sh + 16 * v]) = a0;
+    *reinterpret_cast<uint4*>(&sA[buf][sr * WS + sh + 16 * v + 8]) = a1;
+   }
+    if (bload) {
+#pragma unroll
+      for (int q = 0; q < BR; ++q)
+#pragma unroll
+        for (int v = 0; v < 2 * NV; ++v) *reinterpret_cast<uint4*>(&sB[buf][(sr + 256 * q) * WS + sh + 8 * v]) = r.w[q][v];
+    }
+  };
+
+  f32x16 acc[2][JB];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) acc[i][j] = f32x16{};
+
+  Raw r0, r1;
+  if (nsteps > 0) load_raw(0, r0);
+  if (nsteps > 1) load_raw(1, r1);
+  if (nsteps > 0) convert_store(r0, 0);
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    // r1 holds stage st + 1 (loaded last iteration); refill r0 with stage st + 2
+    if (st + 2 < nsteps) load_raw(st + 2, r0);
+#pragma unroll
+    for (int s = 0; s < WK / 16; ++s) {  // lane (r, h) holds A[r][16s + 8h + j], B[16s + 8h + j][r]
+      bf16x8 a[2], w[JB];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 64 + i * 32 + c32) * WS + 16 * s + 8 * h]);
+#pragma unroll
+      for (int j = 0; j < JB; ++j)
+        w[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * WN + j * 32 + c32) * WS + 16 * s + 8 * h]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], w[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nsteps) convert_store(r1, buf ^ 1);
+    __syncthreads();
+    r1 = r0;
+  }
+
+  float* out = part + (int64_t)split * bpad * ldw + col0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[row * ldw + wn * WN + j * 32 + c32] = acc[i][j][r];
+      }
+}
+
 // Wt16[c][px] = bf16(W[px][c]) (32 x 32 tiles through LDS), mean_r = round(mean).
 __global__ void bf16_model_kernel(const float* __restrict__ W, const float* __restrict__ mean, int64_t d, int ldw,
                                   unsigned short* __restrict__ Wt16, float* __restrict__ mean_r) {
@@ -200,10 +357,45 @@ hipError_t launch_bf16_model(hipStream_t s, const float* W, const float* mean, i
   return hipGetLastError();
 }
 
-int project_bf16_nsplit(int64_t bpad, int64_t d, int ldw, int64_t* pix_per_split) {
+// The wide form needs uint8 probes, whole 32-pixel stages per split, 16-byte aligned rows.
+static bool bf16_wide_ok(int p_dtype, const void* P, int64_t d, int ldw, const uint8_t* mean_u8) {
+  return mean_u8 && p_dtype == EF_U8 && d % WKS == 0 && ldw % 128 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0;
+}
+
+// round(mean) as bytes (the wide kernel's subtrahend); *bad counts entries outside 0..255
+// (then the wide kernel is not used: its byte subtrahend could not represent them)
+__global__ void mean_u8_kernel(const float* __restrict__ mean_r, int64_t d, uint8_t* __restrict__ out,
+                               int* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d) return;
+  const float v = mean_r[i];
+  if (!(v >= 0.f && v <= 255.f)) atomicAdd(bad, 1);
+  out[i] = (uint8_t)fminf(fmaxf(v, 0.f), 255.f);
+}
+
+hipError_t launch_mean_u8(hipStream_t s, const float* mean_r, int64_t d, uint8_t* out, int* bad) {
+  hipLaunchKernelGGL(mean_u8_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, mean_r, d, out, bad);
+  return hipGetLastError();
+}
+
+int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int64_t bpad, int64_t d, int ldw,
+                        int64_t* pix_per_split) {
+  const int64_t steps = (d + HK - 1) / HK;
+  if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8)) {
+    const int64_t wsteps = d / WKS;
+    const int nt = ldw % 256 == 0 ? ldw / 256 : ldw / 128;
+    const int64_t tiles = (bpad + WM - 1) / WM * nt;
+    // fill the 256 CUs with one workgroup each; the item count must be a multiple of 8
+    int64_t ns = (256 + tiles - 1) / tiles;
+    if (ns > wsteps) ns = wsteps;
+    if (ns < 1) ns = 1;
+    while ((tiles * ns) % 8 != 0) ++ns;
+    const int64_t steps_per = (wsteps + ns - 1) / ns;
+    *pix_per_split = steps_per * WKS;
+    return (int)((d + *pix_per_split - 1) / *pix_per_split);
+  }
   const int64_t tiles = bpad / HM * ((ldw + HN - 1) / HN);
   int64_t ns = (512 + tiles - 1) / tiles;  // ~2 workgroups per CU
-  const int64_t steps = (d + HK - 1) / HK;
   if (ns > steps) ns = steps;
   if (ns < 1) ns = 1;
   if (ns > 64) ns = 64;
@@ -213,9 +405,24 @@ int project_bf16_nsplit(int64_t bpad, int64_t d, int ldw, int64_t* pix_per_split
 }
 
 hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_t b, int64_t bpad, int64_t d,
-                               const float* mean_r, const unsigned short* Wt16, int ldw, float* part, int nsplit,
-                               int64_t pps) {
+                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16, int ldw,
+                               float* part, int nsplit, int64_t pps) {
   if (ldw % HN != 0) return hipErrorInvalidValue;
+  if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8)) {
+    const bool n256 = ldw % 256 == 0;
+    const int nt = n256 ? ldw / 256 : ldw / 128;
+    const int mt = (int)((bpad + WM - 1) / WM);
+    const int total = mt * nt * nsplit;
+    if (total % 8 != 0 || bpad % WM != 0) return hipErrorInvalidValue;
+    const uint8_t* p8 = static_cast<const uint8_t*>(P);
+    if (n256)
+      hipLaunchKernelGGL((project_bf16_wide_kernel<256, WKS>), dim3((unsigned)total), dim3(512), 0, s, p8, b, d, mean_u8,
+                         Wt16, ldw, part, bpad, pps, mt, nt, nsplit);
+    else
+      hipLaunchKernelGGL((project_bf16_wide_kernel<128, WKS>), dim3((unsigned)total), dim3(512), 0, s, p8, b, d, mean_u8,
+                         Wt16, ldw, part, bpad, pps, mt, nt, nsplit);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(bpad / HM), (unsigned)nsplit, (unsigned)(ldw / HN));
   const bool vec = (d % 16 == 0) && (pps % 16 == 0) && ((reinterpret_cast<uintptr_t>(P) & 15) == 0);
   if (p_dtype == EF_U8) {

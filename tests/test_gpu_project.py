@@ -73,12 +73,17 @@ def test_recognize_fused_wide_k(eng):
 BF16_REL = 2.0 ** -8  # stated tolerance: |f_bf16 - f| <= 2^-8 * sum_px |p - round(mean)| |W| (+ fp32 term)
 
 
-@pytest.mark.parametrize("d,k,b", [(4096, 64, 300), (10000, 200, 129), (65536, 512, 256)])
-def test_project_bf16_tolerance(eng, d, k, b):
+@pytest.mark.parametrize("d,k,b,mean_lo,mean_hi", [
+    (4096, 64, 300, 60, 200),      # wide kernel, 128-column tiles
+    (10000, 200, 129, 60, 200),    # d % 64 != 0: the 128 x 128 kernel
+    (65536, 512, 256, 60, 200),    # config 5: wide kernel, 256-column tiles
+    (8192, 256, 257, 60, 200),     # ragged batch through the wide kernel
+    (4096, 128, 200, -40, 300)])   # round(mean) outside 0..255: the byte-mean wide kernel is skipped
+def test_project_bf16_tolerance(eng, d, k, b, mean_lo, mean_hi):
     """Config 5 bf16 projection: uint8 pixels minus round(mean) are exact in bf16, so the
     error is W's bf16 rounding only (unit roundoff 2^-9), bounded per feature."""
     rng = np.random.default_rng(d + k)
-    mu = rng.uniform(60, 200, d).astype(np.float32)
+    mu = rng.uniform(mean_lo, mean_hi, d).astype(np.float32)
     w = (rng.standard_normal((d, k)) / np.sqrt(d)).astype(np.float32)
     p = rng.integers(0, 256, (b, d), dtype=np.uint8)
     eng.set_model(mu, w, precision="bf16")
