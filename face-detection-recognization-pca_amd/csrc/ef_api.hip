@@ -241,8 +241,9 @@ void ef_destroy(ef_ctx* c) {
   }
   DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->mean_u8,   &c->corr,      &c->G,
                     &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
-                    &c->p_stage, &c->proj_part, &c->feats_dev};
+                    &c->p_stage, &c->proj_part, &c->feats_dev, &c->jpeg_ws, &c->jpeg_out, &c->jpeg_rows};
   for (DevBuf* b : bufs) release(*b);
+  if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);
@@ -277,6 +278,12 @@ int ef_trim(ef_ctx* c) {
   EF_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   for (auto& b : c->fit_pool) release(b);
   c->fit_pool.clear();
+  release(c->jpeg_ws);
+  release(c->jpeg_out);
+  release(c->jpeg_rows);
+  if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
+  c->jpeg_pinned = nullptr;
+  c->jpeg_pinned_bytes = 0;
   return EF_OK;
 }
 

@@ -108,6 +108,11 @@ struct ef_ctx {
 
   std::vector<ef::DevBuf> fit_pool;  // ef_fit workspaces, reused across calls (ef_trim frees)
 
+  // JPEG decode (ef_jpeg.hip): device workspace, host-output staging, pinned upload buffer
+  ef::DevBuf jpeg_ws, jpeg_out, jpeg_rows;
+  void* jpeg_pinned = nullptr;
+  size_t jpeg_pinned_bytes = 0;
+
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
 

@@ -21,7 +21,10 @@ EF_FIT_STANDARDIZE = 0x1
 EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
-EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR = 0, 1, 2, 3, 4
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR, EF_KERNEL_JPEG = \
+    0, 1, 2, 3, 4, 5
+EF_JPEG_GRAY, EF_JPEG_BGR = 0, 1
+EF_JPEG_E_UNSUPPORTED, EF_JPEG_E_CORRUPT = -10, -11
 EF_KEY_NONE = (1 << 63) - 1
 EF_UNIQUE_ID_BYTES = 128
 EF_OPT_FIT_MAX_ITERS, EF_OPT_FIT_FP32_COARSE, EF_OPT_COV_SLAB_BYTES, EF_OPT_TM_INT64_SUMS, EF_OPT_HAAR_ORDERED = \
@@ -82,6 +85,9 @@ _SIGS = {
     "ef_set_option": ([vp, i32, i64], C.c_int),
     "ef_get_option": ([vp, i32, C.POINTER(i64)], C.c_int),
     "ef_preprocess": ([vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, u32], C.c_int),
+    "ef_jpeg_info": ([vp, vp, vp, i32, vp, vp, vp, vp], C.c_int),
+    "ef_jpeg_decode": ([vp, vp, vp, vp, i32, i32, vp, vp, vp, u32], C.c_int),
+    "ef_jpeg_ingest": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp, u32], C.c_int),
     "ef_tm_prepare": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, u32], C.c_int),
     "ef_tm_match": ([vp, vp, i64, vp, vp, vp, vp, u32], C.c_int),
     "ef_tm_info": ([vp, C.POINTER(i32), C.POINTER(i64), vp, vp], C.c_int),
@@ -116,7 +122,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 2:
+        if h.ef_api_version() != 3:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

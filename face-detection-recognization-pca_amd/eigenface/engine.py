@@ -462,6 +462,57 @@ class Engine:
                                           ws.ctypes.data, cs.ctypes.data, n, oh, ow, res.ctypes.data, flags))
         return res
 
+    # ----------------------------------------------------------------- JPEG decode
+    def decode_jpegs(self, blobs, mode="bgr"):
+        """GPU decode of a batch of JPEG files (include/eigenface.h ef_jpeg_decode):
+        ``blobs`` are the files' bytes; ``mode`` "bgr" (cv2.imread IMREAD_COLOR) or "gray"
+        (IMREAD_GRAYSCALE).  Returns a list of uint8 arrays, None where the GPU decoder
+        does not take the file (progressive, CMYK, ...; ``status`` says why)."""
+        m = _jpeg_mode(mode)
+        data, offs, sizes = _pack_blobs(blobs)
+        n = len(blobs)
+        if n == 0:
+            return []
+        h, w, _, st = jpeg_info(blobs, _packed=(data, offs, sizes))
+        ch = 1 if m == N.EF_JPEG_GRAY else 3
+        px = np.where(st == 0, h.astype(np.int64) * w * ch, 0)
+        ooff = np.zeros(n, np.int64)
+        ooff[1:] = np.cumsum(px)[:-1]
+        out = np.empty(max(1, int(px.sum())), np.uint8)
+        self._chk(self._lib.ef_jpeg_decode(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+                                           out.ctypes.data, ooff.ctypes.data, st.ctypes.data, 0))
+        res = []
+        for i in range(n):
+            if st[i] != 0:
+                res.append(None)
+                continue
+            a = out[ooff[i]:ooff[i] + px[i]]
+            res.append(a.reshape(h[i], w[i]) if ch == 1 else a.reshape(h[i], w[i], 3))
+        return res
+
+    def ingest_jpegs(self, blobs, size=(64, 64), mode="bgr", out=None):
+        """Fused GPU decode + grey + INTER_LINEAR resize of JPEG files
+        (ef_jpeg_ingest): (rows uint8 (n, h*w) — or device tensor ``out`` filled —,
+        status int32 (n,)).  Rows of files with status != 0 are zero."""
+        m = _jpeg_mode(mode)
+        ow, oh = int(size[0]), int(size[1])
+        n = len(blobs)
+        st = np.zeros(n, np.int32)
+        if n == 0:
+            return np.empty((0, oh * ow), np.uint8), st
+        data, offs, sizes = _pack_blobs(blobs)
+        if out is not None:
+            import torch
+            o, op = _dev(out, torch.uint8)
+            self._dev_out(o, (n, oh * ow), torch.uint8, "out")
+            self._chk(self._lib.ef_jpeg_ingest(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+                                               oh, ow, op, st.ctypes.data, N.EF_MEM_DEVICE))
+            return out, st
+        rows = np.empty((n, oh * ow), np.uint8)
+        self._chk(self._lib.ef_jpeg_ingest(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+                                           oh, ow, rows.ctypes.data, st.ctypes.data, 0))
+        return rows, st
+
     def tm_prepare(self, templates, problems, frame_shape):
         """Resident template-localiser operands (ef_tm_prepare).  ``templates``: list of
         grey uint8 (h, w) arrays; ``problems``: list of (template index, height, width)
@@ -524,7 +575,7 @@ class Engine:
 
     def timing_get(self, kernel="search"):
         kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT, "tmatch": N.EF_KERNEL_TMATCH,
-               "ingest": N.EF_KERNEL_INGEST, "haar": N.EF_KERNEL_HAAR}[kernel]
+               "ingest": N.EF_KERNEL_INGEST, "haar": N.EF_KERNEL_HAAR, "jpeg": N.EF_KERNEL_JPEG}[kernel]
         ms = C.c_double(0)
         n = C.c_int64(0)
         self._chk(self._lib.ef_timing_get(self._h, kid, C.byref(ms), C.byref(n)))
@@ -554,6 +605,40 @@ def merge_matches_host(parts, b):
         if rc != N.EF_OK:
             raise N.EigenfaceError(rc, "ef_matches_merge failed")
     return keys
+
+
+def _jpeg_mode(mode):
+    try:
+        return {"bgr": N.EF_JPEG_BGR, "color": N.EF_JPEG_BGR, "gray": N.EF_JPEG_GRAY, "grey": N.EF_JPEG_GRAY}[mode]
+    except KeyError:
+        raise ValueError(f"unknown JPEG output mode {mode!r} (bgr | gray)") from None
+
+
+def _pack_blobs(blobs):
+    """Concatenate file contents: (uint8 buffer, int64 offsets, int64 sizes)."""
+    mv = [memoryview(b).cast("B") for b in blobs]
+    sizes = np.array([len(b) for b in mv], np.int64)
+    offs = np.zeros(len(mv), np.int64)
+    if len(mv) > 1:
+        offs[1:] = np.cumsum(sizes)[:-1]
+    data = np.empty(max(1, int(sizes.sum())), np.uint8)
+    for o, b in zip(offs, mv):
+        data[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    return data, offs, sizes
+
+
+def jpeg_info(blobs, _packed=None):
+    """Header parse on the host (ef_jpeg_info, no GPU): (height, width, components,
+    status) int32 arrays; status 0 = the GPU decoder takes the file."""
+    data, offs, sizes = _packed if _packed is not None else _pack_blobs(blobs)
+    n = len(sizes)
+    h, w, c, st = (np.zeros(n, np.int32) for _ in range(4))
+    if n:
+        rc = N.lib().ef_jpeg_info(data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, h.ctypes.data,
+                                  w.ctypes.data, c.ctypes.data, st.ctypes.data)
+        if rc != N.EF_OK:
+            raise N.EigenfaceError(rc, "ef_jpeg_info failed")
+    return h, w, c, st
 
 
 def device_count() -> int:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 2
+#define EF_API_VERSION 3
 
 /* status codes */
 #define EF_OK 0
@@ -60,6 +60,7 @@ extern "C" {
 #define EF_KERNEL_TMATCH 2  /* template localiser, one frame    */
 #define EF_KERNEL_INGEST 3  /* grey + resize of one image batch */
 #define EF_KERNEL_HAAR 4    /* Haar cascade detection, one frame (GPU part) */
+#define EF_KERNEL_JPEG 5    /* JPEG entropy decode + IDCT + colour, one batch */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX
@@ -204,6 +205,36 @@ int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 int ef_preprocess(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int32_t* heights,
                   const int32_t* widths, const int32_t* channels, int64_t count, int32_t out_h,
                   int32_t out_w, uint8_t* out, uint32_t flags);
+
+/* ------------------------------------------------------------------ JPEG decode
+ * Replaces the per-file cv2.imread of the ingest paths (train-v4.py:59 IMREAD_COLOR;
+ * useless/train.py:33 and scan-template-v4.py:52 IMREAD_GRAYSCALE) for a batch of
+ * JPEG files: image i is sizes[i] bytes at data + offsets[i] (data is always a host
+ * pointer).  Decoded on the GPU with libjpeg-turbo's default arithmetic (islow IDCT,
+ * fancy upsampling, its YCbCr->RGB tables), so the pixels equal what imread returns:
+ *   EF_JPEG_GRAY  h x w luma (libjpeg JCS_GRAYSCALE output, IMREAD_GRAYSCALE)
+ *   EF_JPEG_BGR   h x w x 3 BGR (IMREAD_COLOR)
+ * written at out + out_offsets[i] (host, or device with EF_MEM_DEVICE — then the
+ * pixels can go straight into ef_preprocess with EF_MEM_DEVICE).  Supported: sequential
+ * Huffman (SOF0/SOF1) 8-bit, 1 or 3 components, luma at the maximal sampling factors,
+ * chroma at 1x or 2x horizontally and vertically (4:4:4, 4:2:2, 4:2:0), one scan,
+ * restart intervals.  status[i] (optional) is 0, or EF_JPEG_E_UNSUPPORTED /
+ * EF_JPEG_E_CORRUPT for a file the caller must decode on the host (nothing is written
+ * for it).  ef_jpeg_info parses the headers on the host (no context, no GPU). */
+#define EF_JPEG_GRAY 0
+#define EF_JPEG_BGR 1
+#define EF_JPEG_E_UNSUPPORTED (-10)
+#define EF_JPEG_E_CORRUPT (-11)
+int ef_jpeg_info(const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count, int32_t* heights,
+                 int32_t* widths, int32_t* components, int32_t* status);
+int ef_jpeg_decode(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count,
+                   int32_t mode, uint8_t* out, const int64_t* out_offsets, int32_t* status, uint32_t flags);
+/* Fused ingest (train-v4.py:59-68 for a batch of files): ef_jpeg_decode into device
+ * scratch, then ef_preprocess (grey + INTER_LINEAR resize to out_h x out_w) without a host
+ * round trip.  out: count x out_h x out_w uint8 rows (host, or device with EF_MEM_DEVICE);
+ * the row of a file with status[i] != 0 is zero and the caller decodes that file itself. */
+int ef_jpeg_ingest(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count,
+                   int32_t mode, int32_t out_h, int32_t out_w, uint8_t* out, int32_t* status, uint32_t flags);
 
 /* -------------------------------------------------------- template localiser
  * Replaces template_match_all_models' inner loops (scan-template-v4.py:127-200):

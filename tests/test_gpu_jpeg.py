@@ -1,0 +1,101 @@
+"""GPU JPEG decode (include/eigenface.h ef_jpeg_decode / ef_jpeg_ingest) against
+libjpeg-turbo, bit for bit.  The oracle is Pillow's libjpeg-turbo decode of the same
+bytes (tests/jpeg_cases.py): the library behind cv2.imread, which the reference calls
+per file (train-v4.py:59, useless/train.py:33, scan-template-v4.py:52)."""
+import io
+
+import numpy as np
+import pytest
+
+import jpeg_cases as J
+from oracle import image_oracle as io_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return J.corpus()
+
+
+@pytest.mark.parametrize("mode", ["bgr", "gray"])
+def test_decode_matches_libjpeg_turbo(eng, corpus, mode):
+    got = eng.decode_jpegs([b for _, b in corpus], mode)
+    for (name, b), g in zip(corpus, got):
+        ref = J.decode_ref(b, mode)
+        assert g is not None, name
+        np.testing.assert_array_equal(g, ref, err_msg=f"{mode} {name}")
+
+
+def _progressive():
+    return J.encode(J.smooth_image(40, 40, 3, 1), quality=80, progressive=True)
+
+
+def _cmyk():
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(J.smooth_image(16, 16, 3, 2)).convert("CMYK").save(b, format="JPEG")
+    return b.getvalue()
+
+
+def test_unsupported_and_corrupt_files_are_reported(eng):
+    good = J.encode(J.smooth_image(30, 20, 3, 3), quality=90)
+    blobs = [good, _progressive(), _cmyk(), b"\xff\xd8\xff\xe0garbage", b"", good[:40], good]
+    from eigenface.engine import jpeg_info
+    _, _, _, st = jpeg_info(blobs)
+    assert st[0] == 0 and st[6] == 0
+    assert st[1] == -10 and st[2] == -10           # progressive, CMYK: EF_JPEG_E_UNSUPPORTED
+    assert st[3] == -11 and st[4] == -11 and st[5] == -11  # EF_JPEG_E_CORRUPT
+    got = eng.decode_jpegs(blobs, "bgr")
+    ref = J.decode_ref(good, "bgr")
+    np.testing.assert_array_equal(got[0], ref)
+    np.testing.assert_array_equal(got[6], ref)
+    assert all(g is None for g in got[1:6])
+
+
+def test_damaged_entropy_data_decodes_without_fault(eng):
+    """Flipped bits and a truncated scan: libjpeg warns and feeds zeros; the decoder must
+    stay in bounds (shape right, no fault) — the pixel values of a damaged stream are not
+    pinned."""
+    rng = np.random.default_rng(5)
+    blobs = []
+    for k in range(40):
+        b = bytearray(J.encode(J.smooth_image(48, 64, 3, k), quality=70, subsampling=k % 3))
+        sos = b.find(b"\xff\xda")
+        for _ in range(8):
+            i = int(rng.integers(sos + 14, len(b) - 2))
+            b[i] ^= 1 << int(rng.integers(0, 8))
+        blobs.append(bytes(b if k % 2 else b[:len(b) * 3 // 4]))
+    got = eng.decode_jpegs(blobs, "bgr")
+    for g in got:
+        assert g is None or g.shape == (48, 64, 3)
+    # the engine is still healthy
+    good = J.encode(J.smooth_image(20, 20, 3, 9))
+    np.testing.assert_array_equal(eng.decode_jpegs([good], "bgr")[0], J.decode_ref(good, "bgr"))
+
+
+@pytest.mark.parametrize("mode", ["bgr", "gray"])
+def test_ingest_equals_decode_then_preprocess(eng, corpus, mode):
+    """ef_jpeg_ingest (decode -> grey -> INTER_LINEAR 64x64 on the GPU, no host round
+    trip) equals libjpeg's pixels through the resize oracle."""
+    blobs = [b for _, b in corpus] + [_progressive()]
+    rows, st = eng.ingest_jpegs(blobs, (64, 64), mode)
+    assert (st[:-1] == 0).all() and st[-1] == -10
+    assert not rows[-1].any()
+    for i, (name, b) in enumerate(corpus):
+        np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(b, mode), (64, 64)),
+                                      err_msg=f"{mode} {name}")
+
+
+def test_ingest_into_device_tensor_large_batch(eng):
+    import torch
+    n = 3000
+    blobs = [J.encode(J.smooth_image(90 + k % 23, 70 + k % 17, 3, k), quality=60 + k % 40, subsampling=k % 3,
+                      **({"restart_marker_blocks": 1 + k % 4} if k % 5 == 0 else {})) for k in range(n)]
+    out = torch.empty((n, 64 * 64), dtype=torch.uint8, device="cuda")
+    _, st = eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    rows = out.cpu().numpy()
+    for i in range(0, n, 97):
+        np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(blobs[i], "bgr"), (64, 64)))

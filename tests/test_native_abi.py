@@ -46,7 +46,7 @@ def test_library_is_gfx950_code_object():
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
-    assert lib.ef_api_version() == 2
+    assert lib.ef_api_version() == 3
     n = ctypes.c_int(-1)
     assert lib.ef_device_count(ctypes.byref(n)) == 0
     if n.value == 0:  # build container: creating a context must fail cleanly, not crash
