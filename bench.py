@@ -272,6 +272,62 @@ PEAK_I8_TOPS = 5000.0   # MI355X dense int8 MFMA (2x the bf16 rate, MI355X_MICRO
 PEAK_HBM_GBS = 8000.0
 
 
+def _face_jpegs(n, sides, seed=11):
+    """n synthetic face-crop JPEGs as the reference writes them (cv2.imwrite defaults:
+    baseline, quality 95, 4:2:0; detection-v4.py:64), smooth photograph-like content."""
+    import io as _io
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        s = sides[i % len(sides)]
+        y, x = np.mgrid[0:s, 0:s].astype(np.float32)
+        a, b, p = rng.uniform(0.03, 0.15, 3)
+        img = np.stack([128 + 80 * np.sin(a * x + p + c) * np.cos(b * y - c) for c in range(3)], 2)
+        img = np.clip(img + rng.normal(0, 5, img.shape), 0, 255).astype(np.uint8)
+        buf = _io.BytesIO()
+        Image.fromarray(img).save(buf, format="JPEG", quality=95)
+        out.append(buf.getvalue())
+    return out
+
+
+def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=5):
+    """JPEG files -> grey 64x64 rows (ef_jpeg_ingest: host marker parse + one upload, GPU
+    Huffman / IDCT / upsample+YCC / resize) against per-file libjpeg-turbo decoding."""
+    import torch
+    blobs = _face_jpegs(n, sides)
+    nbytes = sum(len(b) for b in blobs)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((n, 4096), dtype=torch.uint8, device=dev)
+    eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
+    torch.cuda.synchronize(dev)
+    eng.timing_reset()
+    t = time.perf_counter()
+    for _ in range(reps):
+        _, st = eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t) / reps
+    assert (st == 0).all()
+    k_ms, k_n = eng.timing_get("jpeg")
+    kdt = k_ms / max(k_n, 1) * 1e-3
+    res = {"config": f"{n} JPEG face crops {min(sides)}-{max(sides)} px (q95 4:2:0, {nbytes / n / 1024:.1f} KiB avg)"
+                     " -> decode -> grey 64x64, rows on the device",
+           "faces_per_s": round(n / wall, 1), "ms_per_batch": round(wall * 1e3, 3),
+           "decode_ms_device": round(kdt * 1e3, 3), "file_MBs": round(nbytes / wall / 1e6, 1)}
+    if with_cpu:
+        import io as _io
+        from PIL import Image
+        t = time.perf_counter()
+        m = 0
+        while time.perf_counter() - t < 3.0 and m < n:
+            im = Image.open(_io.BytesIO(blobs[m]))
+            im.load()
+            m += 1
+        res["cpu"] = {"faces_per_s": round(m / (time.perf_counter() - t), 1), "cores": 1, "kind": "reference",
+                      "sample": f"{m} files, Pillow's libjpeg-turbo decode only (the library cv2.imread wraps)"}
+    return res
+
+
 def image_bench(eng, with_cpu: bool, frames=20):
     """Secondary measurements of SURVEY.md §8f ranks 2-3 on the GPU (synthetic pixels):
     ingest = 4096 BGR face crops of the reference's detection sizes (82-325 px) ->
@@ -324,6 +380,7 @@ def image_bench(eng, with_cpu: bool, frames=20):
             io.preprocess(c)
         res["ingest"]["cpu"] = {"faces_per_s": round(m / (time.perf_counter() - t), 1), "cores": 1,
                                 "kind": "port", "sample": f"{m} crops, NumPy restatement of cvtColor+resize"}
+    res["jpeg_ingest"] = jpeg_ingest_bench(eng, with_cpu, sides)
     # ---- template localiser
     H, W = 480, 640
     frame = rng.integers(0, 256, (H, W), dtype=np.uint8)

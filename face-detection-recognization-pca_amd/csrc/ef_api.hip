@@ -544,6 +544,11 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
     case EF_OPT_HAAR_ORDERED:
       c->opt_haar_ordered = value != 0;
       return EF_OK;
+    case EF_OPT_JPEG_CHUNK_BITS:
+      if (value < 0 || value > (1 << 24) || value % 32)
+        return set_err(c, EF_E_INVALID, "EF_OPT_JPEG_CHUNK_BITS must be 0 or a multiple of 32 up to 2^24");
+      c->opt_jpeg_chunk_bits = value;
+      return EF_OK;
     default:
       return set_err(c, EF_E_INVALID, "ef_set_option: unknown option " + std::to_string(option));
   }
@@ -557,6 +562,7 @@ int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
     case EF_OPT_COV_SLAB_BYTES: *value = c->opt_cov_slab_bytes; return EF_OK;
     case EF_OPT_TM_INT64_SUMS: *value = c->opt_tm_int64; return EF_OK;
     case EF_OPT_HAAR_ORDERED: *value = c->opt_haar_ordered; return EF_OK;
+    case EF_OPT_JPEG_CHUNK_BITS: *value = c->opt_jpeg_chunk_bits; return EF_OK;
     default: return EF_E_INVALID;
   }
 }

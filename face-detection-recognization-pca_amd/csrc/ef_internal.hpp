@@ -73,6 +73,7 @@ struct ef_ctx {
   int64_t opt_cov_slab_bytes = (int64_t)8 << 30;
   int64_t opt_tm_int64 = 0;
   int64_t opt_haar_ordered = 0;
+  int64_t opt_jpeg_chunk_bits = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -112,6 +113,7 @@ struct ef_ctx {
   ef::DevBuf jpeg_ws, jpeg_out, jpeg_rows;
   void* jpeg_pinned = nullptr;
   size_t jpeg_pinned_bytes = 0;
+  int jpeg_rounds = 0;  // synchronisation rounds of the last decode (diagnostics)
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade

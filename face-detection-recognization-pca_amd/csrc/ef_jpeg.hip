@@ -28,8 +28,11 @@
 // int16 coefficient blocks; kernel 2 runs one 8x8 IDCT per thread into padded component
 // planes; kernel 3 writes one output pixel per thread (grey copy, or upsample + YCC->BGR).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "ef_internal.hpp"
@@ -48,29 +51,40 @@ struct HuffTab {                // libjpeg d_derived_tbl
 
 struct JComp {
   int h, v;          // sampling factors
-  int q;             // quantisation table index into the image's qt[]
-  int dc, ac;        // Huffman table indices into the global pool
+  int q;             // quantisation table index (Tables::quant)
+  int dc, ac;        // Huffman table indices (Tables::huff)
   int bw, bh;        // blocks per row / column in the coefficient & sample planes
   int dw, dh;        // downsampled width / height (libjpeg's downsampled_width/height)
   int64_t coef_off;  // first block's int16[64] in the coefficient buffer
   int64_t plane_off; // first sample of the padded plane (bw * 8 bytes per row)
 };
 
+constexpr int kMaxBlocksPerMcu = 10;  // JPEG limit on blocks in one MCU (jdinput.c)
+
 struct JImage {
   int w, h, nc, hmax, vmax;
   int mcux, mcuy;          // MCUs per row / column (interleaved), or blocks (one component)
   int interleaved;
   int restart;             // MCUs per restart interval (0 = none)
-  int qt_base;             // first of this image's quantisation tables (4 slots) in the pool
+  int qt_base;             // 0: JComp::q indexes the batch's quantisation tables directly
+  int bpm;                 // blocks per MCU
+  unsigned char bcomp[kMaxBlocksPerMcu];  // component of each block of an MCU
+  unsigned char boff[kMaxBlocksPerMcu];   // (row << 4) | column of that block inside the MCU
   JComp c[kMaxComp];
   int64_t out_off;
   int mode;                // EF_JPEG_GRAY / EF_JPEG_BGR
 };
 
+// An entropy segment: the whole scan, or one restart interval.  Its bytes are uploaded with
+// the 0xFF00 stuffing removed (a clean big-endian bit string of nbits, zero beyond), and it
+// is cut into chunks of chunk_bits for the parallel decode.
 struct JSeg {
   int img;
-  int64_t beg, end;  // entropy-coded bytes [beg, end) in the uploaded data
-  int mcu0, nmcu;    // first MCU and count
+  int mcu0, nmcu;     // first MCU and count
+  int64_t beg, end;   // raw entropy-coded bytes [beg, end) inside the image's file
+  int64_t word_off;   // first 32-bit word of the destuffed bits in the upload
+  int nbits;
+  int chunk0, nchunk;
 };
 
 // --------------------------------------------------------------------- host parsing
@@ -80,7 +94,7 @@ struct RawHuff {
   bool present = false;
 };
 
-bool derive(const RawHuff& r, HuffTab& t) {  // jdhuff.c jpeg_make_d_derived_tbl
+bool derive(const RawHuff& r, HuffTab& t, bool dc) {  // jdhuff.c jpeg_make_d_derived_tbl
   char size[257];
   unsigned code[257];
   int p = 0;
@@ -122,12 +136,46 @@ bool derive(const RawHuff& r, HuffTab& t) {  // jdhuff.c jpeg_make_d_derived_tbl
       for (int ctr = 1 << (8 - l); ctr > 0; --ctr) t.look[lookbits++] = (unsigned short)((l << 8) | r.val[p]);
     }
   for (int i = 0; i < 256; ++i) t.huffval[i] = i < last ? r.val[i] : 0;
+  if (dc)  // DC categories above 15 are rejected as libjpeg does (JERR_BAD_HUFF_TABLE)
+    for (int i = 0; i < last; ++i)
+      if (r.val[i] > 15) return false;
   return true;
 }
 
+// Derived Huffman and quantisation tables shared by the whole batch: files written by the
+// same encoder carry identical tables, so the decode kernels see a handful of tables that
+// stay resident in L1/L2 instead of one set per image.
+struct Tables {
+  std::vector<HuffTab> huff;
+  std::vector<unsigned short> quant;  // 64 entries (natural order) per table
+  std::unordered_map<std::string, int> huff_idx, quant_idx;
+  int huff_table(const RawHuff& r, bool dc) {  // index, or -1 for an invalid table
+    int cnt = 0;
+    for (int l = 1; l <= 16; ++l) cnt += r.bits[l];
+    std::string key(1, dc ? 'D' : 'A');
+    key.append(reinterpret_cast<const char*>(r.bits + 1), 16);
+    key.append(reinterpret_cast<const char*>(r.val), (size_t)std::min(cnt, 256));
+    auto it = huff_idx.find(key);
+    if (it != huff_idx.end()) return it->second;
+    HuffTab t;
+    const int idx = derive(r, t, dc) ? (int)huff.size() : -1;
+    if (idx >= 0) huff.push_back(t);
+    huff_idx.emplace(std::move(key), idx);
+    return idx;
+  }
+  int quant_table(const unsigned short* q) {
+    std::string key(reinterpret_cast<const char*>(q), 128);
+    auto it = quant_idx.find(key);
+    if (it != quant_idx.end()) return it->second;
+    const int idx = (int)(quant.size() / 64);
+    quant.insert(quant.end(), q, q + 64);
+    quant_idx.emplace(std::move(key), idx);
+    return idx;
+  }
+};
+
 // Parse one file: frame, tables, scan, restart segments.  Returns 0 or a negative status.
-int parse(const uint8_t* d, int64_t n, int img_index, JImage& im, std::vector<HuffTab>& pool,
-          std::vector<unsigned short>& qpool, std::vector<JSeg>& segs, int64_t data_base, bool want) {
+int parse(const uint8_t* d, int64_t n, int img_index, JImage& im, Tables& T, std::vector<JSeg>& segs, bool want) {
   if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return EF_JPEG_E_CORRUPT;
   RawHuff dht[2][4];
   unsigned short qt[4][64];
@@ -217,16 +265,9 @@ int parse(const uint8_t* d, int64_t n, int img_index, JImage& im, std::vector<Hu
         for (int j = 0; j < im.nc; ++j)
           if (comp_id[j] == cid) c = j;
         if (c != k || td > 3 || ta > 3 || !dht[0][td].present || !dht[1][ta].present) return EF_JPEG_E_CORRUPT;
-        if (map_dc[td] < 0) {
-          map_dc[td] = (int)pool.size();
-          pool.emplace_back();
-          if (!derive(dht[0][td], pool.back())) return EF_JPEG_E_CORRUPT;
-        }
-        if (map_ac[ta] < 0) {
-          map_ac[ta] = (int)pool.size();
-          pool.emplace_back();
-          if (!derive(dht[1][ta], pool.back())) return EF_JPEG_E_CORRUPT;
-        }
+        if (map_dc[td] < 0) map_dc[td] = T.huff_table(dht[0][td], true);
+        if (map_ac[ta] < 0) map_ac[ta] = T.huff_table(dht[1][ta], false);
+        if (map_dc[td] < 0 || map_ac[ta] < 0) return EF_JPEG_E_CORRUPT;
         im.c[c].dc = map_dc[td];
         im.c[c].ac = map_ac[ta];
         if (!qt_ok[comp_q[c]]) return EF_JPEG_E_CORRUPT;
@@ -263,41 +304,64 @@ int parse(const uint8_t* d, int64_t n, int img_index, JImage& im, std::vector<Hu
         im.mcux = im.c[0].bw;
         im.mcuy = im.c[0].bh;
       }
-      im.qt_base = (int)(qpool.size() / 64);
-      for (int c = 0; c < im.nc; ++c) {
-        qpool.insert(qpool.end(), qt[comp_q[c]], qt[comp_q[c]] + 64);
-        im.c[c].q = c;
+      im.qt_base = 0;
+      for (int c = 0; c < im.nc; ++c) im.c[c].q = T.quant_table(qt[comp_q[c]]);
+      // MCU block pattern (jdinput.c per_scan_setup, MCU_membership)
+      im.bpm = 0;
+      if (im.interleaved) {
+        for (int c = 0; c < im.nc; ++c)
+          for (int yy = 0; yy < im.c[c].v; ++yy)
+            for (int xx = 0; xx < im.c[c].h; ++xx) {
+              if (im.bpm >= kMaxBlocksPerMcu) return EF_JPEG_E_CORRUPT;
+              im.bcomp[im.bpm] = (unsigned char)c;
+              im.boff[im.bpm] = (unsigned char)((yy << 4) | xx);
+              ++im.bpm;
+            }
+      } else {
+        im.bpm = 1;
+        im.bcomp[0] = 0;
+        im.boff[0] = 0;
       }
-      if (!want) return 0;
-      // entropy segments: the scan data up to the next non-RST marker, split at RSTn
-      const int64_t scan_beg = p + 2 + len;
       const int64_t total_mcu = (int64_t)im.mcux * im.mcuy;
+      if (total_mcu * im.bpm > (int64_t)1 << 30) return EF_JPEG_E_UNSUPPORTED;
+      if (!want) return 0;
+      // entropy segments: the whole scan (the bit reader stops at the first marker), or
+      // one per restart interval split at RSTn
+      const int64_t scan_beg = p + 2 + len;
+      if (n - scan_beg > ((int64_t)1 << 27)) return EF_JPEG_E_UNSUPPORTED;  // bit offsets stay in int32
+      if (im.restart == 0) {
+        segs.push_back(JSeg{img_index, 0, (int)total_mcu, scan_beg, n, 0, 0, 0, 0});
+        return 0;
+      }
       int64_t q = scan_beg, seg_beg = scan_beg;
       int mcu0 = 0;
-      const int per = im.restart > 0 ? im.restart : (int)std::min<int64_t>(total_mcu, 0x7FFFFFFF);
-      while (true) {
-        if (q + 1 >= n) break;  // truncated: the last segment runs to the end (zeros fed)
-        if (d[q] == 0xFF && d[q + 1] != 0x00 && d[q + 1] != 0xFF) {
-          const int mk = d[q + 1];
-          if (im.restart > 0 && mk >= 0xD0 && mk <= 0xD7) {
-            const int cnt = (int)std::min<int64_t>(per, total_mcu - mcu0);
-            if (cnt > 0) segs.push_back(JSeg{img_index, data_base + seg_beg, data_base + q, mcu0, cnt});
-            mcu0 += cnt;
-            q += 2;
-            seg_beg = q;
-            continue;
-          }
+      while (mcu0 < total_mcu) {
+        bool rst = false;
+        while (true) {  // next marker at or after q
+          const void* f = q < n ? std::memchr(d + q, 0xFF, (size_t)(n - q)) : nullptr;
+          if (!f) { q = n; break; }
+          q = static_cast<const uint8_t*>(f) - d;
+          if (q + 1 >= n) { q = n; break; }
+          const int nx = d[q + 1];
+          if (nx == 0x00) { q += 2; continue; }
+          if (nx == 0xFF) { q += 1; continue; }
+          rst = nx >= 0xD0 && nx <= 0xD7;
           break;
         }
-        ++q;
-      }
-      const int64_t seg_end = std::min<int64_t>(q + (q + 1 >= n ? 1 : 0), n);
-      if (mcu0 < total_mcu) {
-        const int cnt = (int)(total_mcu - mcu0);
-        // libjpeg's decoder keeps decoding MCUs past a missing RST with zeros fed; one
-        // segment covers every remaining MCU (restart interval boundaries inside it
-        // reset the predictors as the stream would)
-        segs.push_back(JSeg{img_index, data_base + seg_beg, data_base + seg_end, mcu0, cnt});
+        const int left = (int)(total_mcu - mcu0);
+        if (rst) {
+          const int cnt = std::min(im.restart, left);
+          segs.push_back(JSeg{img_index, mcu0, cnt, seg_beg, q, 0, 0, 0, 0});
+          mcu0 += cnt;
+          q += 2;
+          seg_beg = q;
+          continue;
+        }
+        // EOI, another marker or the end of the data: the final interval.  A stream that
+        // dropped RSTn markers relies on libjpeg's resynchronisation, which is not restated.
+        if (left > im.restart) return EF_JPEG_E_UNSUPPORTED;
+        segs.push_back(JSeg{img_index, mcu0, left, seg_beg, q, 0, 0, 0, 0});
+        mcu0 += left;
       }
       return 0;
     }
@@ -317,45 +381,46 @@ __constant__ unsigned char kNatural[80] = EF_NATURAL_ORDER;
 const unsigned char kNaturalHost[80] = EF_NATURAL_ORDER;
 #endif
 
-struct BitReader {  // jdhuff.c bit buffer; a marker or the segment end feeds zeros
-  const uint8_t* p;
-  const uint8_t* end;
+// Destuffed big-endian bit string of one segment, read through aligned 32-bit words into a
+// 64-bit window; past the end it yields zeros, as libjpeg feeds zeros after a marker.
+struct BitStream {
+  const unsigned* w;
+  int nw;
+  int widx;
+  int pos;  // bit offset of the next unread bit
+  int bits; // valid bits in buf
   unsigned long long buf;
-  int bits;
-  __host__ __device__ void fill() {
-    while (bits <= 56) {
-      unsigned c = 0;
-      if (p < end) {
-        c = *p;
-        if (c == 0xFF) {
-          const unsigned nx = p + 1 < end ? p[1] : 0xD9u;
-          if (nx == 0x00) {
-            p += 2;
-          } else {  // a marker: stop, feed zeros
-            end = p;
-            c = 0;
-          }
-        } else {
-          ++p;
-        }
-      }
-      buf |= (unsigned long long)c << (56 - bits);
-      bits += 8;
+  __host__ __device__ unsigned word(int i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+  __host__ __device__ void init(const unsigned* words, int nwords, int p) {
+    w = words;
+    nw = nwords;
+    widx = p >> 5;
+    const int s = p & 31;
+    buf = (unsigned long long)(word(widx) << s) << 32;
+    bits = 32 - s;
+    ++widx;
+    pos = p;
+  }
+  __host__ __device__ void refill() {  // afterwards at least 32 bits are buffered
+    if (bits <= 32) {
+      buf |= (unsigned long long)word(widx) << (32 - bits);
+      bits += 32;
+      ++widx;
     }
   }
-  __host__ __device__ unsigned peek(int n) { return (unsigned)(buf >> (64 - n)); }
-  __host__ __device__ void skip(int n) { buf <<= n; bits -= n; }
-  __host__ __device__ int get(int n) {  // n <= 16
-    if (n == 0) return 0;
-    if (bits < n) fill();
+  __host__ __device__ unsigned peek(int n) const { return (unsigned)(buf >> (64 - n)); }
+  __host__ __device__ void skip(int n) {
+    buf <<= n;
+    bits -= n;
+    pos += n;
+  }
+  __host__ __device__ int get(int n) {  // 1 <= n <= 16
     const int v = (int)peek(n);
     skip(n);
     return v;
   }
-  __host__ __device__ int decode(const HuffTab& t) {
-    if (bits < 16) fill();
-    const unsigned look = peek(8);
-    const unsigned e = t.look[look];
+  __host__ __device__ int decode(const HuffTab& t) {  // jdhuff.c HUFF_DECODE
+    const unsigned e = t.look[peek(8)];
     if (e >> 8) {
       skip((int)(e >> 8));
       return (int)(e & 0xFF);
@@ -366,7 +431,7 @@ struct BitReader {  // jdhuff.c bit buffer; a marker or the segment end feeds ze
       ++l;
       code = (int)peek(l);
     }
-    if (l > 16) {  // corrupt: libjpeg warns and returns 0
+    if (l > 16) {  // corrupt data: libjpeg warns and returns 0
       skip(16);
       return 0;
     }
@@ -377,57 +442,206 @@ struct BitReader {  // jdhuff.c bit buffer; a marker or the segment end feeds ze
 
 __host__ __device__ __forceinline__ int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (-1 << s) + 1 : x; }
 
-// One entropy segment (a whole scan, or one restart interval) -> int16 coefficient blocks.
-__host__ __device__ void huff_segment(const uint8_t* data, const JSeg& sg, const JImage& im, const HuffTab* pool,
-                                      short* coef, const unsigned char* nat) {
-  BitReader br{data + sg.beg, data + sg.end, 0ull, 0};
-  br.fill();
-  int pred[kMaxComp] = {0, 0, 0};
-  for (int t = 0; t < sg.nmcu; ++t) {
-    const int mcu = sg.mcu0 + t;
-    if (im.restart > 0 && t > 0 && mcu % im.restart == 0) {  // a restart boundary without RSTn
-      pred[0] = pred[1] = pred[2] = 0;
-      br.skip(br.bits & 7);
+// Decoder state at a codeword boundary: bit offset, block of the MCU, next coefficient
+// index (0 = the block's DC symbol comes next).
+__host__ __device__ __forceinline__ long long st_pack(int pos, int b, int k) {
+  return ((long long)pos << 16) | (b << 8) | k;
+}
+__host__ __device__ __forceinline__ int st_pos(long long s) { return (int)(s >> 16); }
+__host__ __device__ __forceinline__ int st_b(long long s) { return (int)((s >> 8) & 0xFF); }
+__host__ __device__ __forceinline__ int st_k(long long s) { return (int)(s & 0xFF); }
+constexpr long long kStateNone = -1;
+
+__host__ __device__ __forceinline__ short* block_ptr(const JImage& im, const JSeg& sg, int g, short* coef) {
+  const int q = g / im.bpm, bb = g - q * im.bpm;
+  const int mcu = sg.mcu0 + q;
+  const JComp& cp = im.c[im.bcomp[bb]];
+  const int my = mcu / im.mcux, mx = mcu - my * im.mcux;
+  const int by = im.interleaved ? my * cp.v + (im.boff[bb] >> 4) : my;
+  const int bx = im.interleaved ? mx * cp.h + (im.boff[bb] & 15) : mx;
+  return coef + cp.coef_off + ((int64_t)by * cp.bw + bx) * 64;
+}
+
+// Synchronisation pass over one chunk: decode from state (b, k) at the stream's position to
+// the first codeword boundary at or past end_bit, without storing anything.  Returns the
+// exit state; cnt[0] = blocks started (DC symbols), cnt[1 + c] = sum of component c's DC
+// differences.
+__host__ __device__ long long chunk_sync(const JImage& im, const HuffTab* pool, BitStream& bs, int b, int k,
+                                         int end_bit, int cnt[4]) {
+  int nblk = 0, dc0 = 0, dc1 = 0, dc2 = 0;
+  while (bs.pos < end_bit) {
+    bs.refill();
+    const int c = im.bcomp[b];
+    const JComp& cp = im.c[c];
+    if (k == 0) {
+      const int s = bs.decode(pool[cp.dc]);
+      const int diff = s ? huff_extend(bs.get(s), s) : 0;
+      dc0 += c == 0 ? diff : 0;
+      dc1 += c == 1 ? diff : 0;
+      dc2 += c == 2 ? diff : 0;
+      ++nblk;
+      k = 1;
+    } else {
+      const int rs = bs.decode(pool[cp.ac]);
+      const int s = rs & 15, r = rs >> 4;
+      if (s) {
+        bs.skip(s);
+        k += r + 1;
+      } else {
+        k = r == 15 ? k + 16 : 64;
+      }
     }
-    const int my = mcu / im.mcux, mx = mcu - my * im.mcux;
-    for (int c = 0; c < im.nc; ++c) {
-      const JComp& cp = im.c[c];
-      const int nby = im.interleaved ? cp.v : 1, nbx = im.interleaved ? cp.h : 1;
-      for (int yy = 0; yy < nby; ++yy)
-        for (int xx = 0; xx < nbx; ++xx) {
-          const int by = im.interleaved ? my * cp.v + yy : my, bx = im.interleaved ? mx * cp.h + xx : mx;
-          short* blk = coef + cp.coef_off + ((int64_t)by * cp.bw + bx) * 64;
-          for (int i = 0; i < 64; ++i) blk[i] = 0;
-          int s = br.decode(pool[cp.dc]);
-          if (s) s = huff_extend(br.get(s), s);
-          pred[c] += s;
-          blk[0] = (short)pred[c];
-          const HuffTab& at = pool[cp.ac];
-          for (int k = 1; k < 64; ++k) {
-            int r = br.decode(at);
-            s = r & 15;
-            r >>= 4;
-            if (s) {
-              k += r;
-              const int v = huff_extend(br.get(s), s);
-              blk[nat[k]] = (short)v;
-            } else {
-              if (r != 15) break;
-              k += 15;
-            }
-          }
-        }
+    if (k >= 64) {
+      k = 0;
+      b = b + 1 == im.bpm ? 0 : b + 1;
+    }
+  }
+  cnt[0] = nblk;
+  cnt[1] = dc0;
+  cnt[2] = dc1;
+  cnt[3] = dc2;
+  return st_pack(bs.pos, b, k);
+}
+
+// Output pass over one chunk from its exact start state: g = index (in the segment) of the
+// next block to start, pred = DC predictors there.  Stops at the first codeword boundary at
+// or past end_bit, or once every block of the segment has been decoded.
+__host__ __device__ void chunk_write(const JImage& im, const JSeg& sg, const HuffTab* pool, BitStream& bs, int b,
+                                     int k, int end_bit, int g, int pred[3], short* coef, const unsigned char* nat) {
+  const int total = sg.nmcu * im.bpm;
+  short* blk = k > 0 && g > 0 ? block_ptr(im, sg, g - 1, coef) : nullptr;
+  if (k > 0 && !blk) return;  // inconsistent state (cannot happen for an exact state)
+  while (bs.pos < end_bit) {
+    if (k == 0 && g >= total) break;
+    bs.refill();
+    const int c = im.bcomp[b];
+    const JComp& cp = im.c[c];
+    if (k == 0) {
+      blk = block_ptr(im, sg, g, coef);
+      ++g;
+      const int s = bs.decode(pool[cp.dc]);
+      pred[c] += s ? huff_extend(bs.get(s), s) : 0;
+      blk[0] = (short)pred[c];
+      k = 1;
+    } else {
+      const int rs = bs.decode(pool[cp.ac]);
+      const int s = rs & 15, r = rs >> 4;
+      if (s) {
+        k += r;
+        blk[nat[k]] = (short)huff_extend(bs.get(s), s);
+        ++k;
+      } else {
+        k = r == 15 ? k + 16 : 64;
+      }
+    }
+    if (k >= 64) {
+      k = 0;
+      b = b + 1 == im.bpm ? 0 : b + 1;
     }
   }
 }
 
-__global__ __launch_bounds__(64) void jpeg_huff_kernel(const uint8_t* __restrict__ data, const JSeg* __restrict__ segs,
-                                                      int nseg, const JImage* __restrict__ imgs,
-                                                      const HuffTab* __restrict__ pool, short* __restrict__ coef) {
+struct ChunkCtx {  // what the chunk kernels share
+  const int* chunk_seg;
+  const JSeg* segs;
+  const JImage* imgs;
+  const HuffTab* pool;
+  const unsigned* words;
+  int nchunks;
+  int chunk_bits;
+};
+
+__host__ __device__ __forceinline__ void chunk_stream(const ChunkCtx& X, const JSeg& sg, int pos, BitStream& bs) {
+  bs.init(X.words + sg.word_off, (sg.nbits + 31) >> 5, pos);
+}
+
+// One synchronisation round (Weissenberger & Schmidt's self-synchronising parallel Huffman
+// decoding, with the JPEG syntax position in the state).  Round 0: every chunk decodes from
+// a guess — its first bit, block 0, DC next — except a segment's first chunk, whose start
+// is exact.  Round t: chunk i adopts chunk i-1's exit state of round t-1 when it differs
+// from the one it started from, re-decodes and raises *changed.  At the fixed point every
+// start state is exact by induction from the segment start.  Last chunks of a segment only
+// record their start state (nothing follows them).
+__host__ __device__ void sync_chunk(const ChunkCtx& X, int i, int round, long long* S, const long long* Ein,
+                                    long long* Eout, int* cnt, int* changed) {
+  const JSeg& sg = X.segs[X.chunk_seg[i]];
+  const int j = i - sg.chunk0;
+  const bool last = j == sg.nchunk - 1;
+  long long s;
+  if (round == 0) {
+    s = st_pack(j * X.chunk_bits, 0, 0);
+    S[i] = s;
+  } else {
+    if (j == 0) {
+      Eout[i] = Ein[i];
+      return;
+    }
+    s = Ein[i - 1];
+    if (s == S[i]) {
+      Eout[i] = Ein[i];
+      return;
+    }
+    S[i] = s;
+    if (!last) *changed = 1;
+  }
+  if (last) {
+    Eout[i] = kStateNone;
+    return;
+  }
+  BitStream bs;
+  chunk_stream(X, sg, st_pos(s), bs);
+  Eout[i] = chunk_sync(X.imgs[sg.img], X.pool, bs, st_b(s), st_k(s), (j + 1) * X.chunk_bits, cnt + 4 * i);
+}
+
+__global__ __launch_bounds__(64) void jpeg_sync_kernel(ChunkCtx X, int round, long long* __restrict__ S,
+                                                      const long long* __restrict__ Ein, long long* __restrict__ Eout,
+                                                      int* __restrict__ cnt, int* __restrict__ changed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < X.nchunks) sync_chunk(X, i, round, S, Ein, Eout, cnt, changed);
+}
+
+// Exclusive scan of the chunk counts inside each segment: first block index and DC
+// predictors at every chunk's start.
+__host__ __device__ void scan_segment(const ChunkCtx& X, const JSeg& sg, const int* cnt, int* G, int* P) {
+  int g = 0, p0 = 0, p1 = 0, p2 = 0;
+  for (int j = 0; j < sg.nchunk; ++j) {
+    const int i = sg.chunk0 + j;
+    G[i] = g;
+    P[3 * i] = p0;
+    P[3 * i + 1] = p1;
+    P[3 * i + 2] = p2;
+    if (j + 1 < sg.nchunk) {
+      g += cnt[4 * i];
+      p0 += cnt[4 * i + 1];
+      p1 += cnt[4 * i + 2];
+      p2 += cnt[4 * i + 3];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void jpeg_scan_kernel(ChunkCtx X, int nseg, const int* __restrict__ cnt,
+                                                      int* __restrict__ G, int* __restrict__ P) {
   const int si = blockIdx.x * blockDim.x + threadIdx.x;
-  if (si >= nseg) return;
-  const JSeg sg = segs[si];
-  huff_segment(data, sg, imgs[sg.img], pool, coef, kNatural);
+  if (si < nseg) scan_segment(X, X.segs[si], cnt, G, P);
+}
+
+__host__ __device__ void write_chunk(const ChunkCtx& X, int i, const long long* S, const int* G, const int* P,
+                                     short* coef, const unsigned char* nat) {
+  const JSeg& sg = X.segs[X.chunk_seg[i]];
+  const int j = i - sg.chunk0;
+  const long long s = S[i];
+  BitStream bs;
+  chunk_stream(X, sg, st_pos(s), bs);
+  int pred[3] = {P[3 * i], P[3 * i + 1], P[3 * i + 2]};
+  const int end = j == sg.nchunk - 1 ? 0x7FFFFFFF : (j + 1) * X.chunk_bits;
+  chunk_write(X.imgs[sg.img], sg, X.pool, bs, st_b(s), st_k(s), end, G[i], pred, coef, nat);
+}
+
+__global__ __launch_bounds__(64) void jpeg_write_kernel(ChunkCtx X, const long long* __restrict__ S,
+                                                       const int* __restrict__ G, const int* __restrict__ P,
+                                                       short* __restrict__ coef) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < X.nchunks) write_chunk(X, i, S, G, P, coef, kNatural);
 }
 
 // jidctint.c jpeg_idct_islow arithmetic
@@ -596,8 +810,8 @@ __host__ __device__ int upsample(const uint8_t* pl, const JComp& cp, int hmax, i
 }
 
 // output pixel k (raster order) of image im: grey copy, grey->BGR, or upsample + YCC->BGR
-__host__ __device__ void out_pixel(const JImage& im, int64_t k, const uint8_t* planes, uint8_t* out) {
-  const int y = (int)(k / im.w), x = (int)(k - (int64_t)y * im.w);
+__host__ __device__ void out_pixel(const JImage& im, int y, int x, const uint8_t* planes, uint8_t* out) {
+  const int64_t k = (int64_t)y * im.w + x;
   const uint8_t* p0 = planes + im.c[0].plane_off;
   const int Y = p0[(int64_t)y * im.c[0].bw * 8 + x];
   if (im.mode == EF_JPEG_GRAY) {
@@ -616,51 +830,59 @@ __host__ __device__ void out_pixel(const JImage& im, int64_t k, const uint8_t* p
   o[2] = clamp255(Y + cr_r(cr));       // R
 }
 
-__global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict__ imgs, const int64_t* __restrict__ px_start,
-                                                      int nimg, int64_t total_px, const uint8_t* __restrict__ planes,
+// One wave per output row (the image found once per wave from the row starts), lanes
+// stride across the row.
+__global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict__ imgs, const int64_t* __restrict__ row_start,
+                                                      int nimg, int64_t total_rows, const uint8_t* __restrict__ planes,
                                                       uint8_t* __restrict__ out) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= total_px) return;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= total_rows) return;
   int lo = 0, hi = nimg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (px_start[mid] <= g) lo = mid; else hi = mid - 1;
+    if (row_start[mid] <= r) lo = mid; else hi = mid - 1;
   }
-  out_pixel(imgs[lo], g - px_start[lo], planes, out);
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  const JImage& im = imgs[lo];
+  const int y = (int)(r - row_start[lo]);
+  for (int x = threadIdx.x & 63; x < im.w; x += 64) out_pixel(im, y, x, planes, out);
 }
 
 // ------------------------------------------------------------------ batch layout
 // Everything one decode launch needs, built on the host: per-image geometry, Huffman and
-// quantisation tables, entropy segments, IDCT runs and output pixel starts.
+// quantisation tables, entropy segments and their chunks, IDCT runs, output pixel starts.
 struct Batch {
-  std::vector<HuffTab> pool;
-  std::vector<unsigned short> qpool;
+  Tables T;
   std::vector<JSeg> segs;
   std::vector<JImage> imgs;
   std::vector<int> img_of;            // input index of each decoded image
   std::vector<int64_t> block_start;   // IDCT runs: first global block of (image, component)
   std::vector<int> ic;                // (image << 2) | component of each run
-  std::vector<int64_t> px_start;      // first output pixel of each image
-  int64_t data_bytes = 0, coef_blocks = 0, plane_bytes = 0, blocks = 0, pixels = 0, dense_out = 0;
+  std::vector<int64_t> row_start;     // first output row of each image (rows of all images in order)
+  std::vector<int> chunk_seg;         // segment of each chunk
+  int64_t words = 0;                  // 32-bit words reserved for the destuffed segments
+  int chunk_bits = 0;
+  int64_t coef_blocks = 0, plane_bytes = 0, blocks = 0, rows = 0, dense_out = 0;
 };
 
-// dev_out: images land at out_offsets (device layout); otherwise packed densely
+// out_offsets: images land there (device layout); null: packed densely
 void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int count, int mode,
                  const int64_t* out_offsets, int32_t* status, Batch& B) {
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   for (int i = 0; i < count; ++i) {
     JImage im{};
-    const size_t seg0 = B.segs.size(), pool0 = B.pool.size(), q0 = B.qpool.size();
-    int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], (int)B.imgs.size(), im, B.pool, B.qpool, B.segs,
-                                  B.data_bytes, true)
+    const size_t seg0 = B.segs.size();
+    int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], (int)B.imgs.size(), im, B.T, B.segs, true)
                           : EF_JPEG_E_CORRUPT;
     if (st == 0 && (int64_t)im.w * im.h > ((int64_t)1 << 31)) st = EF_JPEG_E_UNSUPPORTED;
     if (status) status[i] = st;
     if (st != 0) {
       B.segs.resize(seg0);
-      B.pool.resize(pool0);
-      B.qpool.resize(q0);
       continue;
+    }
+    for (size_t k = seg0; k < B.segs.size(); ++k) {  // destuffed bytes never exceed the raw ones
+      B.segs[k].word_off = B.words;
+      B.words += (B.segs[k].end - B.segs[k].beg + 3) / 4 + 1;
     }
     im.mode = mode;
     const int nneed = mode == EF_JPEG_GRAY ? 1 : im.nc;  // grey output needs the luma plane only
@@ -677,12 +899,203 @@ void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* siz
     }
     im.out_off = out_offsets ? out_offsets[i] : B.dense_out;
     B.dense_out += (int64_t)im.w * im.h * ch;
-    B.px_start.push_back(B.pixels);
-    B.pixels += (int64_t)im.w * im.h;
+    B.row_start.push_back(B.rows);
+    B.rows += im.h;
     B.img_of.push_back(i);
     B.imgs.push_back(im);
-    B.data_bytes += sizes[i];
   }
+}
+
+// Copy segment sg's entropy bytes without the 0xFF00 stuffing into dst (zero-padded to a
+// whole word); stops at the first marker, as jdhuff.c's fill_bit_buffer does.  Sets nbits.
+void destuff(const uint8_t* src, int64_t n, JSeg& sg, uint8_t* dst) {
+  int64_t q = 0, o = 0;
+  while (q < n) {
+    const void* f = std::memchr(src + q, 0xFF, (size_t)(n - q));
+    const int64_t run = f ? static_cast<const uint8_t*>(f) - (src + q) : n - q;
+    std::memcpy(dst + o, src + q, (size_t)run);
+    o += run;
+    q += run;
+    if (!f) break;
+    if (q + 1 < n && src[q + 1] == 0x00) {  // stuffed 0xFF
+      dst[o++] = 0xFF;
+      q += 2;
+      continue;
+    }
+    break;  // a marker (or 0xFF fill before one, or a lone trailing 0xFF)
+  }
+  const int64_t padded = (o + 3) / 4 * 4 + 4;
+  std::memset(dst + o, 0, (size_t)(padded - o));
+  sg.nbits = (int)(o * 8);
+}
+
+void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* words) {
+  const size_t n = B.segs.size();
+  auto work = [&](size_t a, size_t e) {
+    for (size_t k = a; k < e; ++k) {
+      JSeg& sg = B.segs[k];
+      const uint8_t* file = data + offsets[B.img_of[sg.img]];
+      destuff(file + sg.beg, sg.end - sg.beg, sg, words + sg.word_off * 4);
+    }
+  };
+  const int64_t bytes = B.words * 4;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = bytes < ((int64_t)4 << 20) ? 1 : std::min<size_t>({16, hw, n});
+  if (nt <= 1) {
+    work(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+  for (auto& t : th) t.join();
+}
+
+// Chunk size: about 128k chunks for the batch (4 per SIMD lane group of the chip), kept in
+// [2048, 16384] bits so self-synchronisation stays a small fraction of each chunk.
+void make_chunks(Batch& B, int64_t opt_bits) {
+  int64_t total = 0;
+  for (const JSeg& sg : B.segs) total += sg.nbits;
+  int64_t cb = opt_bits > 0 ? opt_bits : (total / 131072 + 255) / 256 * 256;
+  cb = std::max<int64_t>(opt_bits > 0 ? 64 : 2048, std::min<int64_t>(cb, 16384));
+  B.chunk_bits = (int)cb;
+  B.chunk_seg.clear();
+  for (size_t k = 0; k < B.segs.size(); ++k) {
+    JSeg& sg = B.segs[k];
+    sg.chunk0 = (int)B.chunk_seg.size();
+    sg.nchunk = (int)std::max<int64_t>(1, (sg.nbits + cb - 1) / cb);
+    B.chunk_seg.insert(B.chunk_seg.end(), sg.nchunk, (int)k);
+  }
+}
+
+// Upload, entropy-decode, IDCT and colour-convert a built batch into dout (device), each
+// image at its out_off.  Stream-ordered on ctx's stream.
+int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* dout) {
+  hipStream_t s = c->stream;
+  // layout: one pinned upload [destuffed words | images | Huffman tables | quant tables |
+  // segments | chunk->segment | IDCT runs | pixel starts] at the front of the device
+  // workspace, then device-only [chunk states S, E x2 | counts | block starts | DC preds |
+  // flag | coefficients | sample planes]
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  size_t off = 0;
+  const size_t o_words = off; off += al((size_t)B.words * 4 + 16);
+  const size_t o_imgs = off; off += al(B.imgs.size() * sizeof(JImage));
+  const size_t o_pool = off; off += al(std::max<size_t>(B.T.huff.size(), 1) * sizeof(HuffTab));
+  const size_t o_q = off; off += al(std::max<size_t>(B.T.quant.size(), 1) * 2);
+  const size_t o_seg = off; off += al(B.segs.size() * sizeof(JSeg));
+  const size_t o_bs = off; off += al(B.block_start.size() * 8);
+  const size_t o_ic = off; off += al(B.ic.size() * 4);
+  const size_t o_ps = off; off += al(B.row_start.size() * 8);
+  const size_t o_cseg = off;  // chunk table last: its size is known only after destuffing
+  // the previous call's upload may still be reading the pinned buffer
+  {
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
+  }
+  const size_t pin_need = o_cseg;
+  if (c->jpeg_pinned_bytes < pin_need) {
+    if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
+    c->jpeg_pinned = nullptr;
+    c->jpeg_pinned_bytes = 0;
+    const hipError_t e = hipHostMalloc(&c->jpeg_pinned, pin_need + pin_need / 4 + 4096, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      c->jpeg_pinned = nullptr;
+      return hip_err(c, e, "hipHostMalloc (jpeg staging)");
+    }
+    c->jpeg_pinned_bytes = pin_need + pin_need / 4 + 4096;
+  }
+  char* h = static_cast<char*>(c->jpeg_pinned);
+  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + o_words));
+  make_chunks(B, c->opt_jpeg_chunk_bits);
+  const int nchunks = (int)B.chunk_seg.size();
+  std::memcpy(h + o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
+  if (!B.T.huff.empty()) std::memcpy(h + o_pool, B.T.huff.data(), B.T.huff.size() * sizeof(HuffTab));
+  if (!B.T.quant.empty()) std::memcpy(h + o_q, B.T.quant.data(), B.T.quant.size() * 2);
+  std::memcpy(h + o_seg, B.segs.data(), B.segs.size() * sizeof(JSeg));
+  std::memcpy(h + o_bs, B.block_start.data(), B.block_start.size() * 8);
+  std::memcpy(h + o_ic, B.ic.data(), B.ic.size() * 4);
+  std::memcpy(h + o_ps, B.row_start.data(), B.row_start.size() * 8);
+  const size_t up_bytes = o_cseg;
+  const size_t o_S = off + al((size_t)nchunks * 4);
+  off = o_S;
+  off += al((size_t)nchunks * 8);
+  const size_t o_E0 = off; off += al((size_t)nchunks * 8);
+  const size_t o_E1 = off; off += al((size_t)nchunks * 8);
+  const size_t o_cnt = off; off += al((size_t)nchunks * 16);
+  const size_t o_G = off; off += al((size_t)nchunks * 4);
+  const size_t o_P = off; off += al((size_t)nchunks * 12);
+  const size_t o_flag = off; off += al(16);
+  const size_t o_coef = off; off += al((size_t)B.coef_blocks * 64 * 2);
+  const size_t o_planes = off; off += al((size_t)B.plane_bytes + 16);
+  {
+    const int rc = ensure(c, c->jpeg_ws, off);
+    if (rc != EF_OK) return rc;
+  }
+  char* base = static_cast<char*>(c->jpeg_ws.p);
+  hipError_t e = hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)  // pageable; complete before the first round's flag read below
+    e = hipMemcpyAsync(base + o_cseg, B.chunk_seg.data(), (size_t)nchunks * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(base + o_coef, 0, (size_t)B.coef_blocks * 64 * 2, s);
+  ChunkCtx X;
+  X.chunk_seg = reinterpret_cast<const int*>(base + o_cseg);
+  X.segs = reinterpret_cast<const JSeg*>(base + o_seg);
+  X.imgs = reinterpret_cast<const JImage*>(base + o_imgs);
+  X.pool = reinterpret_cast<const HuffTab*>(base + o_pool);
+  X.words = reinterpret_cast<const unsigned*>(base + o_words);
+  X.nchunks = nchunks;
+  X.chunk_bits = B.chunk_bits;
+  long long* S = reinterpret_cast<long long*>(base + o_S);
+  long long* E[2] = {reinterpret_cast<long long*>(base + o_E0), reinterpret_cast<long long*>(base + o_E1)};
+  int* cnt = reinterpret_cast<int*>(base + o_cnt);
+  int* G = reinterpret_cast<int*>(base + o_G);
+  int* P = reinterpret_cast<int*>(base + o_P);
+  int* flag = reinterpret_cast<int*>(base + o_flag);
+  int* hflag = reinterpret_cast<int*>(h + pin_need);  // in the pinned buffer's slack
+  int max_chunks = 1;
+  for (const JSeg& sg : B.segs) max_chunks = std::max(max_chunks, sg.nchunk);
+  TimerEvt tev;
+  timer_begin(c, EF_KERNEL_JPEG, &tev);
+  const unsigned cgrid = (unsigned)((nchunks + 63) / 64);
+  int rounds = 0;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(64), 0, s, X, 0, S, E[1], E[0], cnt, flag);
+    e = hipGetLastError();
+  }
+  // synchronisation rounds until no start state changes; at most one per chunk of the
+  // longest segment (each round makes at least the next chunk in every segment exact)
+  int cur = 0;
+  for (int r = 1; e == hipSuccess && r <= max_chunks; ++r) {
+    e = hipMemsetAsync(flag, 0, 4, s);
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(64), 0, s, X, r, S, E[cur], E[cur ^ 1], cnt, flag);
+    e = hipGetLastError();
+    cur ^= 1;
+    rounds = r;
+    if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess || *hflag == 0) break;
+  }
+  c->jpeg_rounds = rounds;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
+                       (int)B.segs.size(), cnt, G, P);
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(64), 0, s, X, S, G, P,
+                       reinterpret_cast<short*>(base + o_coef));
+    const JImage* d_imgs = X.imgs;
+    short* d_coef = reinterpret_cast<short*>(base + o_coef);
+    uint8_t* d_planes = reinterpret_cast<uint8_t*>(base + o_planes);
+    if (B.blocks > 0)
+      hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((B.blocks + kIdctBlocks - 1) / kIdctBlocks)), dim3(256), 0,
+                         s, d_coef, d_imgs, reinterpret_cast<const int64_t*>(base + o_bs), (int)B.block_start.size(),
+                         reinterpret_cast<const int*>(base + o_ic), reinterpret_cast<const unsigned short*>(base + o_q),
+                         B.blocks, d_planes);
+    if (B.rows > 0)
+      hipLaunchKernelGGL(jpeg_out_kernel, dim3((unsigned)((B.rows + 3) / 4)), dim3(256), 0, s, d_imgs,
+                         reinterpret_cast<const int64_t*>(base + o_ps), (int)B.imgs.size(), B.rows, d_planes, dout);
+    e = hipGetLastError();
+  }
+  timer_end(c, &tev);
+  if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
+  return EF_OK;
 }
 
 }  // namespace
@@ -695,14 +1108,11 @@ extern "C" {
 int ef_jpeg_info(const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count, int32_t* heights,
                  int32_t* widths, int32_t* components, int32_t* status) {
   if (count < 0 || (count > 0 && (!data || !offsets || !sizes))) return EF_E_INVALID;
-  std::vector<HuffTab> pool;
-  std::vector<unsigned short> qpool;
+  Tables T;
   std::vector<JSeg> segs;
   for (int i = 0; i < count; ++i) {
     JImage im{};
-    pool.clear();
-    qpool.clear();
-    int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], i, im, pool, qpool, segs, 0, false) : EF_JPEG_E_CORRUPT;
+    int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], i, im, T, segs, false) : EF_JPEG_E_CORRUPT;
     if (st == 0 && (int64_t)im.w * im.h > ((int64_t)1 << 31)) st = EF_JPEG_E_UNSUPPORTED;
     if (heights) heights[i] = st == 0 ? im.h : 0;
     if (widths) widths[i] = st == 0 ? im.w : 0;
@@ -720,99 +1130,22 @@ int ef_jpeg_decode(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     return set_err(c, EF_E_INVALID, "ef_jpeg_decode: bad arguments");
   if (count == 0) return EF_OK;
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->stream;
   const bool dev_out = (flags & EF_MEM_DEVICE) != 0;
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   Batch B;
   build_batch(data, offsets, sizes, count, mode, dev_out ? out_offsets : nullptr, status, B);
   if (B.imgs.empty()) return EF_OK;
-  // one pinned upload [files | images | Huffman tables | quant tables | segments | runs]
-  // into the front of the device workspace; coefficients and sample planes follow
-  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  size_t off = 0;
-  const size_t o_data = off; off += al((size_t)B.data_bytes + 16);
-  const size_t o_imgs = off; off += al(B.imgs.size() * sizeof(JImage));
-  const size_t o_pool = off; off += al(std::max<size_t>(B.pool.size(), 1) * sizeof(HuffTab));
-  const size_t o_q = off; off += al(std::max<size_t>(B.qpool.size(), 1) * 2);
-  const size_t o_seg = off; off += al(std::max<size_t>(B.segs.size(), 1) * sizeof(JSeg));
-  const size_t o_bs = off; off += al(B.block_start.size() * 8);
-  const size_t o_ic = off; off += al(B.ic.size() * 4);
-  const size_t o_ps = off; off += al(B.px_start.size() * 8);
-  const size_t up_bytes = off;
-  const size_t o_coef = off; off += al((size_t)B.coef_blocks * 64 * 2);
-  const size_t o_planes = off; off += al((size_t)B.plane_bytes + 16);
-  // the previous call's upload may still be reading the pinned buffer
-  {
-    const hipError_t e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
-  }
-  if (c->jpeg_pinned_bytes < up_bytes) {
-    if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
-    c->jpeg_pinned = nullptr;
-    c->jpeg_pinned_bytes = 0;
-    const hipError_t e = hipHostMalloc(&c->jpeg_pinned, up_bytes, hipHostMallocDefault);
-    if (e != hipSuccess) {
-      c->jpeg_pinned = nullptr;
-      return hip_err(c, e, "hipHostMalloc (jpeg staging)");
-    }
-    c->jpeg_pinned_bytes = up_bytes;
-  }
-  char* h = static_cast<char*>(c->jpeg_pinned);
-  {
-    int64_t o = 0;
-    for (size_t i = 0; i < B.imgs.size(); ++i) {
-      const int idx = B.img_of[i];
-      std::memcpy(h + o_data + o, data + offsets[idx], (size_t)sizes[idx]);
-      o += sizes[idx];
-    }
-    std::memset(h + o_data + o, 0, 16);
-  }
-  std::memcpy(h + o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
-  if (!B.pool.empty()) std::memcpy(h + o_pool, B.pool.data(), B.pool.size() * sizeof(HuffTab));
-  if (!B.qpool.empty()) std::memcpy(h + o_q, B.qpool.data(), B.qpool.size() * 2);
-  if (!B.segs.empty()) std::memcpy(h + o_seg, B.segs.data(), B.segs.size() * sizeof(JSeg));
-  std::memcpy(h + o_bs, B.block_start.data(), B.block_start.size() * 8);
-  std::memcpy(h + o_ic, B.ic.data(), B.ic.size() * 4);
-  std::memcpy(h + o_ps, B.px_start.data(), B.px_start.size() * 8);
-  {
-    const int rc = ensure(c, c->jpeg_ws, off);
-    if (rc != EF_OK) return rc;
-  }
   uint8_t* dout = out;
   if (!dev_out) {
     const int rc = ensure(c, c->jpeg_out, (size_t)B.dense_out + 16);
     if (rc != EF_OK) return rc;
     dout = static_cast<uint8_t*>(c->jpeg_out.p);
   }
-  char* base = static_cast<char*>(c->jpeg_ws.p);
-  hipError_t e = hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, s);
-  TimerEvt tev;
-  timer_begin(c, EF_KERNEL_JPEG, &tev);
-  if (e == hipSuccess) {
-    const uint8_t* d_data = reinterpret_cast<const uint8_t*>(base + o_data);
-    const JImage* d_imgs = reinterpret_cast<const JImage*>(base + o_imgs);
-    short* d_coef = reinterpret_cast<short*>(base + o_coef);
-    uint8_t* d_planes = reinterpret_cast<uint8_t*>(base + o_planes);
-    if (!B.segs.empty())
-      hipLaunchKernelGGL(jpeg_huff_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, d_data,
-                         reinterpret_cast<const JSeg*>(base + o_seg), (int)B.segs.size(), d_imgs,
-                         reinterpret_cast<const HuffTab*>(base + o_pool), d_coef);
-    if (B.blocks > 0)
-      hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((B.blocks + kIdctBlocks - 1) / kIdctBlocks)), dim3(256), 0,
-                         s, d_coef, d_imgs, reinterpret_cast<const int64_t*>(base + o_bs), (int)B.block_start.size(),
-                         reinterpret_cast<const int*>(base + o_ic), reinterpret_cast<const unsigned short*>(base + o_q),
-                         B.blocks, d_planes);
-    if (B.pixels > 0)
-      hipLaunchKernelGGL(jpeg_out_kernel, dim3((unsigned)((B.pixels + 255) / 256)), dim3(256), 0, s, d_imgs,
-                         reinterpret_cast<const int64_t*>(base + o_ps), (int)B.imgs.size(), B.pixels, d_planes, dout);
-    e = hipGetLastError();
-  }
-  timer_end(c, &tev);
-  if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
-  if (dev_out) return EF_OK;  // stream-ordered, like the other EF_MEM_DEVICE calls
+  const int rc = decode_batch(c, B, data, offsets, dout);
+  if (rc != EF_OK || dev_out) return rc;  // device output: stream-ordered like other EF_MEM_DEVICE calls
   std::vector<uint8_t> dense((size_t)B.dense_out);
-  e = hipMemcpyAsync(dense.data(), dout, (size_t)B.dense_out, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  hipError_t e = hipMemcpyAsync(dense.data(), dout, (size_t)B.dense_out, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   for (size_t i = 0; i < B.imgs.size(); ++i)
     std::memcpy(out + out_offsets[B.img_of[i]], dense.data() + B.imgs[i].out_off, (size_t)B.imgs[i].w * B.imgs[i].h * ch);
@@ -826,34 +1159,32 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       (mode != EF_JPEG_GRAY && mode != EF_JPEG_BGR))
     return set_err(c, EF_E_INVALID, "ef_jpeg_ingest: bad arguments");
   if (count == 0) return EF_OK;
+  (void)hipSetDevice(c->device);
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   const int64_t row = (int64_t)out_h * out_w;
   for (int32_t a = 0; a < count; a += 65535) {  // ef_preprocess's per-call image limit
     const int32_t m = std::min<int32_t>(65535, count - a);
-    std::vector<int32_t> hh(m), ww(m), st(m), cc(m, ch);
-    std::vector<int64_t> doff(m);
-    int rc = ef_jpeg_info(data, offsets + a, sizes + a, m, hh.data(), ww.data(), nullptr, st.data());
-    if (rc != EF_OK) return set_err(c, rc, "ef_jpeg_ingest: bad arguments");
-    int64_t dense = 0;
-    for (int32_t i = 0; i < m; ++i) {
-      doff[i] = dense;
-      if (st[i] == 0) dense += (int64_t)hh[i] * ww[i] * ch;
-    }
-    rc = ensure(c, c->jpeg_out, (size_t)dense + 256);
+    std::vector<int32_t> st(m), hh(m, 1), ww(m, 1), cc(m, 1);
+    Batch B;
+    build_batch(data, offsets + a, sizes + a, m, mode, nullptr, st.data(), B);
+    int rc = ensure(c, c->jpeg_out, (size_t)B.dense_out + 256);
     if (rc != EF_OK) return rc;
     uint8_t* pix = static_cast<uint8_t*>(c->jpeg_out.p);
-    rc = ef_jpeg_decode(c, data, offsets + a, sizes + a, m, mode, pix, doff.data(), st.data(), EF_MEM_DEVICE);
-    if (rc != EF_OK) return rc;
+    if (!B.imgs.empty()) {
+      rc = decode_batch(c, B, data, offsets + a, pix);
+      if (rc != EF_OK) return rc;
+    }
     // a file the GPU decoder does not take becomes a 1x1 zero image: its row is zero
-    bool any_bad = false;
-    for (int32_t i = 0; i < m; ++i)
-      if (st[i] != 0) {
-        any_bad = true;
-        doff[i] = dense;
-        hh[i] = ww[i] = cc[i] = 1;
-      }
-    if (any_bad) {
-      const hipError_t e = hipMemsetAsync(pix + dense, 0, 16, c->stream);
+    std::vector<int64_t> doff(m, B.dense_out);
+    for (size_t i = 0; i < B.imgs.size(); ++i) {
+      const int k = B.img_of[i];
+      doff[k] = B.imgs[i].out_off;
+      hh[k] = B.imgs[i].h;
+      ww[k] = B.imgs[i].w;
+      cc[k] = ch;
+    }
+    if ((int32_t)B.imgs.size() < m) {
+      const hipError_t e = hipMemsetAsync(pix + B.dense_out, 0, 16, c->stream);
       if (e != hipSuccess) return hip_err(c, e, "jpeg ingest");
     }
     uint8_t* rows = out + (int64_t)a * row;
@@ -876,29 +1207,45 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
 
 }  // extern "C"
 
+
 #ifdef EF_DIAGNOSTICS
 // Diagnostic build only (never loaded by the package): the same per-thread device
 // functions run in host loops, so decoder changes can be checked on a machine without
-// a GPU (tools/micro/jpeg_host_check.py).  Output layout as ef_jpeg_decode's host form.
+// a GPU (tools/micro/jpeg_host_check.py).  Output layout as ef_jpeg_decode's host form;
+// *rounds_out receives the number of synchronisation rounds.
 extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offsets, const int64_t* sizes,
                                         int32_t count, int32_t mode, uint8_t* out, const int64_t* out_offsets,
-                                        int32_t* status) {
+                                        int32_t* status, int32_t chunk_bits, int32_t* rounds_out) {
   Batch B;
   build_batch(data, offsets, sizes, count, mode, out_offsets, status, B);
-  std::vector<uint8_t> cat((size_t)B.data_bytes + 16, 0);
-  int64_t o = 0;
-  for (size_t i = 0; i < B.imgs.size(); ++i) {
-    const int idx = B.img_of[i];
-    std::memcpy(cat.data() + o, data + offsets[idx], (size_t)sizes[idx]);
-    o += sizes[idx];
+  std::vector<unsigned> words((size_t)B.words + 4, 0);
+  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(words.data()));
+  make_chunks(B, chunk_bits);
+  const int nch = (int)B.chunk_seg.size();
+  ChunkCtx X{B.chunk_seg.data(), B.segs.data(), B.imgs.data(), B.T.huff.data(), words.data(), nch, B.chunk_bits};
+  std::vector<long long> S(nch), E0(nch), E1(nch);
+  std::vector<int> cnt((size_t)nch * 4), G(nch), P((size_t)nch * 3);
+  int changed = 0;
+  for (int i = 0; i < nch; ++i) sync_chunk(X, i, 0, S.data(), E1.data(), E0.data(), cnt.data(), &changed);
+  long long* Ein = E0.data();
+  long long* Eout = E1.data();
+  int rounds = 0;
+  for (int r = 1; r <= nch + 1; ++r) {
+    changed = 0;
+    for (int i = 0; i < nch; ++i) sync_chunk(X, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
+    std::swap(Ein, Eout);
+    rounds = r;
+    if (!changed) break;
   }
-  std::vector<short> coef((size_t)B.coef_blocks * 64 + 64);
+  if (rounds_out) *rounds_out = rounds;
+  for (const JSeg& sg : B.segs) scan_segment(X, sg, cnt.data(), G.data(), P.data());
+  std::vector<short> coef((size_t)B.coef_blocks * 64 + 64, 0);
+  for (int i = 0; i < nch; ++i) write_chunk(X, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost);
   std::vector<uint8_t> planes((size_t)B.plane_bytes + 16);
-  for (const JSeg& sg : B.segs) huff_segment(cat.data(), sg, B.imgs[sg.img], B.pool.data(), coef.data(), kNaturalHost);
   for (size_t r = 0; r < B.block_start.size(); ++r) {
     const JImage& im = B.imgs[B.ic[r] >> 2];
     const JComp& cp = im.c[B.ic[r] & 3];
-    const unsigned short* q = B.qpool.data() + (int64_t)(im.qt_base + cp.q) * 64;
+    const unsigned short* q = B.T.quant.data() + (int64_t)(im.qt_base + cp.q) * 64;
     for (int64_t b = 0; b < (int64_t)cp.bw * cp.bh; ++b) {
       int w[64];
       for (int j = 0; j < 8; ++j) idct_col(coef.data() + cp.coef_off + b * 64, q, j, w);
@@ -910,7 +1257,27 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
     }
   }
   for (const JImage& im : B.imgs)
-    for (int64_t k = 0; k < (int64_t)im.w * im.h; ++k) out_pixel(im, k, planes.data(), out);
+    for (int y = 0; y < im.h; ++y)
+      for (int x = 0; x < im.w; ++x) out_pixel(im, y, x, planes.data(), out);
   return EF_OK;
+}
+// host preparation only (parse, destuff, chunking): wall time of each stage in ms
+extern "C" int ef_diag_jpeg_prep_host(const uint8_t* data, const int64_t* offsets, const int64_t* sizes,
+                                      int32_t count, int32_t mode, double* ms3) {
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const auto t0 = now();
+  Batch B;
+  build_batch(data, offsets, sizes, count, mode, nullptr, nullptr, B);
+  std::vector<unsigned> words((size_t)B.words + 4, 0);
+  const auto t1 = now();
+  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(words.data()));
+  const auto t2 = now();
+  make_chunks(B, 0);
+  const auto t3 = now();
+  ms3[0] = ms(t0, t1);
+  ms3[1] = ms(t1, t2);
+  ms3[2] = ms(t2, t3);
+  return (int)B.T.huff.size();
 }
 #endif

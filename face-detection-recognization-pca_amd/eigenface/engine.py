@@ -35,7 +35,7 @@ def _dev(x, torch_dtype):
 
 _OPTIONS = {"fit_max_iters": N.EF_OPT_FIT_MAX_ITERS, "fit_fp32_coarse": N.EF_OPT_FIT_FP32_COARSE,
             "cov_slab_bytes": N.EF_OPT_COV_SLAB_BYTES, "tm_int64_sums": N.EF_OPT_TM_INT64_SUMS,
-            "haar_ordered": N.EF_OPT_HAAR_ORDERED}
+            "haar_ordered": N.EF_OPT_HAAR_ORDERED, "jpeg_chunk_bits": N.EF_OPT_JPEG_CHUNK_BITS}
 
 
 def _option(o):
@@ -469,17 +469,18 @@ class Engine:
         (IMREAD_GRAYSCALE).  Returns a list of uint8 arrays, None where the GPU decoder
         does not take the file (progressive, CMYK, ...; ``status`` says why)."""
         m = _jpeg_mode(mode)
-        data, offs, sizes = _pack_blobs(blobs)
         n = len(blobs)
         if n == 0:
             return []
-        h, w, _, st = jpeg_info(blobs, _packed=(data, offs, sizes))
+        packed = _pack_blobs(blobs)
+        data, offs, sizes, _keep = packed
+        h, w, _, st = jpeg_info(blobs, _packed=packed)
         ch = 1 if m == N.EF_JPEG_GRAY else 3
         px = np.where(st == 0, h.astype(np.int64) * w * ch, 0)
         ooff = np.zeros(n, np.int64)
         ooff[1:] = np.cumsum(px)[:-1]
         out = np.empty(max(1, int(px.sum())), np.uint8)
-        self._chk(self._lib.ef_jpeg_decode(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+        self._chk(self._lib.ef_jpeg_decode(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,
                                            out.ctypes.data, ooff.ctypes.data, st.ctypes.data, 0))
         res = []
         for i in range(n):
@@ -500,16 +501,16 @@ class Engine:
         st = np.zeros(n, np.int32)
         if n == 0:
             return np.empty((0, oh * ow), np.uint8), st
-        data, offs, sizes = _pack_blobs(blobs)
+        data, offs, sizes, _keep = _pack_blobs(blobs)
         if out is not None:
             import torch
             o, op = _dev(out, torch.uint8)
             self._dev_out(o, (n, oh * ow), torch.uint8, "out")
-            self._chk(self._lib.ef_jpeg_ingest(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+            self._chk(self._lib.ef_jpeg_ingest(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,
                                                oh, ow, op, st.ctypes.data, N.EF_MEM_DEVICE))
             return out, st
         rows = np.empty((n, oh * ow), np.uint8)
-        self._chk(self._lib.ef_jpeg_ingest(self._h, data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, m,
+        self._chk(self._lib.ef_jpeg_ingest(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,
                                            oh, ow, rows.ctypes.data, st.ctypes.data, 0))
         return rows, st
 
@@ -615,26 +616,23 @@ def _jpeg_mode(mode):
 
 
 def _pack_blobs(blobs):
-    """Concatenate file contents: (uint8 buffer, int64 offsets, int64 sizes)."""
-    mv = [memoryview(b).cast("B") for b in blobs]
-    sizes = np.array([len(b) for b in mv], np.int64)
-    offs = np.zeros(len(mv), np.int64)
-    if len(mv) > 1:
-        offs[1:] = np.cumsum(sizes)[:-1]
-    data = np.empty(max(1, int(sizes.sum())), np.uint8)
-    for o, b in zip(offs, mv):
-        data[o:o + len(b)] = np.frombuffer(b, np.uint8)
-    return data, offs, sizes
+    """Address the files in place (no concatenation): (base pointer, int64 offsets from it,
+    int64 sizes, keep-alive list).  The C ABI reads file i at base + offsets[i]."""
+    views = [np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8) for b in blobs]
+    sizes = np.fromiter((len(b) for b in blobs), np.int64, len(blobs))
+    addrs = np.fromiter((v.ctypes.data for v in views), np.int64, len(views))
+    base = int(addrs.min()) if len(views) else 0
+    return base, addrs - base, sizes, views
 
 
 def jpeg_info(blobs, _packed=None):
     """Header parse on the host (ef_jpeg_info, no GPU): (height, width, components,
     status) int32 arrays; status 0 = the GPU decoder takes the file."""
-    data, offs, sizes = _packed if _packed is not None else _pack_blobs(blobs)
+    data, offs, sizes, _keep = _packed if _packed is not None else _pack_blobs(blobs)
     n = len(sizes)
     h, w, c, st = (np.zeros(n, np.int32) for _ in range(4))
     if n:
-        rc = N.lib().ef_jpeg_info(data.ctypes.data, offs.ctypes.data, sizes.ctypes.data, n, h.ctypes.data,
+        rc = N.lib().ef_jpeg_info(data, offs.ctypes.data, sizes.ctypes.data, n, h.ctypes.data,
                                   w.ctypes.data, c.ctypes.data, st.ctypes.data)
         if rc != N.EF_OK:
             raise N.EigenfaceError(rc, "ef_jpeg_info failed")
