@@ -29,6 +29,8 @@
 // planes; kernel 3 writes one output pixel per thread (grey copy, or upsample + YCC->BGR).
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -42,8 +44,12 @@ namespace {
 
 constexpr int kMaxComp = 3;
 
-struct HuffTab {                // libjpeg d_derived_tbl
-  unsigned short look[256];     // (nbits << 8) | symbol for codes <= 8 bits; nbits 0 = longer
+constexpr int kLookBits = 12;   // lookahead bits (libjpeg uses 8; 12 covers nearly every code)
+constexpr int kLookSize = 1 << kLookBits;
+constexpr int kLdsTables = 8;   // batches with at most this many distinct tables decode from LDS
+
+struct HuffTab {                // libjpeg d_derived_tbl with a 12-bit lookahead
+  unsigned short look[kLookSize];  // (nbits << 8) | symbol for codes <= 12 bits; nbits 0 = longer
   int maxcode[18];              // largest code of each length (-1: none), maxcode[17] sentinel
   int valoffset[18];            // huffval index offset per length
   unsigned char huffval[256];
@@ -128,12 +134,13 @@ bool derive(const RawHuff& r, HuffTab& t, bool dc) {  // jdhuff.c jpeg_make_d_de
   t.maxcode[17] = 0x7FFFFFFF;  // sentinel: ensures the slow decode terminates
   t.maxcode[0] = -1;
   t.valoffset[0] = 0;
-  for (int i = 0; i < 256; ++i) t.look[i] = 0;
+  for (int i = 0; i < kLookSize; ++i) t.look[i] = 0;
   p = 0;
-  for (int l = 1; l <= 8; ++l)
+  for (int l = 1; l <= kLookBits; ++l)
     for (int i = 1; i <= r.bits[l]; ++i, ++p) {
-      int lookbits = (int)code[p] << (8 - l);
-      for (int ctr = 1 << (8 - l); ctr > 0; --ctr) t.look[lookbits++] = (unsigned short)((l << 8) | r.val[p]);
+      int lookbits = (int)code[p] << (kLookBits - l);
+      for (int ctr = 1 << (kLookBits - l); ctr > 0; --ctr)
+        t.look[lookbits++] = (unsigned short)((l << 8) | r.val[p]);
     }
   for (int i = 0; i < 256; ++i) t.huffval[i] = i < last ? r.val[i] : 0;
   if (dc)  // DC categories above 15 are rejected as libjpeg does (JERR_BAD_HUFF_TABLE)
@@ -386,26 +393,27 @@ const unsigned char kNaturalHost[80] = EF_NATURAL_ORDER;
 struct BitStream {
   const unsigned* w;
   int nw;
-  int widx;
-  int pos;  // bit offset of the next unread bit
-  int bits; // valid bits in buf
+  int widx;   // index of the word after nextw
+  int pos;    // bit offset of the next unread bit
+  int bits;   // valid bits in buf
+  unsigned nextw;  // the word the next refill appends, loaded one refill ahead
   unsigned long long buf;
   __host__ __device__ unsigned word(int i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
-  __host__ __device__ void init(const unsigned* words, int nwords, int p) {
+  __host__ __device__ __forceinline__ void init(const unsigned* words, int nwords, int p) {
     w = words;
     nw = nwords;
-    widx = p >> 5;
-    const int s = p & 31;
-    buf = (unsigned long long)(word(widx) << s) << 32;
+    const int i = p >> 5, s = p & 31;
+    buf = (unsigned long long)(word(i) << s) << 32;
     bits = 32 - s;
-    ++widx;
+    nextw = word(i + 1);
+    widx = i + 2;
     pos = p;
   }
   __host__ __device__ void refill() {  // afterwards at least 32 bits are buffered
     if (bits <= 32) {
-      buf |= (unsigned long long)word(widx) << (32 - bits);
+      buf |= (unsigned long long)nextw << (32 - bits);
       bits += 32;
-      ++widx;
+      nextw = word(widx++);
     }
   }
   __host__ __device__ unsigned peek(int n) const { return (unsigned)(buf >> (64 - n)); }
@@ -419,20 +427,22 @@ struct BitStream {
     skip(n);
     return v;
   }
-  __host__ __device__ int decode(const HuffTab& t) {  // jdhuff.c HUFF_DECODE
-    const unsigned e = t.look[peek(8)];
+  // jdhuff.c HUFF_DECODE: lookahead table lut (t.look, or its copy in LDS), then the
+  // canonical maxcode walk for longer codes
+  __host__ __device__ int decode(const HuffTab& t, const unsigned short* lut) {
+    const unsigned e = lut[peek(kLookBits)];
     if (e >> 8) {
       skip((int)(e >> 8));
       return (int)(e & 0xFF);
     }
-    int l = 9;
-    int code = (int)peek(9);
+    int l = kLookBits + 1;
+    int code = (int)peek(l);
     while (l <= 16 && code > t.maxcode[l]) {
       ++l;
       code = (int)peek(l);
     }
-    if (l > 16) {  // corrupt data: libjpeg warns and returns 0
-      skip(16);
+    if (l > 16) {  // corrupt data: libjpeg warns, returns 0 having read 17 bits
+      skip(17);
       return 0;
     }
     skip(l);
@@ -452,37 +462,132 @@ __host__ __device__ __forceinline__ int st_b(long long s) { return (int)((s >> 8
 __host__ __device__ __forceinline__ int st_k(long long s) { return (int)(s & 0xFF); }
 constexpr long long kStateNone = -1;
 
-__host__ __device__ __forceinline__ short* block_ptr(const JImage& im, const JSeg& sg, int g, short* coef) {
-  const int q = g / im.bpm, bb = g - q * im.bpm;
-  const int mcu = sg.mcu0 + q;
-  const JComp& cp = im.c[im.bcomp[bb]];
-  const int my = mcu / im.mcux, mx = mcu - my * im.mcux;
-  const int by = im.interleaved ? my * cp.v + (im.boff[bb] >> 4) : my;
-  const int bx = im.interleaved ? mx * cp.h + (im.boff[bb] & 15) : mx;
-  return coef + cp.coef_off + ((int64_t)by * cp.bw + bx) * 64;
-}
+// Per-image MCU description held in registers for the chunk loops (no global loads per
+// symbol): the MCU layout packed 6 bits per block (comp | row << 2 | column << 4) into one
+// 64-bit word read with a variable shift, and each component's tables and coefficient-plane
+// geometry as named scalars.  (Arrays indexed by a run-time block or component number
+// would be placed in scratch memory.)
+constexpr int kMaxTables = 1 << 13;
+struct McuInfo {
+  unsigned long long layout;
+  int bpm, mcux, interleaved;
+  int dc0, dc1, dc2, ac0, ac1, ac2;
+  int base0, base1, base2, bw0, bw1, bw2, h0, h1, h2, v0, v1, v2;
+  __host__ __device__ __forceinline__ void load(const JImage& im) {
+    bpm = im.bpm;
+    mcux = im.mcux;
+    interleaved = im.interleaved;
+    layout = 0;
+    for (int t = 0; t < im.bpm; ++t)
+      layout |= (unsigned long long)(im.bcomp[t] | (im.boff[t] >> 4) << 2 | (im.boff[t] & 15) << 4) << (6 * t);
+    dc0 = im.c[0].dc; ac0 = im.c[0].ac; base0 = (int)(im.c[0].coef_off / 64); bw0 = im.c[0].bw;
+    h0 = im.c[0].h; v0 = im.c[0].v;
+    dc1 = im.c[1].dc; ac1 = im.c[1].ac; base1 = (int)(im.c[1].coef_off / 64); bw1 = im.c[1].bw;
+    h1 = im.c[1].h; v1 = im.c[1].v;
+    dc2 = im.c[2].dc; ac2 = im.c[2].ac; base2 = (int)(im.c[2].coef_off / 64); bw2 = im.c[2].bw;
+    h2 = im.c[2].h; v2 = im.c[2].v;
+  }
+  __host__ __device__ __forceinline__ unsigned info(int b) const { return (unsigned)(layout >> (6 * b)) & 63u; }
+  __host__ __device__ static __forceinline__ int pick(int c, int a0, int a1, int a2) {
+    return c == 0 ? a0 : (c == 1 ? a1 : a2);
+  }
+  // coefficient block of MCU block info bi in MCU (my, mx)
+  __host__ __device__ __forceinline__ short* block(unsigned bi, int my, int mx, short* coef) const {
+    const int c = bi & 3, yy = (bi >> 2) & 3, xx = (bi >> 4) & 3;
+    const int by = interleaved ? my * pick(c, v0, v1, v2) + yy : my;
+    const int bx = interleaved ? mx * pick(c, h0, h1, h2) + xx : mx;
+    return coef + ((int64_t)pick(c, base0, base1, base2) + (int64_t)by * pick(c, bw0, bw1, bw2) + bx) * 64;
+  }
+};
+
+struct CurTabs {  // the tables of the current MCU block
+  const HuffTab* tdc;
+  const HuffTab* tac;
+  const unsigned short* ldc;
+  const unsigned short* lac;
+  int comp;
+  __host__ __device__ __forceinline__ void set(const McuInfo& M, unsigned bi, const HuffTab* pool,
+                                               const unsigned short* luts, int lstride) {
+    comp = bi & 3;
+    const int dc = McuInfo::pick(comp, M.dc0, M.dc1, M.dc2), ac = McuInfo::pick(comp, M.ac0, M.ac1, M.ac2);
+    tdc = pool + dc;
+    tac = pool + ac;
+    ldc = luts + (int64_t)dc * lstride;
+    lac = luts + (int64_t)ac * lstride;
+  }
+};
+
+// Checkpoint of a chunk's decode trajectory: the state at the first codeword boundary at or
+// past a fixed bit position, and the counts accumulated from the chunk start up to there.
+struct Checkpoint {
+  long long st;
+  int n, d0, d1, d2, pad;
+};
+constexpr int kCheckpoints = 7;  // at 1/8 .. 7/8 of every chunk
 
 // Synchronisation pass over one chunk: decode from state (b, k) at the stream's position to
-// the first codeword boundary at or past end_bit, without storing anything.  Returns the
+// the first codeword boundary at or past end_bit, without storing coefficients.  Returns the
 // exit state; cnt[0] = blocks started (DC symbols), cnt[1 + c] = sum of component c's DC
-// differences.
-__host__ __device__ long long chunk_sync(const JImage& im, const HuffTab* pool, BitStream& bs, int b, int k,
-                                         int end_bit, int cnt[4]) {
+// differences.  With checkpoints (cp_bits > 0) the trajectory is recorded at start + m *
+// cp_bits; when `merge` is set the recorded one is the chunk's previous trajectory, and the
+// first checkpoint where the new decode lands in the same state ends the pass early: from
+// there on both decodes are the same, so the exit is old_exit and the counts are the old
+// ones shifted by the difference of the prefixes (the later checkpoints are shifted too).
+__host__ __device__ __forceinline__ long long chunk_sync(const McuInfo& M, const HuffTab* pool, const unsigned short* luts,
+                                         int lstride, BitStream& bs, int b, int k, int end_bit, int cnt[4],
+                                         int start = 0, int cp_bits = 0, Checkpoint* cps = nullptr,
+                                         bool merge = false, long long old_exit = 0) {
   int nblk = 0, dc0 = 0, dc1 = 0, dc2 = 0;
+  int m = 1;
+  int next_cp = cp_bits > 0 ? start + cp_bits : 0x7FFFFFFF;
+  CurTabs T;
+  T.set(M, M.info(b), pool, luts, lstride);
   while (bs.pos < end_bit) {
+    while (bs.pos >= next_cp) {  // (one step can pass several checkpoints)
+      const long long st = st_pack(bs.pos, b, k);
+      Checkpoint& c = cps[m - 1];
+      if (merge && st == c.st) {
+#if defined(EF_DIAGNOSTICS) && !defined(__HIP_DEVICE_COMPILE__)
+        if (std::getenv("EF_JPEG_CHECK")) {
+          BitStream b2 = bs;
+          int c4[4];
+          const long long e2 = chunk_sync(M, pool, luts, lstride, b2, b, k, end_bit, c4);
+          if (e2 != old_exit)
+            std::fprintf(stderr, "bad merge at cp %d pos %d: continuation exit %lld, old exit %lld\n", m, bs.pos, e2,
+                         old_exit);
+        }
+#endif
+        const int dn = nblk - c.n, e0 = dc0 - c.d0, e1 = dc1 - c.d1, e2 = dc2 - c.d2;
+        for (int q = m - 1; q < kCheckpoints; ++q) {
+          cps[q].n += dn;
+          cps[q].d0 += e0;
+          cps[q].d1 += e1;
+          cps[q].d2 += e2;
+        }
+        cnt[0] += dn;
+        cnt[1] += e0;
+        cnt[2] += e1;
+        cnt[3] += e2;
+        return old_exit;
+      }
+      c.st = st;
+      c.n = nblk;
+      c.d0 = dc0;
+      c.d1 = dc1;
+      c.d2 = dc2;
+      next_cp = ++m <= kCheckpoints ? start + m * cp_bits : 0x7FFFFFFF;
+    }
     bs.refill();
-    const int c = im.bcomp[b];
-    const JComp& cp = im.c[c];
     if (k == 0) {
-      const int s = bs.decode(pool[cp.dc]);
+      const int s = bs.decode(*T.tdc, T.ldc);
       const int diff = s ? huff_extend(bs.get(s), s) : 0;
-      dc0 += c == 0 ? diff : 0;
-      dc1 += c == 1 ? diff : 0;
-      dc2 += c == 2 ? diff : 0;
+      dc0 += T.comp == 0 ? diff : 0;
+      dc1 += T.comp == 1 ? diff : 0;
+      dc2 += T.comp == 2 ? diff : 0;
       ++nblk;
       k = 1;
     } else {
-      const int rs = bs.decode(pool[cp.ac]);
+      const int rs = bs.decode(*T.tac, T.lac);
       const int s = rs & 15, r = rs >> 4;
       if (s) {
         bs.skip(s);
@@ -493,51 +598,104 @@ __host__ __device__ long long chunk_sync(const JImage& im, const HuffTab* pool, 
     }
     if (k >= 64) {
       k = 0;
-      b = b + 1 == im.bpm ? 0 : b + 1;
+      b = b + 1 == M.bpm ? 0 : b + 1;
+      T.set(M, M.info(b), pool, luts, lstride);
     }
+  }
+  const long long exit_st = st_pack(bs.pos, b, k);
+  for (; m <= kCheckpoints && next_cp != 0x7FFFFFFF; ++m) {  // checkpoints the last step jumped past
+    Checkpoint& c = cps[m - 1];
+    c.st = exit_st;
+    c.n = nblk;
+    c.d0 = dc0;
+    c.d1 = dc1;
+    c.d2 = dc2;
   }
   cnt[0] = nblk;
   cnt[1] = dc0;
   cnt[2] = dc1;
   cnt[3] = dc2;
-  return st_pack(bs.pos, b, k);
+  return exit_st;
 }
 
 // Output pass over one chunk from its exact start state: g = index (in the segment) of the
 // next block to start, pred = DC predictors there.  Stops at the first codeword boundary at
-// or past end_bit, or once every block of the segment has been decoded.
-__host__ __device__ void chunk_write(const JImage& im, const JSeg& sg, const HuffTab* pool, BitStream& bs, int b,
-                                     int k, int end_bit, int g, int pred[3], short* coef, const unsigned char* nat) {
-  const int total = sg.nmcu * im.bpm;
-  short* blk = k > 0 && g > 0 ? block_ptr(im, sg, g - 1, coef) : nullptr;
-  if (k > 0 && !blk) return;  // inconsistent state (cannot happen for an exact state)
+// or past end_bit, or once all `total` blocks of the segment are decoded.  A block decoded
+// whole inside the chunk is assembled in lblk (64 zeroed coefficients, 4-byte aligned: LDS
+// at a 33-word stride per thread so the threads of a wave hit distinct banks, or a host
+// array) and written as one 128-byte piece; the pieces of a block shared with a neighbour
+// chunk are scattered coefficient by coefficient into the zeroed buffer.
+__host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0, const HuffTab* pool, const unsigned short* luts,
+                                     int lstride, BitStream& bs, int b, int k, int end_bit, int g, int total,
+                                     int pred[3], short* coef, const unsigned char* nat, short* lblk) {
+  if (k > 0 && g == 0) return;  // inconsistent state (cannot happen for an exact state)
+  int mcu = mcu0 + (k > 0 ? g - 1 : g) / M.bpm;
+  int my = mcu / M.mcux, mx = mcu - my * M.mcux;
+  unsigned bi = M.info(b);
+  CurTabs T;
+  T.set(M, bi, pool, luts, lstride);
+  short* gblk = k > 0 ? M.block(bi, my, mx, coef) : nullptr;
+  bool scatter = k > 0;
   while (bs.pos < end_bit) {
     if (k == 0 && g >= total) break;
     bs.refill();
-    const int c = im.bcomp[b];
-    const JComp& cp = im.c[c];
     if (k == 0) {
-      blk = block_ptr(im, sg, g, coef);
+      gblk = M.block(bi, my, mx, coef);
+      scatter = false;
       ++g;
-      const int s = bs.decode(pool[cp.dc]);
-      pred[c] += s ? huff_extend(bs.get(s), s) : 0;
-      blk[0] = (short)pred[c];
+      const int s = bs.decode(*T.tdc, T.ldc);
+      const int diff = s ? huff_extend(bs.get(s), s) : 0;
+      int p;
+      if (T.comp == 0) p = pred[0] += diff;
+      else if (T.comp == 1) p = pred[1] += diff;
+      else p = pred[2] += diff;
+      lblk[0] = (short)p;
       k = 1;
     } else {
-      const int rs = bs.decode(pool[cp.ac]);
+      const int rs = bs.decode(*T.tac, T.lac);
       const int s = rs & 15, r = rs >> 4;
       if (s) {
         k += r;
-        blk[nat[k]] = (short)huff_extend(bs.get(s), s);
+        const short v = (short)huff_extend(bs.get(s), s);
+        if (scatter) gblk[nat[k]] = v;
+        else lblk[nat[k]] = v;
         ++k;
       } else {
         k = r == 15 ? k + 16 : 64;
       }
     }
     if (k >= 64) {
+      if (!scatter) {  // (memcpy: word access to the short buffer without aliasing hazards)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          uint4 v;
+          __builtin_memcpy(&v.x, lblk + 8 * t, 4);
+          __builtin_memcpy(&v.y, lblk + 8 * t + 2, 4);
+          __builtin_memcpy(&v.z, lblk + 8 * t + 4, 4);
+          __builtin_memcpy(&v.w, lblk + 8 * t + 6, 4);
+          reinterpret_cast<uint4*>(gblk)[t] = v;
+        }
+        __builtin_memset(lblk, 0, 128);
+      }
+      scatter = false;
       k = 0;
-      b = b + 1 == im.bpm ? 0 : b + 1;
+      if (++b == M.bpm) {
+        b = 0;
+        if (++mx == M.mcux) {
+          mx = 0;
+          ++my;
+        }
+      }
+      bi = M.info(b);
+      T.set(M, bi, pool, luts, lstride);
     }
+  }
+  if (k > 0 && !scatter) {  // the chunk ends inside a block it started: hand over its part
+    for (int t = 0; t < 64; ++t)
+      if (lblk[t]) {
+        gblk[t] = lblk[t];
+        lblk[t] = 0;
+      }
   }
 }
 
@@ -549,6 +707,8 @@ struct ChunkCtx {  // what the chunk kernels share
   const unsigned* words;
   int nchunks;
   int chunk_bits;
+  int warm_bits;  // round-0 warm-up before each chunk (<= chunk_bits)
+  Checkpoint* cps;  // kCheckpoints per chunk
 };
 
 __host__ __device__ __forceinline__ void chunk_stream(const ChunkCtx& X, const JSeg& sg, int pos, BitStream& bs) {
@@ -557,13 +717,14 @@ __host__ __device__ __forceinline__ void chunk_stream(const ChunkCtx& X, const J
 
 // One synchronisation round (Weissenberger & Schmidt's self-synchronising parallel Huffman
 // decoding, with the JPEG syntax position in the state).  Round 0: every chunk decodes from
-// a guess — its first bit, block 0, DC next — except a segment's first chunk, whose start
-// is exact.  Round t: chunk i adopts chunk i-1's exit state of round t-1 when it differs
+// a guess — block 0, DC next, warm_bits before its first bit — and takes the state at its
+// first codeword boundary as its start, except a segment's first chunk, whose start is
+// exact.  Round t: chunk i adopts chunk i-1's exit state of round t-1 when it differs
 // from the one it started from, re-decodes and raises *changed.  At the fixed point every
 // start state is exact by induction from the segment start.  Last chunks of a segment only
 // record their start state (nothing follows them).
-__host__ __device__ void sync_chunk(const ChunkCtx& X, int i, int round, long long* S, const long long* Ein,
-                                    long long* Eout, int* cnt, int* changed) {
+__host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const unsigned short* luts, int lstride, int i, int round,
+                                    long long* S, const long long* Ein, long long* Eout, int* cnt, int* changed) {
   const JSeg& sg = X.segs[X.chunk_seg[i]];
   const int j = i - sg.chunk0;
   const bool last = j == sg.nchunk - 1;
@@ -582,27 +743,74 @@ __host__ __device__ void sync_chunk(const ChunkCtx& X, int i, int round, long lo
       return;
     }
     S[i] = s;
-    if (!last) *changed = 1;
   }
   if (last) {
     Eout[i] = kStateNone;
     return;
   }
+  McuInfo M;
+  M.load(X.imgs[sg.img]);
   BitStream bs;
+  const int start = j * X.chunk_bits, end = (j + 1) * X.chunk_bits;
+  const int cp_bits = X.chunk_bits / (kCheckpoints + 1);
+  Checkpoint* cps = X.cps + (int64_t)i * kCheckpoints;
+  if (round == 0) {
+    if (j > 0) {
+      // warm-up: decode from a guess X.warm_bits before the chunk; the state at its first
+      // codeword boundary is often already exact
+      chunk_stream(X, sg, start - X.warm_bits, bs);
+      int dummy[4];
+      s = chunk_sync(M, X.pool, luts, lstride, bs, 0, 0, start, dummy);
+      S[i] = s;
+    } else {
+      chunk_stream(X, sg, st_pos(s), bs);
+    }
+    Eout[i] = chunk_sync(M, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits, cps);
+    return;
+  }
   chunk_stream(X, sg, st_pos(s), bs);
-  Eout[i] = chunk_sync(X.imgs[sg.img], X.pool, bs, st_b(s), st_k(s), (j + 1) * X.chunk_bits, cnt + 4 * i);
+  const long long e = chunk_sync(M, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits,
+                                 cps, true, Ein[i]);
+  Eout[i] = e;
+  if (e != Ein[i]) *changed = 1;  // only a changed exit can change the next chunk
 }
 
-__global__ __launch_bounds__(64) void jpeg_sync_kernel(ChunkCtx X, int round, long long* __restrict__ S,
-                                                      const long long* __restrict__ Ein, long long* __restrict__ Eout,
-                                                      int* __restrict__ cnt, int* __restrict__ changed) {
+constexpr int kChunkThreads = 256;
+constexpr int kGlobalLutStride = (int)(sizeof(HuffTab) / 2);
+
+// The batch's lookahead tables in LDS when there are at most kLdsTables of them (the usual
+// case: one encoder's 4 tables), else read from the global pool.
+__device__ __forceinline__ const unsigned short* stage_luts(const ChunkCtx& X, int lds_tables, unsigned short* slut,
+                                                            int* lstride) {
+  if (lds_tables == 0) {
+    *lstride = kGlobalLutStride;
+    return X.pool[0].look;
+  }
+  constexpr int kVec = kLookSize * 2 / 16;  // 16-byte pieces per table
+  for (int t = threadIdx.x; t < lds_tables * kVec; t += blockDim.x) {
+    const int tb = t / kVec, v = t - tb * kVec;
+    reinterpret_cast<uint4*>(slut + tb * kLookSize)[v] = reinterpret_cast<const uint4*>(X.pool[tb].look)[v];
+  }
+  __syncthreads();
+  *lstride = kLookSize;
+  return slut;
+}
+
+__global__ __launch_bounds__(kChunkThreads) void jpeg_sync_kernel(ChunkCtx X, int lds_tables, int round,
+                                                                  long long* __restrict__ S,
+                                                                  const long long* __restrict__ Ein,
+                                                                  long long* __restrict__ Eout, int* __restrict__ cnt,
+                                                                  int* __restrict__ changed) {
+  extern __shared__ unsigned short slut[];
+  int lstride;
+  const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < X.nchunks) sync_chunk(X, i, round, S, Ein, Eout, cnt, changed);
+  if (i < X.nchunks) sync_chunk(X, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
 }
 
 // Exclusive scan of the chunk counts inside each segment: first block index and DC
 // predictors at every chunk's start.
-__host__ __device__ void scan_segment(const ChunkCtx& X, const JSeg& sg, const int* cnt, int* G, int* P) {
+__host__ __device__ __forceinline__ void scan_segment(const ChunkCtx& X, const JSeg& sg, const int* cnt, int* G, int* P) {
   int g = 0, p0 = 0, p1 = 0, p2 = 0;
   for (int j = 0; j < sg.nchunk; ++j) {
     const int i = sg.chunk0 + j;
@@ -625,8 +833,9 @@ __global__ __launch_bounds__(64) void jpeg_scan_kernel(ChunkCtx X, int nseg, con
   if (si < nseg) scan_segment(X, X.segs[si], cnt, G, P);
 }
 
-__host__ __device__ void write_chunk(const ChunkCtx& X, int i, const long long* S, const int* G, const int* P,
-                                     short* coef, const unsigned char* nat) {
+__host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const unsigned short* luts, int lstride, int i,
+                                     const long long* S, const int* G, const int* P, short* coef,
+                                     const unsigned char* nat, short* lblk) {
   const JSeg& sg = X.segs[X.chunk_seg[i]];
   const int j = i - sg.chunk0;
   const long long s = S[i];
@@ -634,14 +843,27 @@ __host__ __device__ void write_chunk(const ChunkCtx& X, int i, const long long* 
   chunk_stream(X, sg, st_pos(s), bs);
   int pred[3] = {P[3 * i], P[3 * i + 1], P[3 * i + 2]};
   const int end = j == sg.nchunk - 1 ? 0x7FFFFFFF : (j + 1) * X.chunk_bits;
-  chunk_write(X.imgs[sg.img], sg, X.pool, bs, st_b(s), st_k(s), end, G[i], pred, coef, nat);
+  McuInfo M;
+  M.load(X.imgs[sg.img]);
+  chunk_write(M, sg.mcu0, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, G[i], sg.nmcu * M.bpm, pred, coef, nat,
+              lblk);
 }
 
-__global__ __launch_bounds__(64) void jpeg_write_kernel(ChunkCtx X, const long long* __restrict__ S,
-                                                       const int* __restrict__ G, const int* __restrict__ P,
-                                                       short* __restrict__ coef) {
+// LDS: [lookahead tables | natural order | one 64-coefficient block per thread]
+constexpr int kBlkWords = 33;  // per-thread block stride in LDS words (bank-conflict free)
+__global__ __launch_bounds__(kChunkThreads) void jpeg_write_kernel(ChunkCtx X, int lds_tables,
+                                                                   const long long* __restrict__ S,
+                                                                   const int* __restrict__ G, const int* __restrict__ P,
+                                                                   short* __restrict__ coef) {
+  extern __shared__ unsigned short slut[];
+  unsigned char* snat = reinterpret_cast<unsigned char*>(slut + lds_tables * kLookSize);
+  short* sblk = reinterpret_cast<short*>(snat + 128) + threadIdx.x * (2 * kBlkWords);
+  if (threadIdx.x < 80) snat[threadIdx.x] = kNatural[threadIdx.x];
+  __builtin_memset(sblk, 0, 128);
+  int lstride;
+  const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);  // ends with a barrier
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < X.nchunks) write_chunk(X, i, S, G, P, coef, kNatural);
+  if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat, sblk);
 }
 
 // jidctint.c jpeg_idct_islow arithmetic
@@ -861,7 +1083,7 @@ struct Batch {
   std::vector<int64_t> row_start;     // first output row of each image (rows of all images in order)
   std::vector<int> chunk_seg;         // segment of each chunk
   int64_t words = 0;                  // 32-bit words reserved for the destuffed segments
-  int chunk_bits = 0;
+  int chunk_bits = 0, warm_bits = 0;
   int64_t coef_blocks = 0, plane_bytes = 0, blocks = 0, rows = 0, dense_out = 0;
 };
 
@@ -875,6 +1097,7 @@ void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* siz
     int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], (int)B.imgs.size(), im, B.T, B.segs, true)
                           : EF_JPEG_E_CORRUPT;
     if (st == 0 && (int64_t)im.w * im.h > ((int64_t)1 << 31)) st = EF_JPEG_E_UNSUPPORTED;
+    if (st == 0 && B.T.huff.size() >= (size_t)kMaxTables) st = EF_JPEG_E_UNSUPPORTED;  // int32 table offsets
     if (status) status[i] = st;
     if (st != 0) {
       B.segs.resize(seg0);
@@ -958,6 +1181,7 @@ void make_chunks(Batch& B, int64_t opt_bits) {
   int64_t cb = opt_bits > 0 ? opt_bits : (total / 131072 + 255) / 256 * 256;
   cb = std::max<int64_t>(opt_bits > 0 ? 64 : 2048, std::min<int64_t>(cb, 16384));
   B.chunk_bits = (int)cb;
+  B.warm_bits = (int)std::min<int64_t>(cb, 1024);
   B.chunk_seg.clear();
   for (size_t k = 0; k < B.segs.size(); ++k) {
     JSeg& sg = B.segs[k];
@@ -1024,6 +1248,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   const size_t o_G = off; off += al((size_t)nchunks * 4);
   const size_t o_P = off; off += al((size_t)nchunks * 12);
   const size_t o_flag = off; off += al(16);
+  const size_t o_cps = off; off += al((size_t)nchunks * kCheckpoints * sizeof(Checkpoint));
   const size_t o_coef = off; off += al((size_t)B.coef_blocks * 64 * 2);
   const size_t o_planes = off; off += al((size_t)B.plane_bytes + 16);
   {
@@ -1043,6 +1268,8 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   X.words = reinterpret_cast<const unsigned*>(base + o_words);
   X.nchunks = nchunks;
   X.chunk_bits = B.chunk_bits;
+  X.warm_bits = B.warm_bits;
+  X.cps = reinterpret_cast<Checkpoint*>(base + o_cps);
   long long* S = reinterpret_cast<long long*>(base + o_S);
   long long* E[2] = {reinterpret_cast<long long*>(base + o_E0), reinterpret_cast<long long*>(base + o_E1)};
   int* cnt = reinterpret_cast<int*>(base + o_cnt);
@@ -1054,10 +1281,13 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   for (const JSeg& sg : B.segs) max_chunks = std::max(max_chunks, sg.nchunk);
   TimerEvt tev;
   timer_begin(c, EF_KERNEL_JPEG, &tev);
-  const unsigned cgrid = (unsigned)((nchunks + 63) / 64);
+  const unsigned cgrid = (unsigned)((nchunks + kChunkThreads - 1) / kChunkThreads);
+  const int lds_tables = B.T.huff.size() <= (size_t)kLdsTables ? (int)B.T.huff.size() : 0;
+  const size_t lds_bytes = (size_t)lds_tables * kLookSize * 2;
   int rounds = 0;
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(64), 0, s, X, 0, S, E[1], E[0], cnt, flag);
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, 0, S, E[1],
+                       E[0], cnt, flag);
     e = hipGetLastError();
   }
   // synchronisation rounds until no start state changes; at most one per chunk of the
@@ -1066,7 +1296,8 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   for (int r = 1; e == hipSuccess && r <= max_chunks; ++r) {
     e = hipMemsetAsync(flag, 0, 4, s);
     if (e != hipSuccess) break;
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(64), 0, s, X, r, S, E[cur], E[cur ^ 1], cnt, flag);
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S, E[cur],
+                       E[cur ^ 1], cnt, flag);
     e = hipGetLastError();
     cur ^= 1;
     rounds = r;
@@ -1078,7 +1309,8 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   if (e == hipSuccess) {
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
                        (int)B.segs.size(), cnt, G, P);
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(64), 0, s, X, S, G, P,
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128 + kChunkThreads * kBlkWords * 4, s,
+                       X, lds_tables, S, G, P,
                        reinterpret_cast<short*>(base + o_coef));
     const JImage* d_imgs = X.imgs;
     short* d_coef = reinterpret_cast<short*>(base + o_coef);
@@ -1222,25 +1454,56 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(words.data()));
   make_chunks(B, chunk_bits);
   const int nch = (int)B.chunk_seg.size();
-  ChunkCtx X{B.chunk_seg.data(), B.segs.data(), B.imgs.data(), B.T.huff.data(), words.data(), nch, B.chunk_bits};
+  std::vector<Checkpoint> cps((size_t)nch * kCheckpoints);
+  ChunkCtx X{B.chunk_seg.data(), B.segs.data(), B.imgs.data(), B.T.huff.data(), words.data(), nch, B.chunk_bits,
+             B.warm_bits, cps.data()};
   std::vector<long long> S(nch), E0(nch), E1(nch);
   std::vector<int> cnt((size_t)nch * 4), G(nch), P((size_t)nch * 3);
   int changed = 0;
-  for (int i = 0; i < nch; ++i) sync_chunk(X, i, 0, S.data(), E1.data(), E0.data(), cnt.data(), &changed);
+  const unsigned short* luts = B.T.huff.empty() ? nullptr : B.T.huff[0].look;
+  const int ls = kGlobalLutStride;
+  for (int i = 0; i < nch; ++i) sync_chunk(X, luts, ls, i, 0, S.data(), E1.data(), E0.data(), cnt.data(), &changed);
   long long* Ein = E0.data();
   long long* Eout = E1.data();
   int rounds = 0;
   for (int r = 1; r <= nch + 1; ++r) {
     changed = 0;
-    for (int i = 0; i < nch; ++i) sync_chunk(X, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
+    const std::vector<long long> S0 = S;
+    for (int i = 0; i < nch; ++i) sync_chunk(X, luts, ls, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
+    int nchg = 0;
+    for (int i = 0; i < nch; ++i) nchg += S[i] != S0[i];
+    std::fprintf(stderr, "round %d: %d of %d chunk starts changed\n", r, nchg, nch);
     std::swap(Ein, Eout);
     rounds = r;
     if (!changed) break;
   }
   if (rounds_out) *rounds_out = rounds;
+  if (std::getenv("EF_JPEG_CHECK")) {  // recompute every non-last chunk's counts and exit from its start
+    int bad = 0;
+    for (int i = 0; i < nch; ++i) {
+      const JSeg& sg = B.segs[B.chunk_seg[i]];
+      const int j = i - sg.chunk0;
+      if (j == sg.nchunk - 1) continue;
+      McuInfo M;
+      M.load(B.imgs[sg.img]);
+      BitStream bs;
+      chunk_stream(X, sg, st_pos(S[i]), bs);
+      int c4[4];
+      const long long e = chunk_sync(M, X.pool, luts, ls, bs, st_b(S[i]), st_k(S[i]), (j + 1) * X.chunk_bits, c4);
+      if (e != Ein[i] || c4[0] != cnt[4 * i] || c4[1] != cnt[4 * i + 1] || c4[2] != cnt[4 * i + 2] ||
+          c4[3] != cnt[4 * i + 3] || (j + 1 < sg.nchunk && S[i + 1] != e)) {
+        if (bad++ < 5)
+          std::fprintf(stderr, "chunk %d (seg %d j %d): exit %lld vs %lld, n %d vs %d, next S %lld\n", i,
+                       B.chunk_seg[i], j, e, Ein[i], c4[0], cnt[4 * i], S[i + 1]);
+      }
+    }
+    std::fprintf(stderr, "check: %d bad chunks\n", bad);
+  }
   for (const JSeg& sg : B.segs) scan_segment(X, sg, cnt.data(), G.data(), P.data());
   std::vector<short> coef((size_t)B.coef_blocks * 64 + 64, 0);
-  for (int i = 0; i < nch; ++i) write_chunk(X, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost);
+  alignas(16) short lblk[66] = {0};
+  for (int i = 0; i < nch; ++i)
+    write_chunk(X, luts, ls, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost, lblk);
   std::vector<uint8_t> planes((size_t)B.plane_bytes + 16);
   for (size_t r = 0; r < B.block_start.size(); ++r) {
     const JImage& im = B.imgs[B.ic[r] >> 2];
