@@ -620,28 +620,27 @@ __host__ __device__ __forceinline__ long long chunk_sync(const McuInfo& M, const
 
 // Output pass over one chunk from its exact start state: g = index (in the segment) of the
 // next block to start, pred = DC predictors there.  Stops at the first codeword boundary at
-// or past end_bit, or once all `total` blocks of the segment are decoded.  A block decoded
-// whole inside the chunk is assembled in lblk (64 zeroed coefficients, 4-byte aligned: LDS
-// at a 33-word stride per thread so the threads of a wave hit distinct banks, or a host
-// array) and written as one 128-byte piece; the pieces of a block shared with a neighbour
-// chunk are scattered coefficient by coefficient into the zeroed buffer.
-__host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0, const HuffTab* pool, const unsigned short* luts,
-                                     int lstride, BitStream& bs, int b, int k, int end_bit, int g, int total,
-                                     int pred[3], short* coef, const unsigned char* nat, short* lblk) {
+// or past end_bit, or once all `total` blocks of the segment are decoded.  Coefficients are
+// stored straight into the zeroed coefficient buffer (a block shared with a neighbouring
+// chunk gets disjoint coefficients from each).  Measured against assembling each block in
+// LDS and writing it as one 128-byte piece, the direct stores were faster: the per-block
+// flush runs divergently in nearly every step of a 64-chunk wave.
+__host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0, const HuffTab* pool,
+                                                     const unsigned short* luts, int lstride, BitStream& bs, int b,
+                                                     int k, int end_bit, int g, int total, int pred[3], short* coef,
+                                                     const unsigned char* nat) {
   if (k > 0 && g == 0) return;  // inconsistent state (cannot happen for an exact state)
   int mcu = mcu0 + (k > 0 ? g - 1 : g) / M.bpm;
   int my = mcu / M.mcux, mx = mcu - my * M.mcux;
   unsigned bi = M.info(b);
   CurTabs T;
   T.set(M, bi, pool, luts, lstride);
-  short* gblk = k > 0 ? M.block(bi, my, mx, coef) : nullptr;
-  bool scatter = k > 0;
+  short* blk = k > 0 ? M.block(bi, my, mx, coef) : nullptr;
   while (bs.pos < end_bit) {
     if (k == 0 && g >= total) break;
     bs.refill();
     if (k == 0) {
-      gblk = M.block(bi, my, mx, coef);
-      scatter = false;
+      blk = M.block(bi, my, mx, coef);
       ++g;
       const int s = bs.decode(*T.tdc, T.ldc);
       const int diff = s ? huff_extend(bs.get(s), s) : 0;
@@ -649,35 +648,20 @@ __host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0,
       if (T.comp == 0) p = pred[0] += diff;
       else if (T.comp == 1) p = pred[1] += diff;
       else p = pred[2] += diff;
-      lblk[0] = (short)p;
+      blk[0] = (short)p;
       k = 1;
     } else {
       const int rs = bs.decode(*T.tac, T.lac);
       const int s = rs & 15, r = rs >> 4;
       if (s) {
         k += r;
-        const short v = (short)huff_extend(bs.get(s), s);
-        if (scatter) gblk[nat[k]] = v;
-        else lblk[nat[k]] = v;
+        blk[nat[k]] = (short)huff_extend(bs.get(s), s);
         ++k;
       } else {
         k = r == 15 ? k + 16 : 64;
       }
     }
     if (k >= 64) {
-      if (!scatter) {  // (memcpy: word access to the short buffer without aliasing hazards)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          uint4 v;
-          __builtin_memcpy(&v.x, lblk + 8 * t, 4);
-          __builtin_memcpy(&v.y, lblk + 8 * t + 2, 4);
-          __builtin_memcpy(&v.z, lblk + 8 * t + 4, 4);
-          __builtin_memcpy(&v.w, lblk + 8 * t + 6, 4);
-          reinterpret_cast<uint4*>(gblk)[t] = v;
-        }
-        __builtin_memset(lblk, 0, 128);
-      }
-      scatter = false;
       k = 0;
       if (++b == M.bpm) {
         b = 0;
@@ -689,13 +673,6 @@ __host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0,
       bi = M.info(b);
       T.set(M, bi, pool, luts, lstride);
     }
-  }
-  if (k > 0 && !scatter) {  // the chunk ends inside a block it started: hand over its part
-    for (int t = 0; t < 64; ++t)
-      if (lblk[t]) {
-        gblk[t] = lblk[t];
-        lblk[t] = 0;
-      }
   }
 }
 
@@ -834,8 +811,8 @@ __global__ __launch_bounds__(64) void jpeg_scan_kernel(ChunkCtx X, int nseg, con
 }
 
 __host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const unsigned short* luts, int lstride, int i,
-                                     const long long* S, const int* G, const int* P, short* coef,
-                                     const unsigned char* nat, short* lblk) {
+                                                     const long long* S, const int* G, const int* P, short* coef,
+                                                     const unsigned char* nat) {
   const JSeg& sg = X.segs[X.chunk_seg[i]];
   const int j = i - sg.chunk0;
   const long long s = S[i];
@@ -845,25 +822,21 @@ __host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const un
   const int end = j == sg.nchunk - 1 ? 0x7FFFFFFF : (j + 1) * X.chunk_bits;
   McuInfo M;
   M.load(X.imgs[sg.img]);
-  chunk_write(M, sg.mcu0, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, G[i], sg.nmcu * M.bpm, pred, coef, nat,
-              lblk);
+  chunk_write(M, sg.mcu0, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, G[i], sg.nmcu * M.bpm, pred, coef, nat);
 }
 
-// LDS: [lookahead tables | natural order | one 64-coefficient block per thread]
-constexpr int kBlkWords = 33;  // per-thread block stride in LDS words (bank-conflict free)
+// LDS: [lookahead tables | natural order]
 __global__ __launch_bounds__(kChunkThreads) void jpeg_write_kernel(ChunkCtx X, int lds_tables,
                                                                    const long long* __restrict__ S,
                                                                    const int* __restrict__ G, const int* __restrict__ P,
                                                                    short* __restrict__ coef) {
   extern __shared__ unsigned short slut[];
   unsigned char* snat = reinterpret_cast<unsigned char*>(slut + lds_tables * kLookSize);
-  short* sblk = reinterpret_cast<short*>(snat + 128) + threadIdx.x * (2 * kBlkWords);
   if (threadIdx.x < 80) snat[threadIdx.x] = kNatural[threadIdx.x];
-  __builtin_memset(sblk, 0, 128);
   int lstride;
   const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);  // ends with a barrier
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat, sblk);
+  if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat);
 }
 
 // jidctint.c jpeg_idct_islow arithmetic
@@ -972,13 +945,14 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const short* __restrict_
                                                        int64_t total_blocks, uint8_t* __restrict__ planes) {
   __shared__ int ws[kIdctBlocks][65];
   const int lb = threadIdx.x >> 3, j = threadIdx.x & 7;
-  const int64_t gb = (int64_t)blockIdx.x * kIdctBlocks + lb;
+  const int64_t gb0 = (int64_t)blockIdx.x * kIdctBlocks, gb = gb0 + lb;
   if (gb >= total_blocks) return;  // whole 8-lane groups leave together
-  int lo = 0, hi = nruns - 1;  // the (image, component) run holding this block
-  while (lo < hi) {
+  int lo = 0, hi = nruns - 1;  // the (image, component) run holding the workgroup's first block
+  while (lo < hi) {  // (uniform: scalar loads)
     const int mid = (lo + hi + 1) >> 1;
-    if (block_start[mid] <= gb) lo = mid; else hi = mid - 1;
+    if (block_start[mid] <= gb0) lo = mid; else hi = mid - 1;
   }
+  while (lo + 1 < nruns && block_start[lo + 1] <= gb) ++lo;  // then this group's run
   const int img = ic_img[lo] >> 2, comp = ic_img[lo] & 3;
   const JImage& im = imgs[img];
   const JComp& cp = im.c[comp];
@@ -1054,20 +1028,103 @@ __host__ __device__ void out_pixel(const JImage& im, int y, int x, const uint8_t
 
 // One wave per output row (the image found once per wave from the row starts), lanes
 // stride across the row.
+__host__ __device__ __forceinline__ unsigned load4(const uint8_t* p) {  // 4-byte aligned
+  return *reinterpret_cast<const unsigned*>(p);
+}
+
+// Fancy-upsampled chroma of output columns x0..x0+3 (x0 % 4 == 0) of row y for a component
+// subsampled 2x horizontally (v2: and vertically) with downsampled_width > 2: the same
+// jdsample.c arithmetic as upsample(), sharing the column sums of chroma columns
+// j0-1 .. j0+2 between the four pixels.
+__host__ __device__ __forceinline__ void upsample_h2_quad(const uint8_t* pl, const JComp& cp, bool v2, int y, int x0,
+                                                          int o[4]) {
+  const int64_t pitch = (int64_t)cp.bw * 8;
+  const int j0 = x0 >> 1, last = cp.dw - 1, wmax = cp.bw * 8 - 1;
+  const uint8_t* r0 = pl + (int64_t)(v2 ? y >> 1 : y) * pitch;
+  const uint8_t* r1 = r0;
+  if (v2) {
+    int i1 = (y & 1) ? (y >> 1) + 1 : (y >> 1) - 1;
+    i1 = i1 < 0 ? 0 : (i1 > cp.dh - 1 ? cp.dh - 1 : i1);
+    r1 = pl + (int64_t)i1 * pitch;
+  }
+  int cs[4];  // column sums of chroma columns j0-1 .. j0+2 (clamped into the padded row)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    int c = j0 - 1 + t;
+    c = c < 0 ? 0 : (c > wmax ? wmax : c);
+    cs[t] = v2 ? r0[c] * 3 + r1[c] : r0[c];
+  }
+  // h2v2: 3 * nearer + further, rounding 8 / 7 >> 4;  h2v1: 3 * nearer + further, 1 / 2 >> 2
+  const int sh = v2 ? 4 : 2, b0 = v2 ? 8 : 1, b1 = v2 ? 7 : 2;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {  // chroma column j = j0 + p -> output columns 2j, 2j+1
+    const int j = j0 + p;
+    const int c = cs[p + 1];
+    o[2 * p] = j == 0 ? (v2 ? (c * 4 + 8) >> 4 : c) : (c * 3 + cs[p] + b0) >> sh;
+    o[2 * p + 1] = j == last ? (v2 ? (c * 4 + 7) >> 4 : c) : (c * 3 + cs[p + 2] + b1) >> sh;
+  }
+}
+
+// Output columns x0..x0+3 of row y (those < w): one Y word, shared chroma column sums; the
+// general per-pixel path covers grey sources, box upsampling and the rest.
+__host__ __device__ __forceinline__ void out_quad(const JImage& im, int y, int x0, const uint8_t* planes,
+                                                  uint8_t* out) {
+  const int n = im.w - x0 < 4 ? im.w - x0 : 4;
+  const uint8_t* prow = planes + im.c[0].plane_off + (int64_t)y * im.c[0].bw * 8;
+  if (im.mode == EF_JPEG_GRAY) {
+    for (int t = 0; t < n; ++t) out[im.out_off + (int64_t)y * im.w + x0 + t] = prow[x0 + t];
+    return;
+  }
+  const JComp& cb = im.c[1];
+  const JComp& cr = im.c[2];
+  const bool h2 = im.nc == 3 && im.hmax == 2 * cb.h && cb.h == cr.h && cb.v == cr.v && cb.dw > 2;
+  const bool full = im.nc == 3 && im.hmax == cb.h && im.vmax == cb.v && cb.h == cr.h && cb.v == cr.v;
+  if (!h2 && !full) {
+    for (int t = 0; t < n; ++t) out_pixel(im, y, x0 + t, planes, out);
+    return;
+  }
+  const unsigned yw = load4(prow + x0);
+  int ub[4], vr[4];
+  if (h2) {
+    const bool v2 = im.vmax == 2 * cb.v;
+    upsample_h2_quad(planes + cb.plane_off, cb, v2, y, x0, ub);
+    upsample_h2_quad(planes + cr.plane_off, cr, v2, y, x0, vr);
+  } else {
+    const unsigned bw = load4(planes + cb.plane_off + (int64_t)y * cb.bw * 8 + x0);
+    const unsigned rw = load4(planes + cr.plane_off + (int64_t)y * cr.bw * 8 + x0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ub[t] = (bw >> (8 * t)) & 255;
+      vr[t] = (rw >> (8 * t)) & 255;
+    }
+  }
+  uint8_t* o = out + im.out_off + 3 * ((int64_t)y * im.w + x0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t < n) {
+      const int Y = (yw >> (8 * t)) & 255;
+      o[3 * t] = clamp255(Y + cb_b(ub[t]));
+      o[3 * t + 1] = clamp255(Y + cbcr_g(ub[t], vr[t]));
+      o[3 * t + 2] = clamp255(Y + cr_r(vr[t]));
+    }
+  }
+}
+
+// One wave per output row (the image found once per wave from the row starts), each lane
+// four adjacent pixels.
 __global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict__ imgs, const int64_t* __restrict__ row_start,
                                                       int nimg, int64_t total_rows, const uint8_t* __restrict__ planes,
                                                       uint8_t* __restrict__ out) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
   if (r >= total_rows) return;
   int lo = 0, hi = nimg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (row_start[mid] <= r) lo = mid; else hi = mid - 1;
   }
-  lo = __builtin_amdgcn_readfirstlane(lo);
   const JImage& im = imgs[lo];
   const int y = (int)(r - row_start[lo]);
-  for (int x = threadIdx.x & 63; x < im.w; x += 64) out_pixel(im, y, x, planes, out);
+  for (int x0 = 4 * (threadIdx.x & 63); x0 < im.w; x0 += 256) out_quad(im, y, x0, planes, out);
 }
 
 // ------------------------------------------------------------------ batch layout
@@ -1309,9 +1366,8 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   if (e == hipSuccess) {
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
                        (int)B.segs.size(), cnt, G, P);
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128 + kChunkThreads * kBlkWords * 4, s,
-                       X, lds_tables, S, G, P,
-                       reinterpret_cast<short*>(base + o_coef));
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S, G,
+                       P, reinterpret_cast<short*>(base + o_coef));
     const JImage* d_imgs = X.imgs;
     short* d_coef = reinterpret_cast<short*>(base + o_coef);
     uint8_t* d_planes = reinterpret_cast<uint8_t*>(base + o_planes);
@@ -1501,9 +1557,7 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   }
   for (const JSeg& sg : B.segs) scan_segment(X, sg, cnt.data(), G.data(), P.data());
   std::vector<short> coef((size_t)B.coef_blocks * 64 + 64, 0);
-  alignas(16) short lblk[66] = {0};
-  for (int i = 0; i < nch; ++i)
-    write_chunk(X, luts, ls, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost, lblk);
+  for (int i = 0; i < nch; ++i) write_chunk(X, luts, ls, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost);
   std::vector<uint8_t> planes((size_t)B.plane_bytes + 16);
   for (size_t r = 0; r < B.block_start.size(); ++r) {
     const JImage& im = B.imgs[B.ic[r] >> 2];
@@ -1521,7 +1575,7 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   }
   for (const JImage& im : B.imgs)
     for (int y = 0; y < im.h; ++y)
-      for (int x = 0; x < im.w; ++x) out_pixel(im, y, x, planes.data(), out);
+      for (int x0 = 0; x0 < im.w; x0 += 4) out_quad(im, y, x0, planes.data(), out);
   return EF_OK;
 }
 // host preparation only (parse, destuff, chunking): wall time of each stage in ms

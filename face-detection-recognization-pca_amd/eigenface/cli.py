@@ -55,17 +55,18 @@ def train_manual(faces_dir, person, model_dir="models", version=None, n_componen
     from .compat import read_face, save_pca_model, visualize_eigenfaces
     from .pca import manual_pca
 
+    from .compat import read_gray_images
+
     files = sorted(f for f in os.listdir(faces_dir) if f.lower().endswith((".jpg", ".jpeg", ".png")))
     rows, names = [], []
-    for f in files:
-        from PIL import Image
-        try:
-            im = Image.open(os.path.join(faces_dir, f))
-            im.draft("L", im.size)  # libjpeg grey output == cv2.IMREAD_GRAYSCALE (pinned by EVR)
-            rows.append(np.asarray(im.convert("L"), dtype=np.uint8).ravel())
-            names.append(f)
-        except OSError:
+    # cv2.imread(IMREAD_GRAYSCALE) per file (useless/train.py:33): JPEGs decoded on the GPU
+    # in one batch (libjpeg's grey output, pinned by the reference models' EVR)
+    for f, im in zip(files, read_gray_images([os.path.join(faces_dir, f) for f in files])):
+        if im is None:
             print(f"Warning: Could not load image {f}")
+            continue
+        rows.append(np.ascontiguousarray(im, dtype=np.uint8).ravel())
+        names.append(f)
     if not rows:
         print("Error: No valid face images could be loaded")
         return 1

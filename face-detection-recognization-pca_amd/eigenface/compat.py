@@ -11,10 +11,13 @@ Appendix A, §8a rows a1/a10/a11), backed by the GPU engine.
                                is installed (scan-template-v4.py:36-37, :265-266)
 * ``extract_face_features``, ``recognize_face_all_models`` — scan-template-v4.py:253-319
 
-Image ingest (a1): files are decoded on the host (OpenCV's ``imread`` when importable,
-else Pillow — both libjpeg), then ``cvtColor(BGR2GRAY)`` + ``resize(64, 64)`` run for the
-whole batch in one GPU launch with OpenCV's CV_8U fixed-point rules (``ef_preprocess``;
-*parity unpinned* against OpenCV itself, which is absent where this was built).
+Image ingest (a1, §8f rank 2): JPEG files are decoded on the GPU in one batch with
+libjpeg-turbo's arithmetic (``ef_jpeg_ingest`` / ``ef_jpeg_decode``, bit-exact against
+Pillow's libjpeg-turbo — the library cv2.imread wraps), then ``cvtColor(BGR2GRAY)`` +
+``resize(64, 64)`` run in the same call with OpenCV's CV_8U fixed-point rules (*parity
+unpinned* against OpenCV itself, which is absent where this was built).  Files
+the GPU decoder does not take (PNG, progressive/CMYK JPEG) are decoded on the host by
+OpenCV or Pillow and join the GPU grey+resize launch.
 """
 from __future__ import annotations
 
@@ -49,20 +52,67 @@ def decode_image(path):
         return None
 
 
+def _read_bytes(path):
+    try:
+        with open(path, "rb") as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def _is_jpeg(blob):
+    return blob is not None and len(blob) > 3 and blob[0] == 0xFF and blob[1] == 0xD8
+
+
 def read_faces(paths, size=(64, 64), device=0):
-    """train-v4.py:59-68 for a list of files: decode on the host, then ONE GPU launch for
-    cvtColor(BGR2GRAY) + resize(size) of the whole batch (ef_preprocess).  Returns
-    (rows uint8 (m, h*w), kept indices) — unreadable files are skipped like the
-    reference's ``img is None`` branch."""
-    imgs, keep = [], []
+    """train-v4.py:59-68 for a list of files: JPEG files are decoded, converted to grey
+    and resized on the GPU in one batch (ef_jpeg_ingest; libjpeg-turbo's IMREAD_COLOR
+    pixels, then cvtColor(BGR2GRAY) + resize(size)); files the GPU decoder does not take
+    (PNG, progressive or CMYK JPEG) are decoded on the host by the reference's own decoder
+    and join one GPU grey+resize launch (ef_preprocess).  Returns (rows uint8 (m, h*w),
+    kept indices) — unreadable files are skipped like the reference's ``img is None``
+    branch."""
+    eng = get_engine(device)
+    blobs = [_read_bytes(p) for p in paths]
+    jpg = [i for i, b in enumerate(blobs) if _is_jpeg(b)]
+    rows = {}
+    if jpg:
+        r, st = eng.ingest_jpegs([blobs[i] for i in jpg], size, "bgr")
+        for k, i in enumerate(jpg):
+            if st[k] == 0:
+                rows[i] = r[k]
+    rest, imgs = [], []
     for i, p in enumerate(paths):
+        if i in rows or blobs[i] is None:
+            continue
         im = decode_image(p)
         if im is not None:
+            rest.append(i)
             imgs.append(im)
-            keep.append(i)
-    if not imgs:
+    if imgs:
+        for i, r in zip(rest, eng.preprocess(imgs, size)):
+            rows[i] = r
+    keep = sorted(rows)
+    if not keep:
         return np.zeros((0, size[0] * size[1]), np.uint8), keep
-    return get_engine(device).preprocess(imgs, size), keep
+    return np.stack([rows[i] for i in keep]), keep
+
+
+def read_gray_images(paths, device=0):
+    """cv2.imread(path, IMREAD_GRAYSCALE) for a list of files (useless/train.py:33,
+    scan-template-v4.py:52): JPEGs decoded on the GPU in one batch (libjpeg's grey output),
+    other files by decode_gray on the host.  Returns a list of uint8 arrays (None for an
+    unreadable file)."""
+    blobs = [_read_bytes(p) for p in paths]
+    jpg = [i for i, b in enumerate(blobs) if _is_jpeg(b)]
+    out = [None] * len(paths)
+    if jpg:
+        for i, im in zip(jpg, get_engine(device).decode_jpegs([blobs[i] for i in jpg], "gray")):
+            out[i] = im
+    for i, p in enumerate(paths):
+        if out[i] is None and blobs[i] is not None:
+            out[i] = decode_gray(p)
+    return out
 
 
 def read_face(path, size=(64, 64), device=0):
@@ -452,12 +502,10 @@ def load_all_models(root="."):
                     det = json.load(f)
             templates = []
             if det and det.get("faces"):
-                for face in det["faces"][:5]:
-                    path = face["image_path"]
-                    if os.path.exists(path):
-                        img = decode_gray(path)
-                        if img is not None:
-                            templates.append({"image": img, "width": face["width"], "height": face["height"]})
+                first = [f for f in det["faces"][:5] if os.path.exists(f["image_path"])]
+                for face, img in zip(first, read_gray_images([f["image_path"] for f in first])):
+                    if img is not None:
+                        templates.append({"image": img, "width": face["width"], "height": face["height"]})
             models[person_name] = {"model_data": md, "detection_data": det, "template_images": templates,
                                    "model_path": model_path}
             print(f"  - {person_name}: {len(md['face_features']) if md else 0} faces")

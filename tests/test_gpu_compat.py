@@ -105,6 +105,36 @@ def test_read_faces_gpu_ingest_matches_oracle(tmp_path):
     assert read_face(paths[2]) is None
 
 
+def test_read_faces_and_grey_decode_jpeg_on_gpu(tmp_path):
+    """JPEG files go through the GPU decoder (ef_jpeg_ingest / ef_jpeg_decode): the rows
+    equal libjpeg-turbo's pixels (Pillow) through the resize oracle; a progressive JPEG and
+    a PNG take the host decoder inside the same call."""
+    import jpeg_cases as J
+    from eigenface.compat import read_faces, read_gray_images
+    from oracle import image_oracle as io
+    paths, blobs = [], []
+    for i, (h, w, sub) in enumerate([(120, 96, 2), (61, 77, 0), (200, 150, 1)]):
+        b = J.encode(J.smooth_image(h, w, 3, i), quality=95, subsampling=sub)
+        blobs.append(b)
+    blobs.append(J.encode(J.smooth_image(90, 90, 3, 7), quality=80, progressive=True))
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"face_{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+    from PIL import Image
+    png = J.smooth_image(50, 70, 3, 9)
+    Image.fromarray(png).save(tmp_path / "face_png.png")
+    paths.append(str(tmp_path / "face_png.png"))
+    rows, keep = read_faces(paths)
+    assert keep == [0, 1, 2, 3, 4]
+    for i in range(4):
+        np.testing.assert_array_equal(rows[i], io.preprocess(J.decode_ref(blobs[i], "bgr"), (64, 64)))
+    np.testing.assert_array_equal(rows[4], io.preprocess(png[..., ::-1], (64, 64)))
+    grey = read_gray_images(paths[:4])
+    for i in range(4):
+        np.testing.assert_array_equal(grey[i], J.decode_ref(blobs[i], "gray"))
+
+
 def test_engine_owner_tokens_interleaved_models():
     """Two EigenfacePCA instances and the drop-in functions share one engine per device:
     each must re-upload its model / gallery when another caller replaced it (owner
