@@ -19,6 +19,8 @@ KERNEL = "search_kernel<128, 0, false, 0>"
 CONFIGS = {
     "c3": ("search_kernel<128, 0, false, 0>", 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4),
     "c5": ("search_wide_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
+    # C5 bf16 projection: uint8 probe pixels + bf16 W + fp32 partial features
+    "c5proj": ("project_bf16_wide_kernel", 4096 * 65536 + 512 * 65536 * 2 + 4096 * 512 * 4),
 }
 SIMDS = 1024  # 256 CUs x 4
 XCDS = 8
@@ -66,6 +68,9 @@ def main():
         "clock_ghz": grbm_xcd / ns,
         "sq_wait_any_frac": s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"],
     }
+    if "SQ_LDS_BANK_CONFLICT" in s:
+        rec["lds_bank_conflict_cycles"] = s["SQ_LDS_BANK_CONFLICT"]
+        rec["lds_insts"] = s.get("SQ_INSTS_LDS")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
