@@ -217,6 +217,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   const int max_iters = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_fit_max_iters, 1 << 20));
   bool converged = false;
   double last_worst = 1.0;
+  int next_rr = 8;  // iteration of the next scheduled Rayleigh-Ritz step
   for (it = 1; it <= max_iters; ++it) {
     const bool fine = !coarse;  // this iteration's product is fp64
     if (coarse) {
@@ -234,7 +235,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
     // no iteration count), 8, then every rr_period(dim)
     const bool early = dim < 12288 && (it <= 2 || it == 4);
-    const bool rr = early || it == 8 || it % rr_period(dim) == 0 || it == max_iters;
+    const bool rr = early || it == next_rr || it == max_iters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
                            work, kWorkElems),
@@ -262,6 +263,21 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       (void)wi;
 #endif
       if (coarse && worst < 1e-4) coarse = false;  // fp64 products from the next iteration on
+      // Schedule the next Rayleigh-Ritz step.  The test above passes once the PREVIOUS
+      // step's Ritz values were already within 1e-13, so with the change per period
+      // shrinking geometrically (worst now vs worst at the previous step) the current error
+      // is predicted as worst * rate: when that is below the tolerance the next step comes
+      // one iteration later (the test then passes instead of waiting out the period); a
+      // wrong prediction only costs that one extra Rayleigh-Ritz step.
+      {
+        const int period = rr_period(dim);
+        next_rr = (it / period + 1) * period;
+        if (it < 8) next_rr = 8;
+        if (fine && prev_fine && have_prev && last_worst > 0.0 && worst < last_worst) {
+          const double e_now = worst * (worst / last_worst);
+          if (e_now <= 3e-14) next_rr = it + 1;
+        }
+      }
       prev = th;
       have_prev = true;
       prev_fine = fine;

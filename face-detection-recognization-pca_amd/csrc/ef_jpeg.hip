@@ -1127,6 +1127,25 @@ __global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict_
   for (int x0 = 4 * (threadIdx.x & 63); x0 < im.w; x0 += 256) out_quad(im, y, x0, planes, out);
 }
 
+// Diagnostic build: wall time of the host stages of a decode (EF_JPEG_TIMES=1 prints them).
+#ifdef EF_DIAGNOSTICS
+struct StageTimer {
+  const bool on = std::getenv("EF_JPEG_TIMES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what, hipStream_t s = nullptr, bool sync = false) {
+    if (!on) return;
+    if (sync) (void)hipStreamSynchronize(s);
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[jpeg] %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+#else
+struct StageTimer {
+  void mark(const char*, hipStream_t = nullptr, bool = false) {}
+};
+#endif
+
 // ------------------------------------------------------------------ batch layout
 // Everything one decode launch needs, built on the host: per-image geometry, Huffman and
 // quantisation tables, entropy segments and their chunks, IDCT runs, output pixel starts.
@@ -1252,6 +1271,7 @@ void make_chunks(Batch& B, int64_t opt_bits) {
 // image at its out_off.  Stream-ordered on ctx's stream.
 int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* dout) {
   hipStream_t s = c->stream;
+  StageTimer tm;
   // layout: one pinned upload [destuffed words | images | Huffman tables | quant tables |
   // segments | chunk->segment | IDCT runs | pixel starts] at the front of the device
   // workspace, then device-only [chunk states S, E x2 | counts | block starts | DC preds |
@@ -1285,7 +1305,9 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
     c->jpeg_pinned_bytes = pin_need + pin_need / 4 + 4096;
   }
   char* h = static_cast<char*>(c->jpeg_pinned);
+  tm.mark("pinned");
   destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + o_words));
+  tm.mark("destuff");
   make_chunks(B, c->opt_jpeg_chunk_bits);
   const int nchunks = (int)B.chunk_seg.size();
   std::memcpy(h + o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
@@ -1313,7 +1335,9 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
     if (rc != EF_OK) return rc;
   }
   char* base = static_cast<char*>(c->jpeg_ws.p);
+  tm.mark("tables");
   hipError_t e = hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, s);
+  tm.mark("upload", s, true);
   if (e == hipSuccess)  // pageable; complete before the first round's flag read below
     e = hipMemcpyAsync(base + o_cseg, B.chunk_seg.data(), (size_t)nchunks * 4, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemsetAsync(base + o_coef, 0, (size_t)B.coef_blocks * 64 * 2, s);
@@ -1363,6 +1387,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
     if (e != hipSuccess || *hflag == 0) break;
   }
   c->jpeg_rounds = rounds;
+  tm.mark("sync-rounds");
   if (e == hipSuccess) {
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
                        (int)B.segs.size(), cnt, G, P);
@@ -1382,6 +1407,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
     e = hipGetLastError();
   }
   timer_end(c, &tev);
+  tm.mark("kernels", s, true);
   if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   return EF_OK;
 }
@@ -1454,7 +1480,9 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     const int32_t m = std::min<int32_t>(65535, count - a);
     std::vector<int32_t> st(m), hh(m, 1), ww(m, 1), cc(m, 1);
     Batch B;
+    StageTimer tm;
     build_batch(data, offsets + a, sizes + a, m, mode, nullptr, st.data(), B);
+    tm.mark("parse");
     int rc = ensure(c, c->jpeg_out, (size_t)B.dense_out + 256);
     if (rc != EF_OK) return rc;
     uint8_t* pix = static_cast<uint8_t*>(c->jpeg_out.p);
@@ -1481,8 +1509,10 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       if (rc != EF_OK) return rc;
       rows = static_cast<uint8_t*>(c->jpeg_rows.p);
     }
+    tm.mark("decode");
     rc = ef_preprocess(c, pix, doff.data(), hh.data(), ww.data(), cc.data(), m, out_h, out_w, rows, EF_MEM_DEVICE);
     if (rc != EF_OK) return rc;
+    tm.mark("preprocess");
     if (!(flags & EF_MEM_DEVICE)) {
       hipError_t e = hipMemcpyAsync(out + (int64_t)a * row, rows, (size_t)m * row, hipMemcpyDeviceToHost, c->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

@@ -7,6 +7,7 @@ not mix the two.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -65,17 +66,33 @@ class FitResult:
     iters: int
 
 
+_TORCH_READY = False
+
+
+def _init_torch_first():
+    """torch's HIP runtime must come up before this process's first libeigenface context,
+    or torch reports no GPU afterwards (seen on the MI355X boxes) — so when torch is
+    installed it is initialised here, whether or not the caller imported it yet."""
+    global _TORCH_READY
+    if _TORCH_READY:
+        return
+    _TORCH_READY = True
+    torch = sys.modules.get("torch")
+    if torch is None:
+        import importlib.util
+        if importlib.util.find_spec("torch") is None:
+            return
+        import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 class Engine:
     """A libeigenface context bound to one HIP device."""
 
     def __init__(self, device: int = 0):
         self._lib = N.lib()
-        import sys
-        torch = sys.modules.get("torch")
-        if torch is not None and torch.cuda.is_available():
-            # torch's HIP runtime must come up before this process's first libeigenface
-            # context, or torch afterwards reports no GPU (seen on the MI355X boxes)
-            torch.cuda.init()
+        _init_torch_first()
         h = C.c_void_p()
         rc = self._lib.ef_create(int(device), C.byref(h))
         if rc != N.EF_OK:
@@ -615,14 +632,38 @@ def _jpeg_mode(mode):
         raise ValueError(f"unknown JPEG output mode {mode!r} (bgr | gray)") from None
 
 
+def _bytes_data_offset():
+    """Offset of a bytes object's payload from id(): CPython's PyBytesObject layout,
+    verified once (0 disables the fast path)."""
+    probe = b"eigenface-probe"
+    off = sys.getsizeof(b"") - 1
+    try:
+        if C.string_at(id(probe) + off, len(probe)) == probe:
+            return off
+    except Exception:  # pragma: no cover - non-CPython
+        pass
+    return 0
+
+
+_BYTES_OFF = None
+
+
 def _pack_blobs(blobs):
     """Address the files in place (no concatenation): (base pointer, int64 offsets from it,
     int64 sizes, keep-alive list).  The C ABI reads file i at base + offsets[i]."""
-    views = [np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8) for b in blobs]
-    sizes = np.fromiter((len(b) for b in blobs), np.int64, len(blobs))
-    addrs = np.fromiter((v.ctypes.data for v in views), np.int64, len(views))
-    base = int(addrs.min()) if len(views) else 0
-    return base, addrs - base, sizes, views
+    global _BYTES_OFF
+    if _BYTES_OFF is None:
+        _BYTES_OFF = _bytes_data_offset()
+    n = len(blobs)
+    sizes = np.fromiter((len(b) for b in blobs), np.int64, n)
+    if _BYTES_OFF and all(type(b) is bytes for b in blobs):  # payload address = id + header
+        addrs = np.fromiter((id(b) for b in blobs), np.int64, n) + _BYTES_OFF
+        keep = blobs
+    else:
+        keep = [np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8) for b in blobs]
+        addrs = np.fromiter((v.ctypes.data for v in keep), np.int64, n)
+    base = int(addrs.min()) if n else 0
+    return base, addrs - base, sizes, keep
 
 
 def jpeg_info(blobs, _packed=None):
