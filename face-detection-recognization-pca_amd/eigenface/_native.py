@@ -103,6 +103,21 @@ _SIGS = {
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
 
+def _load_torch_runtime_first():
+    """One HIP runtime per process.  torch's wheel bundles its own ``libamdhip64.so``
+    (soname ``libamdhip64.so.7``) and its libraries NEED it by the file name
+    ``libamdhip64.so``; libeigenface NEEDs the soname.  Loaded after torch, libeigenface
+    binds to torch's already-mapped runtime; loaded first, it maps /opt/rocm's and a later
+    ``import torch`` maps a second runtime, and whichever initialises second sees no GPU
+    (``ef_create`` fails with EF_E_HIP, or torch reports no device).  So torch, when it is
+    installed, is imported before the library is opened."""
+    import importlib.util
+    import sys
+    if "torch" in sys.modules or importlib.util.find_spec("torch") is None:
+        return
+    import torch  # noqa: F401
+
+
 def lib():
     """Load (once) and return the ctypes handle; raise loudly when unavailable."""
     global _lib
@@ -115,6 +130,7 @@ def lib():
             raise NativeLibraryError(
                 f"{LIB_PATH} not found: build it with `make -C face-detection-recognization-pca_amd` "
                 "or __graft_entry__.build() (there is no CPU fallback)")
+        _load_torch_runtime_first()
         try:
             h = C.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - depends on the box

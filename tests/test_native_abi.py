@@ -43,6 +43,21 @@ def test_library_is_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle target id
 
 
+def test_one_hip_runtime_per_process():
+    """Opening libeigenface before anything imported torch must not map a second HIP
+    runtime when torch comes in later (two runtimes: the one that initialises second
+    sees no GPU — the drop-in trainers' subprocess failure on the box)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from eigenface import _native; _native.lib()\n"
+            "import torch\n"
+            "maps = open('/proc/self/maps').read().split('\\n')\n"
+            "paths = {l.split()[-1] for l in maps if 'libamdhip64' in l}\n"
+            "print(len(paths), sorted(paths))\n") % os.path.join(ROOT, "face-detection-recognization-pca_amd")
+    r = subprocess.run([__import__("sys").executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.startswith("1 "), r.stdout
+
+
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
