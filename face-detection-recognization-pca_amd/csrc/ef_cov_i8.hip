@@ -21,14 +21,15 @@
 // also produces the exact column sums (sum x, sum x^2) the StandardScaler needs, so X is
 // read once for both.
 //
-// SYRK kernel: 256 x 256 output tile per workgroup (upper triangle of tiles only), 8 waves
-// of 128 x 64, K-slices of 64 samples staged by global_load_lds into a 4-stage LDS ring
-// (4 x 32 KiB, two stages in flight behind the landed one, fragments of the next stage
-// read ahead of the current stage's last MFMAs), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the
-// ds_read_b128 fragment reads are conflict-free.  Work items = (tile, K-split): the split
+// SYRK kernel: 256 x 384 output tile per workgroup (the tiles that touch the upper
+// triangle; 256 x 256 below order 2048), 8 waves of 128 x 96, K-slices of 64 samples staged
+// by global_load_lds into a 4-stage LDS ring (4 x 40 KiB = all of LDS, three stages in
+// flight behind the landed one, fragments of the next stage read ahead of the current
+// stage's last MFMAs), 64-B rows XOR-swizzled by ((row >> 2) & 3) so the ds_read_b128
+// fragment reads are conflict-free.  Work items = (tile, K-split): the split
 // count is chosen so items fill whole rounds of the chip (no tail round), and the item list
 // is split-major, so each XCD (blocks b = x mod 8) streams its own K range of every panel
-// while its ~32 resident workgroups run one 4 x 8 block of tiles (12 panels shared in L2).
+// while its ~32 resident workgroups run one 8 x 4 block of tiles (12 panels shared in L2).
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -41,10 +42,8 @@ namespace ef {
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int YT = 256;                   // output tile (rows and columns)
+constexpr int YT = 256;                   // output tile rows (columns: 256 or 384, syrk_tile_cols)
 constexpr int YK = 64;                    // samples per stage
-constexpr int YSL = YT * YK;              // bytes per operand stage
-constexpr int YNB = 4;                    // LDS stages in the ring (YNB - 2 in flight behind the landed one)
 constexpr int64_t kMaxSplitStages = 2047; // 2047 * 64 = 131008 samples: int32-safe
 constexpr int FB = 64;                    // finalize block
 
@@ -161,20 +160,31 @@ __global__ __launch_bounds__(256) void transpose_stats_kernel(const uint8_t* __r
 }
 
 // ---------------------------------------------------------------- SYRK on int8 MFMA
-// Slab[ks][i][j] = sum over split ks's samples of At[.][i][k] At[.][j][k], for the upper
-// triangle of 256-tiles (i-tile <= j-tile).  Item = (split, tile), split-major.
+// Slab[ks][i][j] = sum over split ks's samples of At[.][i][k] At[.][j][k] over the tiles
+// (256 rows x TJ columns) that touch the upper triangle.  Item = (split, tile), split-major.
+// Per CU the kernel is bound by the L2 -> LDS stream (an XCD-L2-resident gather runs at
+// ~30 B/clk per CU): a stage moves (256 + TJ) x 64 B for 256 x TJ x 64 MACs, i.e. 32 B per
+// MFMA-clock at TJ = 256 and 26.7 B at TJ = 384 (192 accumulator VGPRs per lane, the most
+// two waves per SIMD can hold next to their fragments).
+template <int TJ, int NB>
 __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                          int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
                                                          int nitems, const int2* __restrict__ order,
                                                          int* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[YNB * 2 * YSL];  // [stage][A | B], 128 KiB
+  constexpr int NJ = TJ / 128;              // 32-column blocks per wave (waves are 2 x 4 of 128 x TJ/4)
+  constexpr int NPA = YT / 16, NP = (YT + TJ) / 16, PPW = NP / 8;  // 1-KiB DMA pieces: A, all, per wave
+  constexpr int STG = (YT + TJ) * YK;       // bytes per stage (A panel, then B panel)
+  static_assert(NP % 8 == 0, "pieces must split evenly over the 8 waves");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NB * STG];
   const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
   // blocks b and b+8 share an XCD: XCD x runs list entries [x*total/8, (x+1)*total/8)
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
   if (lin >= nitems) return;
   const int ks = lin / ntiles;
   const int2 tt = order[lin - ks * ntiles];
-  const int64_t i0 = (int64_t)tt.x * YT, j0 = (int64_t)tt.y * YT;
+  // wave-uniform: keep the tile origin (and everything derived from it) in SGPRs
+  const int64_t i0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.x) * YT;
+  const int64_t j0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.y) * TJ;
   const int64_t sb = st_begin + ks * kps;
   const int64_t se = sb + kps < st_end ? sb + kps : st_end;
   const int64_t nst = se > sb ? se - sb : 0;
@@ -182,87 +192,97 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c32 = lane & 31;
-  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 x 64
+  const int wm = wave >> 2, wn = wave & 3;
 
-  // DMA: a stage = 16 pieces of 1 KiB (16 rows x 64 B) per operand; wave w issues
-  // pieces 2w, 2w+1 of A and of B.  Lane l -> row 16j + (l >> 2), physical chunk l & 3
-  // holding logical chunk (l & 3) ^ ((l >> 4) & 3).
+  // DMA: a stage = NP pieces of 1 KiB (16 rows x 64 B), A's then B's, contiguous in LDS;
+  // wave w issues pieces PPW*w .. PPW*w + PPW-1.  Lane l -> row 16j + (l >> 2), physical
+  // chunk l & 3 holding logical chunk (l & 3) ^ ((l >> 4) & 3).  The per-lane byte offsets
+  // inside a stage block are fixed for the item: the stage loop only moves the wave-uniform
+  // SGPR base (no per-lane 64-bit address arithmetic per stage).
   const unsigned lds_base = lds_addr(smem);
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
   const int64_t blk = dim * YK;  // bytes per K-stage block of At
-  // per-lane byte offsets inside a stage block are fixed for the item: the stage loop only
-  // moves the wave-uniform SGPR base (no per-lane 64-bit address arithmetic per stage)
-  unsigned voff[2][2];
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int j = wave * 2 + jj;
-    int64_t ra = i0 + j * 16 + lrow, rb = j0 + j * 16 + lrow;
-    ra = ra < dim ? ra : dim - 1;
-    rb = rb < dim ? rb : dim - 1;
-    voff[jj][0] = (unsigned)(ra * YK + lchunk * 16);
-    voff[jj][1] = (unsigned)(rb * YK + lchunk * 16);
-  }
+  // one per-lane offset for every piece; the piece's first row goes into the wave-uniform
+  // SGPR base.  Rows past dim (the last tiles) read the next stage block, or the
+  // kSyrkPadBytes the allocation carries past the last one: finite values whose products
+  // land only in outputs the epilogue masks.
+  const unsigned voff = (unsigned)(lrow * YK + lchunk * 16);
   auto issue = [&](int64_t st, int buf) {
-    const unsigned long long base = (unsigned long long)(size_t)(At + st * blk);
+    const uint8_t* base = At + st * blk;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = wave * 2 + jj;
-      glds16s(voff[jj][0], base, lds_base + (unsigned)(buf * 2 * YSL + j * 1024));
-      glds16s(voff[jj][1], base, lds_base + (unsigned)(buf * 2 * YSL + YSL + j * 1024));
+    for (int q = 0; q < PPW; ++q) {
+      const int p = wave * PPW + q;
+      const int64_t r0 = p < NPA ? i0 + p * 16 : j0 + (p - NPA) * 16;
+      glds16s(voff, (unsigned long long)(size_t)(base + r0 * YK), lds_base + (unsigned)(buf * STG + p * 1024));
     }
   };
 
-  i32x16 acc[4][2];
+  i32x16 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = i32x16{};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = i32x16{};
 
   const int sw = (c32 >> 2) & 3;  // swizzle key of every row this lane reads
   // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r] for k-step s of a stage
-  auto frag = [&](const uint8_t* sa, int s, i32x4 (&a)[4], i32x4 (&b)[2]) {
-    const int pch = ((2 * s + h) ^ sw) * 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const i32x4*>(sa + (wm * 128 + i * 32 + c32) * YK + pch);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sa + YSL + (wn * 64 + j * 32 + c32) * YK + pch);
+  // per-lane fragment offsets for the two k-steps; blocks i / j add i * 2048 / j * 2048
+  // (immediate offsets of one ds_read_b128 base)
+  const unsigned offa[2] = {(unsigned)((wm * 128 + c32) * YK + ((h ^ sw) * 16)),
+                            (unsigned)((wm * 128 + c32) * YK + (((2 + h) ^ sw) * 16))};
+  const unsigned offb[2] = {(unsigned)(YT * YK + (wn * (TJ / 4) + c32) * YK + ((h ^ sw) * 16)),
+                            (unsigned)(YT * YK + (wn * (TJ / 4) + c32) * YK + (((2 + h) ^ sw) * 16))};
+  auto fa = [&](const uint8_t* sa, int s, int i) {
+    return *reinterpret_cast<const i32x4*>(sa + offa[s] + i * 32 * YK);
   };
-  auto mma = [&](const i32x4 (&a)[4], const i32x4 (&b)[2]) {
+  auto fb = [&](const uint8_t* sa, int s, i32x4 (&b)[NJ]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const i32x4*>(sa + offb[s] + j * 32 * YK);
   };
-  // Ring of YNB stages.  Each stage is 4 DMA instructions per wave, so "stage t landed" is
-  // vmcnt <= 4 x (stages issued after it); tail stages past nst are issued as harmless
+  // One k-step's MFMAs, row block by row block; each A fragment is refilled with the
+  // next k-step's as soon as its row block's MFMAs are issued (one A set + two B sets live:
+  // 40 fragment VGPRs next to the 64 * NJ accumulators).
+  auto mma = [&](i32x4 (&a)[4], const i32x4 (&b)[NJ], const uint8_t* nsa, int ns) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+      a[i] = fa(nsa, ns, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Ring of NB stages.  Each stage is PPW DMA instructions per wave, so "stage t landed" is
+  // vmcnt <= PPW x (stages issued after it); tail stages past nst are issued as harmless
   // re-reads of the first stage so the count stays uniform.  One barrier per stage, placed
   // between the stage's two k-steps: it publishes stage st+1 and retires stage st's slot,
   // so the next stage's first fragments are read, and the DMA into the retired slot issued,
-  // while the second k-step's 8 MFMAs are still to run — the MFMA pipe never waits for
-  // the barrier plus an LDS round trip.  3 stages stay in flight behind the landed one.
+  // while the second k-step's MFMAs are still to run — the MFMA pipe never waits for the
+  // barrier plus an LDS round trip.  NB-1 stages stay in flight behind the landed one.
   if (nst > 0) {
-    for (int j = 0; j < YNB; ++j) issue(sb + (j < nst ? j : 0), j);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (YNB - 1)) : "memory");  // stage 0 landed
+    for (int j = 0; j < NB; ++j) issue(sb + (j < nst ? j : 0), j);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 1)) : "memory");  // stage 0 landed
     __syncthreads();
-    i32x4 a0[4], b0[2], a1[4], b1[2];
-    frag(smem, 0, a0, b0);
+    i32x4 a[4], b0[NJ], b1[NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = fa(smem, 0, i);
+    fb(smem, 0, b0);
     for (int64_t st = 0; st < nst; ++st) {
-      const uint8_t* cur = smem + (st % YNB) * 2 * YSL;
-      frag(cur, 1, a1, b1);
+      const uint8_t* cur = smem + (st % NB) * STG;
+      fb(cur, 1, b1);
       __builtin_amdgcn_sched_barrier(0);
-      mma(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (YNB - 2)) : "memory");  // stage st+1 landed
+      mma(a, b0, cur, 1);  // k-step 0; A refilled with k-step 1
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 2)) : "memory");  // stage st+1 landed
       __syncthreads();  // every wave done reading stage st; stage st+1 visible
       {
-        const int64_t nx = st + YNB;
-        issue(sb + (nx < nst ? nx : 0), (int)(nx % YNB));  // into stage st's slot
+        const int64_t nx = st + NB;
+        issue(sb + (nx < nst ? nx : 0), (int)(nx % NB));  // into stage st's slot
       }
-      if (st + 1 < nst) frag(smem + ((st + 1) % YNB) * 2 * YSL, 0, a0, b0);
+      // (after the last stage these read a slot holding a re-read of the first stage:
+      // harmless, unused, and branch-free)
+      const uint8_t* nxt = smem + ((st + 1) % NB) * STG;
+      fb(nxt, 0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      mma(a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
+      mma(a, b1, nxt, 0);  // k-step 1; A refilled with the next stage's k-step 0
     }
     dma_wait_all();
   }
@@ -270,8 +290,8 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = j0 + wn * 64 + j * 32 + c32;
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t col = j0 + wn * (TJ / 4) + j * 32 + c32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = i0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -379,15 +399,40 @@ __global__ __launch_bounds__(256) void cov_finalize_kernel(const int* __restrict
 int64_t cov_i8_kpad(int64_t K) { return (K + YK - 1) / YK * YK; }
 
 int64_t cov_i8_order_bytes(int64_t dim) {
-  const int64_t t = (dim + YT - 1) / YT;
+  const int64_t t = (dim + YT - 1) / YT;  // the 256 x 256 tiling has the most tiles
   return t * (t + 1) / 2 * (int64_t)sizeof(int2) + 64;
+}
+
+// SYRK tile columns: 384 (fewer bytes per MAC) unless the matrix is too small for the
+// wider tile to pay (its diagonal tiles compute more of the lower triangle).
+static int syrk_tile_cols(int64_t dim) {
+  int tj = dim >= 2048 ? 384 : 256;
+#ifdef EF_DIAGNOSTICS
+  if (const char* e = getenv("EF_SYRK_TJ")) tj = atoi(e) == 384 ? 384 : 256;
+#endif
+  return tj;
+}
+
+// Tiles (256 rows x tj columns) that hold an upper-triangle element, in blocks of 8 row
+// tiles x (2048 / tj) column tiles: consecutive list entries run together on one XCD and
+// share their panels in its L2.
+static std::vector<int2> syrk_tiles(int64_t dim, int tj) {
+  const int nti = (int)((dim + YT - 1) / YT), ntj = (int)((dim + tj - 1) / tj);
+  const int bw = 2048 / tj;
+  std::vector<int2> order;
+  for (int bi = 0; bi < nti; bi += 8)
+    for (int bj = 0; bj < ntj; bj += bw)
+      for (int ti = bi; ti < bi + 8 && ti < nti; ++ti)
+        for (int tj_ = bj; tj_ < bj + bw && tj_ < ntj; ++tj_)
+          if (std::min<int64_t>((int64_t)tj_ * tj + tj - 1, dim - 1) >= (int64_t)ti * YT) order.push_back(make_int2(ti, tj_));
+  return order;
 }
 
 CovPlan cov_i8_plan(int64_t dim, int64_t K, int64_t slab_budget) {
   CovPlan p;
   p.nst = cov_i8_kpad(K) / YK;
-  const int64_t t = (dim + YT - 1) / YT;
-  p.ntiles = (int)(t * (t + 1) / 2);
+  p.tj = syrk_tile_cols(dim);
+  p.ntiles = (int)syrk_tiles(dim, p.tj).size();
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (ncu < 1) ncu = 256;
@@ -445,14 +490,7 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
                          double* C) {
   const int64_t dim = gram ? n : d;
-  const int ntile = (int)((dim + YT - 1) / YT);
-  // upper-triangle tiles in 4 x 8 blocks (L2 reuse within an XCD), one H2D of the list
-  std::vector<int2> order;
-  for (int bi = 0; bi < ntile; bi += 4)
-    for (int bj = bi / 8 * 8; bj < ntile; bj += 8)
-      for (int ti = bi; ti < bi + 4 && ti < ntile; ++ti)
-        for (int tj = bj; tj < bj + 8 && tj < ntile; ++tj)
-          if (ti <= tj) order.push_back(make_int2(ti, tj));
+  const std::vector<int2> order = syrk_tiles(dim, p.tj);  // one H2D of the list
   if ((int)order.size() != p.ntiles) return hipErrorInvalidValue;
   hipError_t e = hipMemcpyAsync(order_dev, order.data(), order.size() * sizeof(int2), hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
@@ -467,8 +505,12 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
   for (int pass = 0; pass < p.passes; ++pass) {
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
-    hipLaunchKernelGGL(syrk_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps, p.ntiles,
-                       nitems, static_cast<const int2*>(order_dev), slabs);
+    if (p.tj == 384)
+      hipLaunchKernelGGL((syrk_i8_kernel<384, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+    else
+      hipLaunchKernelGGL((syrk_i8_kernel<256, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
     if (p.passes > 1)
       hipLaunchKernelGGL(slab_accumulate_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s, slabs,
                          p.splits, dim, S64);

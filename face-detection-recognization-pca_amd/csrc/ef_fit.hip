@@ -465,7 +465,7 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
   const bool fused = int8_path && !gram && cov_i8_fused_stats(Xd, d);
   if (int8_path) {
-    EF_TRY(B.get(c, (size_t)dim * cov_i8_kpad(gram ? d : n), &At));
+    EF_TRY(B.get(c, (size_t)dim * cov_i8_kpad(gram ? d : n) + kSyrkPadBytes, &At));
     EF_HIP(c, launch_cov_i8_prep(s, Xd, n, d, gram, At, fused ? S1 : nullptr, fused ? S2 : nullptr), "cov prep");
   }
   if (!fused) EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");

@@ -121,8 +121,10 @@ struct CovPlan {
   int64_t kps = 0;              // K stages per work item (<= 2047: int32-exact)
   int64_t slab_elems = 0;       // splits * dim * dim
   int ntiles = 0, splits = 1, passes = 1;
+  int tj = 256;                 // SYRK tile columns (tiles are 256 x tj)
 };
 int64_t cov_i8_kpad(int64_t K);
+constexpr int64_t kSyrkPadBytes = 384 * 64;  // readable slack the At allocation carries past its end
 int64_t cov_i8_order_bytes(int64_t dim);  // device scratch for the tile order list
 CovPlan cov_i8_plan(int64_t dim, int64_t K, int64_t slab_budget);
 bool cov_i8_fused_stats(const uint8_t* X, int64_t d);  // covariance-path prep can produce S1/S2

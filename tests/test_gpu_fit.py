@@ -63,6 +63,8 @@ def test_sklearn_path_golden():
     (60, 4096, 20, 32), (87, 1000, 86, 32), (500, 64, 10, 32), (300, 48, 48, 32),
     # k > 80: direct grid-Jacobi (order <= 1024) and subspace iteration + grid Jacobi
     (600, 4096, 128, 256), (1500, 4096, 100, 256), (3000, 1024, 130, 256),
+    # order >= 2048: the 256 x 384 SYRK tiles, ragged against both tile sizes (Gram, covariance)
+    (2100, 4096, 20, 32), (2500, 2116, 20, 32),
     # covariance path with n > 65536: the int8 product's int32 -> int64 flush
     (70000, 256, 12, 64),
     # covariance path with d % 4 != 0: byte-granular transpose + separate column stats
@@ -119,15 +121,16 @@ def test_standardized_covariance_path_vs_oracle():
                                atol=1e-7 * np.abs(o["face_features"]).max())
 
 
-def test_covariance_multi_pass():
+@pytest.mark.parametrize("side", [8, 46])
+def test_covariance_multi_pass(side):
     """Force the int8 covariance into several syrk passes (slab budget of one split,
     EF_OPT_COV_SLAB_BYTES): the int64 slab accumulation between passes must keep the
-    product exact."""
+    product exact (order 64: 256 x 256 tiles; order 2116: 256 x 384 tiles)."""
     from eigenface import get_engine, manual_pca
-    x, _ = orc.synth_faces(140_000, 8, r=32, seed=5)  # K = 140000 > 2047 * 64 samples per split
+    x, _ = orc.synth_faces(140_000, side, r=32, seed=5)  # K = 140000 > 2047 * 64 samples per split
     e = get_engine(0)
     default = e.get_option("cov_slab_bytes")
-    e.set_option("cov_slab_bytes", 64 * 64 * 4)
+    e.set_option("cov_slab_bytes", side ** 4 * 4)
     try:
         eig, mean, proj, lam = manual_pca(x, 8)
     finally:
