@@ -169,13 +169,18 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
                          kWorkElems),
            "G = Y^T.Y");
     int hinfo = -1;
-    if (m <= kCholeskyMax) {
+    const bool fused = chol_inv_supported(m);  // Cholesky + L^-1 in one register-resident workgroup
+    if (fused) {
+      EF_HIP(c, launch_chol_inv(s, G, m, m, 1e-13, Li, cinfo), "cholesky + L^-1");
+    } else if (m <= kCholeskyMax) {
       EF_HIP(c, launch_cholesky(s, G, m, m, 1e-13, cinfo), "cholesky");
+    }
+    if (fused || m <= kCholeskyMax) {
       EF_HIP(c, hipMemcpyAsync(&hinfo, cinfo, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
     }
     if (hinfo == 0) {  // Q = Y . L^-T: explicit inverse of the m x m factor (it IS (L^-T)^T), one GEMM
-      EF_HIP(c, launch_tri_inv(s, G, m, Li), "L^-1");
+      if (!fused) EF_HIP(c, launch_tri_inv(s, G, m, Li), "L^-1");
       if (tall_gemm_supported(m, Y, 8)) {
         EF_HIP(c, tall_gemm_f64(s, Y, m, false, Li, m, Q, m, dim, m, m, 1.0, work, kWorkElems), "Q = Y.L^-T");
       } else {  // odd row pitch: generic GEMM on L^-T written out
@@ -262,7 +267,11 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
 #else
       (void)wi;
 #endif
-      if (coarse && worst < 1e-4) coarse = false;  // fp64 products from the next iteration on
+      double coarse_tol = 1e-4;
+#ifdef EF_DIAGNOSTICS
+      if (const char* e = getenv("EF_FIT_COARSE_TOL")) coarse_tol = atof(e);
+#endif
+      if (coarse && worst < coarse_tol) coarse = false;  // fp64 products from the next iteration on
       // Schedule the next Rayleigh-Ritz step.  The test above passes once the PREVIOUS
       // step's Ritz values were already within 1e-13, so with the change per period
       // shrinking geometrically (worst now vs worst at the previous step) the current error

@@ -3,6 +3,7 @@
 // fp32 eigenvectors cannot meet 1e-4 on the trailing real-face components
 // (SURVEY.md §7 "fp32 conditioning"), and the reference itself is fp64 LAPACK
 // (useless/train.py:84-95).
+#include "ef_dma.hpp"
 #include "ef_linalg.hpp"
 
 #include <climits>
@@ -539,6 +540,193 @@ hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double 
   }
   hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), (size_t)m * kCholPS * sizeof(double), s, A, m, lda, tol_rel,
                      info);
+  return hipGetLastError();
+}
+
+// CholQR factor for the subspace block (m <= 256): Li = L^-1 with G = L L^T, in ONE
+// workgroup with the matrices in registers.  1024 threads as a 32 x 32 grid (p, q); thread
+// (p, q) owns the lower-triangle entries (i, l) = (p + 32x, q + 32y), x, y in 0..7: x > y,
+// or x == y when p >= q — at most 36 fp64 values, packed in slots s(x, y) = x(x+1)/2 + y.
+// (Row/column blocks of 8 would need 528 threads x 128 VGPRs: over the 3-wave budget.)
+// Orders below 256 are padded with a diagonal equal to the largest pivot candidate.
+//  Phase 1 (right-looking Cholesky on unscaled columns, the chol_small_kernel form): step t
+//  publishes column t through LDS, one barrier, then A[i][l] -= A[i][t] A[l][t] / A[t][t]
+//  for l > t; the square roots and the scaling come at the end.  L^T goes to Li.
+//  Phase 2 (forward substitution L X = I, right-looking): step t finalises row t of X,
+//  X[t][:] = R[t][:] / L[t][t], publishes it, one barrier, then R[i][l] -= L[i][t] X[t][l]
+//  for i > t; the columns of L stream back from Li into LDS eight at a time by LDS-DMA,
+//  one chunk ahead.  X then overwrites Li (zeros above the diagonal).
+// t = 32 Y + tq with the block index Y unrolled, so every register slot is addressed by a
+// compile-time constant (a run-time index would move the array to scratch).  Replaces
+// the global-memory pair chol_kernel (0.34 ms at m = 256) + tri_inv_kernel (0.19 ms),
+// which were bound by per-step L2 round trips.  A pivot <= tol_rel * max diagonal:
+// *info = -(t+1), Li untouched.
+constexpr int kCholInvMax = 256;
+
+__device__ __forceinline__ constexpr int cslot(int x, int y) { return x * (x + 1) / 2 + y; }
+
+__global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict__ G, int m, int64_t lda,
+                                                        double tol_rel, double* __restrict__ Li,
+                                                        int* __restrict__ info) {
+  __shared__ double col[2][kCholInvMax];  // phase 1: column t; phase 2: row t of X
+  __shared__ double sq[kCholInvMax];      // diag(L) = sqrt of the pivots
+  __shared__ __attribute__((aligned(16))) double lch[2][8][kCholInvMax];  // phase 2: 8 columns of L
+  __shared__ double red[16];
+  const int tid = threadIdx.x, p = tid >> 5, q = tid & 31;
+  const bool pq = p >= q;
+  if (tid < 2 * kCholInvMax) col[tid >> 8][tid & 255] = 0.0;
+
+  // max diagonal (pivot tolerance and padding value)
+  double dm = 0.0;
+  if (p == q)
+    for (int x = 0; x < 8; ++x)
+      if (p + 32 * x < m) dm = fmax(dm, G[(int64_t)(p + 32 * x) * lda + p + 32 * x]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dm = fmax(dm, __shfl_xor(dm, off));
+  if ((tid & 63) == 0) red[tid >> 6] = dm;
+  __syncthreads();
+  double mx = 0.0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) mx = fmax(mx, red[w]);
+  const double tol = tol_rel * mx;
+  const double pad = mx > 0.0 ? mx : 1.0;
+
+  double a[36];
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int y = 0; y <= x; ++y) {
+      const int i = p + 32 * x, l = q + 32 * y;
+      double v = 0.0;
+      if (x > y || pq) v = (i < m && l < m) ? G[(int64_t)i * lda + l] : (i == l ? pad : 0.0);
+      a[cslot(x, y)] = v;
+    }
+
+  // ---- phase 1: unscaled right-looking Cholesky
+#pragma unroll
+  for (int Y = 0; Y < 8; ++Y) {
+    for (int tq = 0; tq < 32; ++tq) {
+      const int t = 32 * Y + tq, buf = t & 1;
+      if (q == tq) {  // publish column t: rows p + 32x, x >= Y
+#pragma unroll
+        for (int x = Y; x < 8; ++x)
+          if (x > Y || pq) col[buf][p + 32 * x] = a[cslot(x, Y)];
+      }
+      __syncthreads();
+      // every LDS read of the step issued together, then one wait (the pivot's division
+      // overlaps the reads)
+      const double d = col[buf][t];
+      double cl[8], ci[8];
+#pragma unroll
+      for (int y = Y; y < 8; ++y) cl[y] = col[buf][q + 32 * y];
+#pragma unroll
+      for (int x = Y; x < 8; ++x) ci[x] = col[buf][p + 32 * x];
+      if (!(d > tol)) {  // uniform: every thread read the same pivot
+        if (tid == 0) *info = -(t + 1);
+        return;
+      }
+      // branch-free update: operands of entries that must not change are selected to 0
+      // (columns l <= t are final; slots outside the triangle are never read); col holds
+      // only finite values (zeroed at entry), so 0 * col stays 0
+      const double inv = 1.0 / d;
+#pragma unroll
+      for (int y = Y; y < 8; ++y) cl[y] = (y > Y || q > tq) ? cl[y] * inv : 0.0;
+#pragma unroll
+      for (int x = Y; x < 8; ++x)
+#pragma unroll
+        for (int y = Y; y <= x; ++y) a[cslot(x, y)] = fma(-ci[x], cl[y], a[cslot(x, y)]);
+    }
+  }
+  if (pq && p == q) {
+#pragma unroll
+    for (int x = 0; x < 8; ++x) sq[p + 32 * x] = sqrt(a[cslot(x, x)]);
+  }
+  __syncthreads();
+  // L^T into Li: row l holds column l of L (L[i][l] = a / sqrt(d_l), sqrt(d_l) on the diagonal)
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int y = 0; y <= x; ++y) {
+      const int i = p + 32 * x, l = q + 32 * y;
+      if ((x > y || pq) && i < m && l < m) Li[(int64_t)l * m + i] = i == l ? sq[l] : a[cslot(x, y)] / sq[l];
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- phase 2: X = L^-1, rows finalised in order (R starts as the identity)
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int y = 0; y <= x; ++y) a[cslot(x, y)] = (x == y && p == q) ? 1.0 : 0.0;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nch = (m + 7) >> 3;
+  const int segs = (m * 8 + 1023) / 1024;  // 1-KiB DMA pieces per row of L^T
+  auto issue_chunk = [&](int ch) {          // rows 8ch..8ch+7 of L^T -> lch[ch & 1]
+    const int row = 8 * ch + wave;
+    if (wave < 8 && row < m) {
+      for (int sg = 0; sg < segs; ++sg) {
+        const int off = sg * 1024 + lane * 16;
+        if (off < m * 8)
+          glds16(reinterpret_cast<const char*>(Li + (int64_t)row * m) + off,
+                 lds_addr(&lch[ch & 1][wave][0]) + (unsigned)(sg * 1024));
+      }
+    }
+  };
+  issue_chunk(0);
+#pragma unroll
+  for (int X = 0; X < 8; ++X) {
+    for (int tp = 0; tp < 32; ++tp) {
+      const int t = 32 * X + tp, buf = t & 1;
+      if (t >= m) break;  // uniform
+      if ((t & 7) == 0) {
+        dma_wait_all();
+        __syncthreads();  // chunk t/8 landed; the previous chunk's buffer is free
+        if ((t >> 3) + 1 < nch) issue_chunk((t >> 3) + 1);
+      }
+      if (p == tp) {  // row t of X: R[t][:] / L[t][t] (entries l <= t), published
+        const double f = 1.0 / sq[t];
+#pragma unroll
+        for (int y = 0; y <= X; ++y)
+          if (y < X || pq) {
+            a[cslot(X, y)] *= f;
+            col[buf][q + 32 * y] = a[cslot(X, y)];
+          }
+      }
+      __syncthreads();
+      // branch-free: rows i <= t are final (L entry selected to 0; the staged row may hold
+      // stale bytes there), X[t][l] = 0 for l > t
+      const double* lc = lch[(t >> 3) & 1][t & 7];
+      double xr[8], li[8];
+#pragma unroll
+      for (int y = 0; y <= X; ++y) xr[y] = col[buf][q + 32 * y];
+#pragma unroll
+      for (int x = X; x < 8; ++x) li[x] = lc[p + 32 * x];
+#pragma unroll
+      for (int y = 0; y <= X; ++y) xr[y] = (y < X || q <= tp) ? xr[y] : 0.0;
+#pragma unroll
+      for (int x = X; x < 8; ++x) li[x] = (x > X || p > tp) ? li[x] : 0.0;
+#pragma unroll
+      for (int x = X; x < 8; ++x)
+#pragma unroll
+        for (int y = 0; y <= X && y <= x; ++y) a[cslot(x, y)] = fma(-li[x], xr[y], a[cslot(x, y)]);
+    }
+  }
+  __syncthreads();  // every DMA read of L^T is done (awaited at its chunk boundary)
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+      const int i = p + 32 * x, l = q + 32 * y;
+      if (i < m && l < m) Li[(int64_t)i * m + l] = (y < x || (y == x && pq)) ? a[cslot(x, y < x ? y : x)] : 0.0;
+    }
+  if (tid == 0) *info = 0;
+}
+
+bool chol_inv_supported(int m) { return m >= 1 && m <= kCholInvMax && m % 2 == 0; }
+
+hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li, int* info) {
+  if (!chol_inv_supported(m)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(1024), 0, s, G, m, lda, tol_rel, Li, info);
   return hipGetLastError();
 }
 

@@ -137,6 +137,11 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
                          double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
+// Li = L^-1 (row-major, zeros above the diagonal) for G = L L^T in one register-resident
+// workgroup (m <= 256, m even: chol_inv_supported); G is not modified; *info as
+// launch_cholesky.
+bool chol_inv_supported(int m);
+hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li, int* info);
 // Training projection F (n x kk, fp64) = ((X - mu) * w) . E on int8 MFMA with E split into
 // base-256 digits (ef_proj_i8.hip); w may be null.  work: proj_i8_work_bytes bytes.
 bool proj_i8_supported(const uint8_t* X, int64_t n, int64_t d, int kk);
