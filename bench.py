@@ -1,10 +1,12 @@
 """Headline benchmark: faces/s recognised (projection + L2 nearest neighbour) against a
 1M-row gallery, 128x128 faces, k=128 eigenfaces, probe batch 4096 (BASELINE.json
-configs[2]; configs[3] when launched on N GPUs: the gallery is row-sharded across ranks
-and one RCCL all-reduce(MIN) over packed (score, index) keys picks the global match).
+configs[2]; configs[3] when launched on N GPUs: the gallery is row-sharded across ranks,
+each rank projects 1/N of the probes and one RCCL all-gather shares the features; after
+the local searches one RCCL all-gather of the per-rank fp64 match records and an exact
+merge pick the global match on every rank).
 
-One step = project 4096 uint8 probe faces (p - mean).W + search the gallery + (N>1)
-all-reduce of the 4096 keys.  Inputs are resident in HBM before timing.  Data are
+One step = project 4096 uint8 probe faces (p - mean).W + search the gallery + (N>1) the
+two all-gathers and the merge.  Inputs are resident in HBM before timing.  Data are
 synthetic (eigenface.synth): planted probes, so the step's result is also checked.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -562,7 +564,7 @@ def main():
     torch.cuda.synchronize(dev)
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s gallery rows [{lo},{hi})")
 
-    def step():  # project + local search + (N>1) all-reduce(MIN) of the packed keys
+    def step():  # project + local search + (N>1) all-gather of match records and exact merge
         shard.recognize_keys(P_dev, args.metric, keys=keys)
 
     for _ in range(args.warmup):
@@ -633,7 +635,8 @@ def main():
                 "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
                             f"probe batch {bsz}, metric {args.metric}, projection {precision}",
                 "gallery": n_total, "face": f"{side}x{side}", "k": k, "batch": bsz,
-                "parallelism": f"gallery row-shard x{world} + RCCL all-reduce(MIN) of packed keys"
+                "parallelism": f"gallery row-shard x{world}: projection split + RCCL all-gather of "
+                               "features, local search, RCCL all-gather of fp64 match records + exact merge"
                                if world > 1 else "1 GPU",
             },
             "roofline": {
