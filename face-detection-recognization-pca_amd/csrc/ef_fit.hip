@@ -131,16 +131,19 @@ __global__ void f64_to_f32_kernel(const double* __restrict__ a, int64_t n, float
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     b[i] = (float)a[i];
 }
-__global__ void f32_to_f64_kernel(const float* __restrict__ a, int64_t n, double* __restrict__ b) {
+// Y (-)= sigma Q: the shifted product (C - sigma I) Q of the subspace iteration; the fp32
+// coarse phase converts its product and shifts in one pass
+__global__ void shift_kernel(double* __restrict__ y, const double* __restrict__ q, int64_t n, double sigma) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    b[i] = (double)a[i];
+    y[i] = fma(-sigma, q[i], y[i]);
+}
+__global__ void f32_to_f64_shift_kernel(const float* __restrict__ a, const double* __restrict__ q, int64_t n,
+                                        double sigma, double* __restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = fma(-sigma, q[i], (double)a[i]);
 }
 static void cvt64to32(hipStream_t s, const double* a, int64_t n, float* b) {
   hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
-                     b);
-}
-static void cvt32to64(hipStream_t s, const float* a, int64_t n, double* b) {
-  hipLaunchKernelGGL(f32_to_f64_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
                      b);
 }
 
@@ -218,6 +221,18 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   }
   std::vector<double> th(m), prev(m, 0.0);
   bool have_prev = false, prev_fine = false;
+  // Spectral shift: the iteration multiplies by C - sigma I.  Convergence of eigenpair i
+  // goes as max_{j > m} |lambda_j - sigma| / (lambda_i - sigma) per product instead of
+  // lambda_{m+1} / lambda_i.  sigma = theta_m / 2 (theta_m, the block's smallest Ritz
+  // value, never exceeds lambda_m) is safe for any PSD C: every unwanted |lambda_j - sigma|
+  // is at most max(lambda_{m+1} - sigma, sigma) < lambda_k - sigma, so the wanted block
+  // stays dominant.  Ritz values are reported and tested unshifted.
+  double sigma = 0.0;
+  bool shift_on = true;
+#ifdef EF_DIAGNOSTICS
+  if (const char* e = getenv("EF_FIT_SHIFT")) shift_on = atoi(e) != 0;
+#endif
+  const unsigned ew_blocks = (unsigned)std::min<int64_t>((dim * m + 255) / 256, 8192);
   int it = 0;
   const int max_iters = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_fit_max_iters, 1 << 20));
   bool converged = false;
@@ -230,11 +245,12 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       EF_HIP(c, tall_gemm_f32(s, C32, dim, false, Q32, dim, Y32, m, dim, m, dim, 1.f, reinterpret_cast<float*>(work),
                               kWorkElems * 2),
              "Y = C.Q (fp32)");
-      cvt32to64(s, Y32, dim * m, Y);
+      hipLaunchKernelGGL(f32_to_f64_shift_kernel, dim3(ew_blocks), dim3(256), 0, s, Y32, Q, dim * m, sigma, Y);
     } else {
       EF_HIP(c, dense_gemm(c, s, Operand::symmetric(C, dim), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
                            kWorkElems, Bt),
              "Y = C.Q");
+      if (sigma != 0.0) hipLaunchKernelGGL(shift_kernel, dim3(ew_blocks), dim3(256), 0, s, Y, Q, dim * m, sigma);
     }
     // Rayleigh-Ritz at iterations 1, 2, 4 (small orders only: there they re-order the block
     // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
@@ -249,6 +265,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
       if (!std::isfinite(th[0])) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
+      for (int i = 0; i < m; ++i) th[i] += sigma;  // Ritz values of C (H = Q^T (C - sigma I) Q)
       // converged when every kept Ritz value moved by <= 1e-13 relative (floor 1e-15 of
       // the largest) since the previous Rayleigh-Ritz step
       bool ok = have_prev && prev_fine && fine;
@@ -287,6 +304,9 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
           if (e_now <= 3e-14) next_rr = it + 1;
         }
       }
+      // the next products use the shift of this step's block (the continuation Y.V below
+      // still carries the old one: any sequence of shifts is a valid polynomial filter)
+      sigma = shift_on && th[m - 1] > 0.0 ? 0.5 * th[m - 1] : 0.0;
       prev = th;
       have_prev = true;
       prev_fine = fine;
@@ -298,7 +318,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
         EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
                              kk, work, kWorkElems, Bt),
                "U = Q.V");
-        EF_HIP(c, hipMemcpyAsync(lam_out, lam, kk * sizeof(double), hipMemcpyDeviceToDevice, s), "copy lam");
+        EF_HIP(c, hipMemcpyAsync(lam_out, th.data(), kk * sizeof(double), hipMemcpyHostToDevice, s), "lam");
         EF_HIP(c, hipStreamSynchronize(s), "sync");
         break;
       }
