@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "face-detection-recognization-pca_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (/opt/skills/guides/MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (same guide; no sparsity)
 
 CONFIGS = {
     # name: (gallery rows, face side, k, probe batch, projection precision)
@@ -522,6 +523,9 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 recognition line")
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
     ap.add_argument("--gallery", type=int, default=0, help="override the gallery size (per-rank studies)")
+    ap.add_argument("--search", default="fp32", choices=["fp32", "split_bf16"],
+                    help="headline gallery-scan arithmetic (k <= 128); the other one is timed as a side leg")
+    ap.add_argument("--no-split", action="store_true", help="skip the side leg of the other scan arithmetic")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -567,33 +571,37 @@ def main():
     def step():  # project + local search + (N>1) all-gather of match records and exact merge
         shard.recognize_keys(P_dev, args.metric, keys=keys)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    # R repeats of exactly K timed steps, each bracketed by barrier + synchronize; the
-    # reported step time is the median repeat (max over ranks within each repeat)
-    reps = []
-    eng.timing(True)
-    eng.timing_reset()
-    for _ in range(max(1, args.repeats)):
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
+    def timed(step):
+        for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        reps.append(el)
-    eng.timing(False)
-    s_ms, s_n = eng.timing_get("search")
-    p_ms, p_n = eng.timing_get("project")
+        # R repeats of exactly K timed steps, each bracketed by barrier + synchronize; the
+        # reported step time is the median repeat (max over ranks within each repeat)
+        reps = []
+        eng.timing(True)
+        eng.timing_reset()
+        for _ in range(max(1, args.repeats)):
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            reps.append(el)
+        eng.timing(False)
+        return reps, eng.timing_get("search"), eng.timing_get("project")
+
+    split_main = args.search == "split_bf16" and k <= 128
+    eng.set_option("search_split_bf16", int(split_main))
+    reps, (s_ms, s_n), (p_ms, p_n) = timed(step)
     el = float(np.median(reps))
 
     idx, best = decode_keys(keys.cpu().numpy(), args.metric)
@@ -609,11 +617,48 @@ def main():
         host_rate = 3 * bsz / (time.perf_counter() - t)
         assert np.array_equal(hk, keys.cpu().numpy())
 
+    split_leg = None
+    if world == 1 and k <= 128 and not args.no_split:
+        # the other scan precision on the same step: split-bf16 when the headline is fp32
+        # (and vice versa); its keys must equal the headline's bit for bit
+        eng.set_stream(stream.cuda_stream)
+        eng.set_option("search_split_bf16", int(not split_main))
+        keys2 = torch.empty_like(keys)
+
+        def step2():
+            shard.recognize_keys(P_dev, args.metric, keys=keys2)
+
+        reps2, (s2_ms, s2_n), _ = timed(step2)
+        eng.set_option("search_split_bf16", int(split_main))
+        split_leg = {"scan": "split_bf16" if not split_main else "fp32", "reps": reps2,
+                     "search_avg_ms": s2_ms / max(s2_n, 1), "launches": s2_n,
+                     "keys_identical": bool(torch.equal(keys2, keys))}
+
     if rank == 0:
         ms_step = el / args.steps * 1e3
         value = bsz * args.steps / el
         search_avg_ms = s_ms / max(s_n, 1)
         flops_launch = 2.0 * bsz * (hi - lo) * k  # algorithmic: 2 k N per face x B faces
+
+        def roof(split, avg_ms):
+            # fp32 scan: priced against the fp32 MFMA peak; split-bf16 scan: its MFMA work
+            # (3 bf16 products per fp32 product, at the padded k) against the dense bf16 peak
+            if split:
+                mflops = 3.0 * 2.0 * bsz * (hi - lo) * kpad
+                a = mflops / (avg_ms * 1e-3) / 1e12
+                return {"bound": "mfma", "kernel": "search_kernel<split-bf16> (3 x bf16 MFMA per fp32 "
+                        "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
+                        "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
+                        "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
+                        "algorithmic_flops_per_launch": flops_launch,
+                        "algorithmic_TFLOPs": round(flops_launch / (avg_ms * 1e-3) / 1e12, 2)}
+            a = flops_launch / (avg_ms * 1e-3) / 1e12
+            return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
+                    + " (fp32 MFMA distance GEMM + fused arg-best)", "achieved": round(a, 2),
+                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_FP32_TFLOPS, 4),
+                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops_launch}
+
+        kpad = next(p for p in (16, 32, 64, 128, 256, 512) if p >= k)
         achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
         rec = {
@@ -629,7 +674,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32" if precision == "fp32" else "bf16 projection, f32 distance",
+            "dtype": ("f32" if precision == "fp32" else "bf16 projection, f32 distance")
+                     if not split_main else "f32 projection, split-bf16 (hi+lo) distance scan, f64 resolve",
             "data": "synthetic (eigenface.synth planted probes; gallery = eigen-coefficients)",
             "config": {
                 "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
@@ -639,24 +685,22 @@ def main():
                                "features, local search, RCCL all-gather of fp64 match records + exact merge"
                                if world > 1 else "1 GPU",
             },
-            "roofline": {
-                "bound": "mfma",
-                "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
-                + " (fp32 MFMA distance GEMM + fused arg-best)",
-                "achieved": round(achieved, 2),
-                "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "avg_launch_ms": round(search_avg_ms, 4),
-                "launches": s_n,
-                "flops_per_launch": flops_launch,
-            },
+            "roofline": dict(roof(split_main, search_avg_ms), traffic=traffic, traffic_source=traffic_src,
+                             launches=s_n),
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
             "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
             "check": {"planted_match": match},
         }
+        if split_leg:
+            el2 = float(np.median(split_leg["reps"]))
+            rec["scan_" + split_leg["scan"]] = {
+                "value": round(bsz * args.steps / el2, 1), "unit": "faces/s",
+                "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                "repeats_ms_per_step": [round(r / args.steps * 1e3, 4) for r in split_leg["reps"]],
+                "keys_identical_to_headline": split_leg["keys_identical"],
+                "roofline": dict(roof(split_leg["scan"] == "split_bf16", split_leg["search_avg_ms"]),
+                                 launches=split_leg["launches"]),
+            }
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
             rec["cpu_baseline"]["reference_pattern"] = reference_pattern(P, mean, W, G.astype(np.float64), 16,

@@ -99,9 +99,19 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
   ws.cand_cnt = reinterpret_cast<int*>(base);
   ws.match = match_dev;
   const float* aux = static_cast<const float*>(metric == EF_METRIC_L2 ? c->gnorm2.p : c->ginv.p);
+  const float* G3 = nullptr;
+  if (c->opt_search_split_bf16 && c->g_kp <= 128) {  // split-bf16 scan (the wide kernels stay fp32)
+    if (!c->g3_valid) {
+      EF_TRY(ensure(c, c->G3, (size_t)c->n_gallery * c->g_kp * sizeof(float)));
+      EF_HIP(c, launch_split_rows(c->stream, static_cast<const float*>(c->G.p), c->n_gallery, c->g_kp, c->G3.p),
+             "split gallery");
+      c->g3_valid = true;
+    }
+    G3 = static_cast<const float*>(c->G3.p);
+  }
   EF_HIP(c,
          launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), bpad, b,
-                       static_cast<const float*>(c->G.p), aux, c->n_gallery, c->g_offset, c->gmax2_host, ws,
+                       static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset, c->gmax2_host, ws,
                        keys_dev, c),
          "search");
   return EF_OK;
@@ -240,7 +250,7 @@ void ef_destroy(ef_ctx* c) {
     (void)hipEventDestroy(t.b);
   }
   DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->mean_u8,   &c->corr,      &c->G,
-                    &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
+                    &c->G3, &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev, &c->jpeg_ws, &c->jpeg_out, &c->jpeg_rows};
   for (DevBuf* b : bufs) release(*b);
   if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
@@ -380,6 +390,7 @@ int ef_gallery_set(ef_ctx* c, const float* G, int64_t n, int32_t k, int64_t offs
   if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 512 is not supported by this build");
   (void)hipSetDevice(c->device);
   c->n_gallery = 0;
+  c->g3_valid = false;
   if (n > 0) {
     EF_TRY(ensure(c, c->G, (size_t)n * kp * sizeof(float)));
     EF_TRY(ensure(c, c->gnorm2, (size_t)n * sizeof(float)));
@@ -549,6 +560,9 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
         return set_err(c, EF_E_INVALID, "EF_OPT_JPEG_CHUNK_BITS must be 0 or a multiple of 32 up to 2^24");
       c->opt_jpeg_chunk_bits = value;
       return EF_OK;
+    case EF_OPT_SEARCH_SPLIT_BF16:
+      c->opt_search_split_bf16 = value != 0;
+      return EF_OK;
     default:
       return set_err(c, EF_E_INVALID, "ef_set_option: unknown option " + std::to_string(option));
   }
@@ -563,6 +577,7 @@ int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
     case EF_OPT_TM_INT64_SUMS: *value = c->opt_tm_int64; return EF_OK;
     case EF_OPT_HAAR_ORDERED: *value = c->opt_haar_ordered; return EF_OK;
     case EF_OPT_JPEG_CHUNK_BITS: *value = c->opt_jpeg_chunk_bits; return EF_OK;
+    case EF_OPT_SEARCH_SPLIT_BF16: *value = c->opt_search_split_bf16; return EF_OK;
     default: return EF_E_INVALID;
   }
 }

@@ -74,6 +74,7 @@ struct ef_ctx {
   int64_t opt_tm_int64 = 0;
   int64_t opt_haar_ordered = 0;
   int64_t opt_jpeg_chunk_bits = 0;
+  int64_t opt_search_split_bf16 = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -97,6 +98,8 @@ struct ef_ctx {
   ef::DevBuf gnorm2; // float[n]  ||g||^2
   ef::DevBuf ginv;   // float[n]  1/||g|| (0 for a zero row)
   ef::DevBuf gmax2;  // uint (float bits) max ||g||^2
+  ef::DevBuf G3;     // split-bf16 copy of G (same bytes), built on the first split search
+  bool g3_valid = false;
   float gmax2_host = 0.f;
 
   // per-call scratch (grown on demand, never shrunk)
@@ -144,9 +147,11 @@ void timer_end(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
 SearchPlan search_plan(int64_t bpad, int64_t n, int kp);
+// G3: split-bf16 copy of G (EF_OPT_SEARCH_SPLIT_BF16, kp <= 128) or null for the fp32 kernels
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
-                         int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
-                         float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
+                         int64_t bpad, int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
+                         int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
+hipError_t launch_split_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out);
 hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b, ef_match* match);
 // keys[b] (+ merged[b]) <- exact arg-best over parts x b match records (ef_comm.hip)
 hipError_t launch_matches_merge(hipStream_t s, const ef_match* parts, int nparts, int64_t b, long long* keys,

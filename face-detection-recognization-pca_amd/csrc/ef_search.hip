@@ -28,6 +28,16 @@
 //   resolve_kernel re-scores them in fp64 and keeps the lowest index among exact ties.
 // Result: the argmin/argmax identity equals an fp64 evaluation with lowest-index
 // tie-break (np.argmin / np.argmax semantics), independent of fp32 rounding.
+//
+// Split-bf16 scores (S3, EF_OPT_SEARCH_SPLIT_BF16): every fp32 operand x is carried as
+// x = hi + lo + e with hi = bf16(x), lo = bf16(x - hi), |e| <= 2^-16 |x|, and the dot
+// product is hi.hi' + hi.lo' + lo.hi' on v_mfma_f32_32x32x16_bf16 (products exact in fp32,
+// fp32 accumulation): 3 bf16 MFMAs per 16 k instead of 8 fp32 ones, i.e. 16/3 x the
+// arithmetic rate.  The gallery's split copy has the fp32 row's byte layout (per 8
+// elements: 16 B of hi, 16 B of lo), so the tile DMA and the LDS reads are those of the
+// fp32 kernel.  The pass-2 bound covers the dropped terms (lo.lo', e) and the longer
+// chain; the winner is still re-scored from the fp32 gallery in fp64, so keys and match
+// records equal the fp32 path's bit for bit whenever both resolve (tests/test_gpu_search.py).
 #include "ef_search_common.hpp"
 
 #include <climits>
@@ -38,13 +48,36 @@ namespace ef {
 
 constexpr int TG = 64;  // gallery rows per LDS tile (two 32-row MFMA blocks)
 
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// round-to-nearest-even fp32 -> bf16 bits (finite inputs) and back
+__device__ __forceinline__ unsigned bf16_bits(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_value(unsigned b) { return __uint_as_float(b << 16); }
+// 8 consecutive fp32 values -> (hi, lo) bf16x8 fragments
+__device__ __forceinline__ void split8(const float* x, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned h = bf16_bits(x[j]);
+    hi[j] = (short)h;
+    lo[j] = (short)bf16_bits(x[j] - bf16_value(h));
+  }
+}
+__device__ __forceinline__ bf16x8 as_bf16x8(const float4& v) {
+  bf16x8 r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
+
 // Workgroup = 8 waves x 32 probes = 256 probes (the gallery is swept Bpad/256 times).
 // Each wave keeps its 32 probes as one B block (KP/2 VGPRs, pre-scaled) and runs the
 // tile's two 32-row blocks as two independent accumulator chains; the arg-best epilogue
 // is a branch-free top-2 in row order on registers.  <= 128 VGPRs -> 4 waves per SIMD.
 // ABL (diagnostic builds only, results invalid): bit 1 skips the epilogue, bit 4 skips
 // the per-tile wait + barrier.
-template <int KP, int METRIC, bool COLLECT, int ABL = 0>
+template <int KP, int METRIC, bool COLLECT, bool S3 = false, int ABL = 0>
 __global__ __launch_bounds__(512, 4) void search_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
     int n_ptiles, int tiles_per_chunk, int64_t bpad, SearchWs ws) {
@@ -188,7 +221,10 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   // (exactly) so the chain yields the score: L2 acc = ||g||^2 + sum(-2q)g (the chain
   // starts from ||g||^2), cosine acc = -q.g (times 1/||g|| after the chain).
   constexpr float QS = METRIC == EF_METRIC_L2 ? -2.f : -1.f;
-  float qb[KH];
+  // S3: the same k range as split (hi, lo) bf16x8 fragments, fragment i = k h*KH + 8i + [0, 8)
+  constexpr int NF = KH / 8;
+  float qb[S3 ? 1 : KH];
+  bf16x8 qh[S3 ? NF : 1], ql[S3 ? NF : 1];
   {
     int64_t r0 = s0;
     bool v0 = true;
@@ -197,10 +233,20 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
       r0 = v0 ? ws.amb_list[s0] : 0;
     }
     const float4* q0 = reinterpret_cast<const float4*>(qpad + r0 * KP + h * KH);
+    if constexpr (S3) {
 #pragma unroll
-    for (int j = 0; j < KH / 4; ++j) {
-      const float4 a = v0 ? q0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      qb[4 * j] = QS * a.x; qb[4 * j + 1] = QS * a.y; qb[4 * j + 2] = QS * a.z; qb[4 * j + 3] = QS * a.w;
+      for (int i = 0; i < NF; ++i) {
+        const float4 a = v0 ? q0[2 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 b = v0 ? q0[2 * i + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float t[8] = {QS * a.x, QS * a.y, QS * a.z, QS * a.w, QS * b.x, QS * b.y, QS * b.z, QS * b.w};
+        split8(t, qh[i], ql[i]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KH / 4; ++j) {
+        const float4 a = v0 ? q0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        qb[4 * j] = QS * a.x; qb[4 * j + 1] = QS * a.y; qb[4 * j + 2] = QS * a.z; qb[4 * j + 3] = QS * a.w;
+      }
     }
   }
   float thr = -__builtin_inff();
@@ -210,8 +256,13 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   // Consume every probe register here, so hipcc places its waits for these loads before
   // the loop; otherwise its (loop-merged) wait state puts vmcnt(0) inside the tile loop,
   // which would also drain the asm LDS-DMA of the next tile.
+  if constexpr (S3) {
 #pragma unroll
-  for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(qb[j]));
+    for (int i = 0; i < NF; ++i) asm volatile("" ::"v"(qh[i]), "v"(ql[i]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < KH; ++j) asm volatile("" ::"v"(qb[j]));
+  }
   asm volatile("" ::"v"(thr));
 
   const float INF = __builtin_inff();
@@ -283,6 +334,25 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
 
     // both 32-row blocks at once: two independent accumulator chains sharing the B operand
     f32x16 acc0 = acc_init(tileA), acc1 = acc_init(tileA + 32);
+    if constexpr (S3) {
+      // fragment i: chunks 2i (hi) and 2i + 1 (lo) of this lane half's k range
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const int c0 = h * (CPR / 2) + 2 * i;
+        const int ch = PAD ? c0 : c0 ^ swz, cl = PAD ? c0 + 1 : (c0 + 1) ^ swz;
+        const bf16x8 ah = as_bf16x8(*reinterpret_cast<const float4*>(arow0 + ch * 4));
+        const bf16x8 bh = as_bf16x8(*reinterpret_cast<const float4*>(arow1 + ch * 4));
+        const bf16x8 al = as_bf16x8(*reinterpret_cast<const float4*>(arow0 + cl * 4));
+        const bf16x8 bl = as_bf16x8(*reinterpret_cast<const float4*>(arow1 + cl * 4));
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, qh[i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, qh[i], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ql[i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, ql[i], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, qh[i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, qh[i], acc1, 0, 0, 0);
+        if (i % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound the A prefetch depth
+      }
+    } else
 #pragma unroll
     for (int s = 0; s < KH; s += 4) {
       const int chunk = PAD ? h * (CPR / 2) + s / 4 : (h * (CPR / 2) + s / 4) ^ swz;
@@ -345,7 +415,7 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
 }
 
 // One wave per probe: winner over chunks, global runner-up, fp64 re-score, ambiguity test.
-template <int KP, int METRIC>
+template <int KP, int METRIC, bool S3 = false>
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ qpad, int64_t b, int64_t bpad,
                                                      int nchunks, const float* __restrict__ G, int64_t n,
                                                      int64_t g_offset, float gmax2, SearchWs ws,
@@ -392,7 +462,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
   const float u = 5.9604645e-08f;  // 2^-24
   const float qn = sqrtf(qq);
   float delta;
-  if constexpr (METRIC == EF_METRIC_L2) {
+  if constexpr (S3) {
+    // split-bf16 chain: dropped terms (lo.lo', hi.e', lo.e', e.q) <= 3.02 * 2^-16 |q||g| per
+    // element, 3 KP exact products + the start value summed in fp32 (2u per add allowed, in
+    // case the matrix core's adds do not round to nearest), ||g||^2 itself to KP u
+    const float es = 3.05f * 1.5258789e-05f;  // 3.05 * 2^-16
+    if constexpr (METRIC == EF_METRIC_L2) {
+      const float gm = sqrtf(gmax2);
+      delta = 2.f * (2.f * es * qn * gm + (3 * KP + 4) * 2.f * u * 1.01f * (2.02f * qn * gm + gmax2) +
+                     KP * u * gmax2 + 4.f * u * fabsf(b1)) + 1e-30f;
+    } else {
+      delta = 2.f * ((es + (3 * KP + 8) * 2.f * u) * 1.01f * qn) + 1e-30f;
+    }
+  } else if constexpr (METRIC == EF_METRIC_L2) {
     const float gm = sqrtf(gmax2);
     delta = 2.f * ((KP + 4) * u * 1.01f * (2.f * qn * gm + gmax2) + 4.f * u * fabsf(b1));
   } else {
@@ -492,6 +574,24 @@ __global__ void gallery_aux_kernel(const float* __restrict__ G, int64_t n, int k
   }
 }
 
+// Split-bf16 copy of the gallery (S3 search): per 8 fp32 elements, 16 B of hi = bf16(x)
+// then 16 B of lo = bf16(x - hi); same row bytes as the fp32 gallery.
+__global__ void split_rows_kernel(const float* __restrict__ G, int64_t groups, uint4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= groups) return;
+  const float4 a = reinterpret_cast<const float4*>(G)[2 * i];
+  const float4 b = reinterpret_cast<const float4*>(G)[2 * i + 1];
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  unsigned hi[8], lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = bf16_bits(x[j]);
+    lo[j] = bf16_bits(x[j] - bf16_value(hi[j]));
+  }
+  out[2 * i] = make_uint4(hi[0] | hi[1] << 16, hi[2] | hi[3] << 16, hi[4] | hi[5] << 16, hi[6] | hi[7] << 16);
+  out[2 * i + 1] = make_uint4(lo[0] | lo[1] << 16, lo[2] | lo[3] << 16, lo[4] | lo[5] << 16, lo[6] | lo[7] << 16);
+}
+
 // max ||g||^2 (one atomic per block; non-negative floats order as their bit patterns)
 __global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out) {
   __shared__ float red[4];
@@ -546,11 +646,41 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
   return pl;
 }
 
+// Split-bf16 search (KP <= 128): S3 kernel on the split gallery G3 for the scan and the
+// collect pass; reduce / resolve re-score from the fp32 gallery G as in the fp32 path.
+template <int KP, int M>
+static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* qpad, int64_t bpad, int64_t b,
+                              const float* G, const float* G3, const float* aux, int64_t n, int64_t g_offset,
+                              float gmax2, const SearchWs& ws, long long* keys, TimerEvt* tev, ef_ctx* c) {
+  if constexpr (KP > 128) {
+    return hipErrorInvalidValue;
+  } else {
+    const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
+    timer_begin(c, EF_KERNEL_SEARCH, tev);
+    hipLaunchKernelGGL((search_kernel<KP, M, false, true>), grid, block, 0, s, qpad, G3, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, bpad, ws);
+    timer_end(c, tev);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    const dim3 pgrid((unsigned)((b + 3) / 4));
+    hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
+                       g_offset, gmax2, ws, keys);
+    hipLaunchKernelGGL((search_kernel<KP, M, true, true>), grid, block, 0, s, qpad, G3, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, bpad, ws);
+    hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+    return hipGetLastError();
+  }
+}
+
 template <int KP, int M>
 static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpad, int64_t bpad, int64_t b,
-                           const float* G, const float* aux, int64_t n, int64_t g_offset, float gmax2,
-                           const SearchWs& ws, long long* keys, bool timed_main, TimerEvt* tev, ef_ctx* c) {
+                           const float* G, const float* G3, const float* aux, int64_t n, int64_t g_offset,
+                           float gmax2, const SearchWs& ws, long long* keys, bool timed_main, TimerEvt* tev,
+                           ef_ctx* c) {
   constexpr bool wide = KP > 128;
+  if (!wide && G3) return search_s3_t<KP, M>(s, pl, qpad, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, tev, c);
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
   if constexpr (wide) {
@@ -564,8 +694,8 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
 #endif
   if (KP == 128 && M == EF_METRIC_L2 && abl > 0) {  // diagnostic build only: ablations (timing, wrong results)
 #ifdef EF_DIAGNOSTICS
-    auto k = abl == 1 ? search_kernel<KP, M, false, 1> : abl == 4 ? search_kernel<KP, M, false, 4>
-                                                                   : search_kernel<KP, M, false, 5>;
+    auto k = abl == 1 ? search_kernel<KP, M, false, false, 1>
+                      : abl == 4 ? search_kernel<KP, M, false, false, 4> : search_kernel<KP, M, false, false, 5>;
     hipLaunchKernelGGL(k, grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles, pl.tiles_per_chunk, bpad, ws);
 #endif
   } else {
@@ -594,17 +724,17 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
 }
 
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
-                         int64_t bpad, int64_t b, const float* G, const float* aux, int64_t n, int64_t g_offset,
-                         float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c) {
+                         int64_t bpad, int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
+                         int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c) {
   TimerEvt tev;
   tev.kernel = -1;
 #define EF_SEARCH_CASE(KPV)                                                                                 \
   case KPV:                                                                                                 \
     return metric == EF_METRIC_L2                                                                           \
-               ? search_t<KPV, EF_METRIC_L2>(s, pl, qpad, bpad, b, G, aux, n, g_offset, gmax2, ws, keys, true, \
-                                             &tev, c)                                                       \
-               : search_t<KPV, EF_METRIC_COSINE>(s, pl, qpad, bpad, b, G, aux, n, g_offset, gmax2, ws, keys,  \
-                                                 true, &tev, c);
+               ? search_t<KPV, EF_METRIC_L2>(s, pl, qpad, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, \
+                                             true, &tev, c)                                                       \
+               : search_t<KPV, EF_METRIC_COSINE>(s, pl, qpad, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, \
+                                                 keys, true, &tev, c);
   switch (kp) {
     EF_SEARCH_CASE(16)
     EF_SEARCH_CASE(32)
@@ -636,6 +766,13 @@ hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k,
   const int64_t tot = rows_pad * kp;
   hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, rows, k,
                      rows_pad, dst, kp);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out) {
+  const int64_t groups = n * kp / 8;
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, G, groups,
+                     static_cast<uint4*>(out));
   return hipGetLastError();
 }
 

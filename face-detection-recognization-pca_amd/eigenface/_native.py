@@ -30,6 +30,7 @@ EF_UNIQUE_ID_BYTES = 128
 EF_OPT_FIT_MAX_ITERS, EF_OPT_FIT_FP32_COARSE, EF_OPT_COV_SLAB_BYTES, EF_OPT_TM_INT64_SUMS, EF_OPT_HAAR_ORDERED = \
     1, 2, 3, 4, 5
 EF_OPT_JPEG_CHUNK_BITS = 6
+EF_OPT_SEARCH_SPLIT_BF16 = 7
 EF_E_NUMERIC = -5
 
 

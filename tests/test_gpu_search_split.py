@@ -1,0 +1,144 @@
+"""Split-bf16 gallery scan (EF_OPT_SEARCH_SPLIT_BF16): the scan runs on bf16 MFMA with
+(hi, lo) operands and a widened error bound; the winner is fp64-resolved exactly as on the
+fp32 scan.  Both paths return the fp64 argmin/argmax with lowest-index ties, so their keys
+must be identical bit for bit, and equal the fp64 oracle wherever the oracle's own
+runner-up gap is clear."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import eigenface_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def split(eng):
+    eng.set_option("search_split_bf16", 1)
+    yield eng
+    eng.set_option("search_split_bf16", 0)
+
+
+def _keys_both(eng, g, q, metric, offset=0):
+    eng.set_option("search_split_bf16", 0)
+    eng.set_gallery(g, global_offset=offset)
+    k32 = eng.search_keys(q, metric)
+    eng.set_option("search_split_bf16", 1)
+    k3 = eng.search_keys(q, metric)  # the split copy is built on this first split search
+    return k32, k3
+
+
+def test_option_roundtrip(split):
+    assert split.get_option("search_split_bf16") == 1
+
+
+@pytest.mark.parametrize("k", [8, 16, 50, 64, 96, 128, 200])
+@pytest.mark.parametrize("n,b", [(1, 3), (33, 257), (3001, 300)])
+def test_split_keys_equal_fp32_random(split, k, n, b):
+    rng = np.random.default_rng(k * 7 + n)
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    q = rng.standard_normal((b, k)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        k32, k3 = _keys_both(split, g, q, metric)
+        np.testing.assert_array_equal(k3, k32)
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_split_matches_oracle(split, k):
+    rng = np.random.default_rng(k)
+    g = rng.standard_normal((20000, k)).astype(np.float32)
+    q = rng.standard_normal((1000, k)).astype(np.float32)
+    split.set_gallery(g)
+    idx, best = split.search(q, "l2")
+    ref_idx, ref_d = orc.l2_argmin(q, g)
+    g64, q64 = g.astype(np.float64), q.astype(np.float64)
+    dd = (q64**2).sum(1)[:, None] + (g64**2).sum(1)[None, :] - 2.0 * q64 @ g64.T
+    s = np.partition(dd, 1, axis=1)[:, :2]
+    clear = (s[:, 1] - s[:, 0]) > 1e-9 * (q64**2).sum(1)
+    assert clear.mean() > 0.99
+    np.testing.assert_array_equal(idx[clear], ref_idx[clear])
+    d_gpu = ((q64 - g64[idx]) ** 2).sum(1)
+    np.testing.assert_allclose(best, d_gpu.astype(np.float32), rtol=1e-6)
+    idx_c, _ = split.search(q, "cosine")
+    ref_c, _ = orc.cosine_argmax(q, g)
+    srt = np.sort(orc.cosine_scores(q, g), axis=1)
+    clear_c = (srt[:, -1] - srt[:, -2]) > 1e-9
+    np.testing.assert_array_equal(idx_c[clear_c], ref_c[clear_c])
+
+
+@pytest.mark.parametrize("k", [32, 128])
+def test_split_near_ties_below_bf16_resolution(split, k):
+    """Rows whose distances to the probe differ by ~1e-6 relative (far below the split
+    scan's ~1e-4 resolution, far above fp64's): the exact winner is the later row."""
+    rng = np.random.default_rng(11 + k)
+    n, b = 5000, 256
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    q = rng.standard_normal((b, k)).astype(np.float32)
+    want = np.empty(b, np.int64)
+    for i in range(b):
+        d = rng.standard_normal(k).astype(np.float32) * 0.5
+        lo, hi = rng.choice(n, 2, replace=False)
+        lo, hi = min(lo, hi), max(lo, hi)
+        g[lo] = q[i] + d
+        g[hi] = q[i] + d * np.float32(1 - 2e-6)  # closer by ~4e-6 relative
+        want[i] = hi
+    # exact fp64 winners (the planted pairs can collide with each other's rows)
+    want = orc.l2_argmin(q, g)[0]
+    k32, k3 = _keys_both(split, g, q, "l2")
+    np.testing.assert_array_equal(k3, k32)
+    idx = (k3 & 0xFFFFFFFF).astype(np.int64)
+    np.testing.assert_array_equal(idx, want)
+
+
+def test_split_duplicates_and_ties_golden(split):
+    g = np.random.default_rng(5).standard_normal((1000, 32)).astype(np.float32)
+    g[700] = g[5]
+    g[999] = g[5]
+    g[300] = g[64]
+    q = np.stack([g[5], g[999], g[64], g[300]])
+    split.set_gallery(g)
+    idx, d = split.search(q, "l2")
+    np.testing.assert_array_equal(idx, [5, 5, 64, 64])
+    np.testing.assert_array_equal(d, [0, 0, 0, 0])
+    t = golden("ties.npz")
+    split.set_gallery(t["gallery"].astype(np.float32))
+    idx, sim = split.search(t["probes"].astype(np.float32), "cosine")
+    np.testing.assert_array_equal(idx, t["idx"])
+    np.testing.assert_allclose(sim, t["sim"], atol=1e-6)
+
+
+def test_split_sharded_offsets(split):
+    rng = np.random.default_rng(9)
+    g = rng.standard_normal((5000, 64)).astype(np.float32)
+    q = rng.standard_normal((700, 64)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        split.set_gallery(g)
+        full = split.search_keys(q, metric)
+        parts = []
+        for lo, hi in [(0, 1700), (1700, 3333), (3333, 5000)]:
+            split.set_gallery(g[lo:hi], global_offset=lo)
+            parts.append(split.search_keys(q, metric))
+        np.testing.assert_array_equal(np.minimum.reduce(parts), full)
+
+
+def test_split_planted_large(split):
+    """The C3 shape at 200k rows: planted probes (gallery row + noise) are exact."""
+    rng = np.random.default_rng(1)
+    n, k, b = 200_000, 128, 4096
+    g = (rng.standard_normal((n, k)) * orc.synth_spectrum(k)).astype(np.float32)
+    t = rng.integers(0, n, b)
+    q = (g[t] + rng.standard_normal((b, k)).astype(np.float32) * 2.0).astype(np.float32)
+    k32, k3 = _keys_both(split, g, q, "l2")
+    np.testing.assert_array_equal(k3, k32)
+    np.testing.assert_array_equal((k3 & 0xFFFFFFFF).astype(np.int64), t)
+    k32c, k3c = _keys_both(split, g, q, "cosine")
+    np.testing.assert_array_equal(k3c, k32c)
+
+
+def test_split_option_ignored_for_wide(split):
+    """k > 128 keeps the fp32 wide kernels under the option (same keys)."""
+    rng = np.random.default_rng(3)
+    g = rng.standard_normal((3000, 300)).astype(np.float32)
+    q = rng.standard_normal((300, 300)).astype(np.float32)
+    k32, k3 = _keys_both(split, g, q, "l2")
+    np.testing.assert_array_equal(k3, k32)
