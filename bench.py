@@ -524,7 +524,7 @@ def main():
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
     ap.add_argument("--gallery", type=int, default=0, help="override the gallery size (per-rank studies)")
     ap.add_argument("--search", default="fp32", choices=["fp32", "split_bf16"],
-                    help="headline gallery-scan arithmetic (k <= 128); the other one is timed as a side leg")
+                    help="headline gallery-scan arithmetic; the other one is timed as a side leg")
     ap.add_argument("--no-split", action="store_true", help="skip the side leg of the other scan arithmetic")
     args = ap.parse_args()
 
@@ -599,7 +599,7 @@ def main():
         eng.timing(False)
         return reps, eng.timing_get("search"), eng.timing_get("project")
 
-    split_main = args.search == "split_bf16" and k <= 128
+    split_main = args.search == "split_bf16"
     eng.set_option("search_split_bf16", int(split_main))
     reps, (s_ms, s_n), (p_ms, p_n) = timed(step)
     el = float(np.median(reps))
@@ -618,7 +618,7 @@ def main():
         assert np.array_equal(hk, keys.cpu().numpy())
 
     split_leg = None
-    if world == 1 and k <= 128 and not args.no_split:
+    if world == 1 and not args.no_split:
         # the other scan precision on the same step: split-bf16 when the headline is fp32
         # (and vice versa); its keys must equal the headline's bit for bit
         eng.set_stream(stream.cuda_stream)
@@ -646,7 +646,8 @@ def main():
             if split:
                 mflops = 3.0 * 2.0 * bsz * (hi - lo) * kpad
                 a = mflops / (avg_ms * 1e-3) / 1e12
-                return {"bound": "mfma", "kernel": "search_kernel<split-bf16> (3 x bf16 MFMA per fp32 "
+                return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
+                        + "<split-bf16> (3 x bf16 MFMA per fp32 "
                         "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
                         "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
                         "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
@@ -660,7 +661,8 @@ def main():
 
         kpad = next(p for p in (16, 32, 64, 128, 256, 512) if p >= k)
         achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+        traffic, traffic_src = (pmc_traffic(args.config + ("s3" if split_main else "")) if world == 1
+                                else (None, None))
         rec = {
             "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128" if args.config == "c3"
                       else f"faces/sec recognized (projection+NN) @{n_total}-gallery k={k}",
@@ -675,7 +677,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": ("f32" if precision == "fp32" else "bf16 projection, f32 distance")
-                     if not split_main else "f32 projection, split-bf16 (hi+lo) distance scan, f64 resolve",
+                     if not split_main else f"{precision} projection, split-bf16 (hi+lo) distance scan, f64 resolve",
             "data": "synthetic (eigenface.synth planted probes; gallery = eigen-coefficients)",
             "config": {
                 "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
@@ -699,7 +701,9 @@ def main():
                 "repeats_ms_per_step": [round(r / args.steps * 1e3, 4) for r in split_leg["reps"]],
                 "keys_identical_to_headline": split_leg["keys_identical"],
                 "roofline": dict(roof(split_leg["scan"] == "split_bf16", split_leg["search_avg_ms"]),
-                                 launches=split_leg["launches"]),
+                                 launches=split_leg["launches"],
+                                 **dict(zip(("traffic", "traffic_source"),
+                                            pmc_traffic(args.config + ("s3" if not split_main else ""))))),
             }
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)

@@ -100,7 +100,12 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
   ws.match = match_dev;
   const float* aux = static_cast<const float*>(metric == EF_METRIC_L2 ? c->gnorm2.p : c->ginv.p);
   const float* G3 = nullptr;
-  if (c->opt_search_split_bf16 && c->g_kp <= 128) {  // split-bf16 scan (the wide kernels stay fp32)
+  float* Q3 = nullptr;
+  if (c->opt_search_split_bf16) {  // split-bf16 scan
+    if (c->g_kp > 128) {
+      EF_TRY(ensure(c, c->q3, (size_t)bpad * c->g_kp * sizeof(float)));
+      Q3 = static_cast<float*>(c->q3.p);
+    }
     if (!c->g3_valid) {
       EF_TRY(ensure(c, c->G3, (size_t)c->n_gallery * c->g_kp * sizeof(float)));
       EF_HIP(c, launch_split_rows(c->stream, static_cast<const float*>(c->G.p), c->n_gallery, c->g_kp, c->G3.p),
@@ -110,7 +115,7 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
     G3 = static_cast<const float*>(c->G3.p);
   }
   EF_HIP(c,
-         launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), bpad, b,
+         launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), Q3, bpad, b,
                        static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset, c->gmax2_host, ws,
                        keys_dev, c),
          "search");
@@ -250,7 +255,7 @@ void ef_destroy(ef_ctx* c) {
     (void)hipEventDestroy(t.b);
   }
   DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->mean_u8,   &c->corr,      &c->G,
-                    &c->G3, &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
+                    &c->G3, &c->q3, &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev, &c->jpeg_ws, &c->jpeg_out, &c->jpeg_rows};
   for (DevBuf* b : bufs) release(*b);
   if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);

@@ -104,6 +104,7 @@ struct ef_ctx {
 
   // per-call scratch (grown on demand, never shrunk)
   ef::DevBuf q_pad;     // float[bpad][kp]
+  ef::DevBuf q3;        // split-bf16 probes [bpad][kp] (wide split-bf16 scans)
   ef::DevBuf keys;      // int64[bpad]
   ef::DevBuf search_ws; // SearchWs carve-out
   ef::DevBuf p_stage;   // probe pixels staged from host
@@ -147,8 +148,9 @@ void timer_end(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
 SearchPlan search_plan(int64_t bpad, int64_t n, int kp);
-// G3: split-bf16 copy of G (EF_OPT_SEARCH_SPLIT_BF16, kp <= 128) or null for the fp32 kernels
-hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad,
+// G3: split-bf16 copy of G (EF_OPT_SEARCH_SPLIT_BF16) or null for the fp32 kernels; Q3: scratch
+// [bpad][kp] for the split probes (kp > 128 with G3 only)
+hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad, float* Q3,
                          int64_t bpad, int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
                          int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
 hipError_t launch_split_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out);

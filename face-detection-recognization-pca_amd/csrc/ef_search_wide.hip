@@ -36,7 +36,17 @@ constexpr int WBK = 32;             // k per slice
 constexpr int WSL = WR * WBK;       // floats per gallery slice (= per probe slice)
 static_assert(WR == 128 && WP == 128, "4 waves x 32 probes, 4 x 32-row blocks");
 
-template <int KP, int METRIC, bool COLLECT>
+typedef short bf16x8w __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x8w as_bf16x8w(const float4& v) {
+  bf16x8w r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
+
+// S3: qpad and G are the split-bf16 copies (ef_search.hip: per 8 elements 16 B of hi, 16 B
+// of lo) — same bytes per row, so the slice DMA is unchanged; each 32-k slice is two
+// 16-k fragments (chunks 4h + 2i = hi, 4h + 2i + 1 = lo of lane half h), 3 bf16 MFMAs each.
+template <int KP, int METRIC, bool COLLECT, bool S3 = false>
 __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
     int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
@@ -154,6 +164,11 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
         }
       }
     } else {
+      // uniform skip of blocks that cannot change the running top-2 (ef_search.hip consume)
+      float mn = v[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mn = fminf(mn, v[r]);
+      if (!__any(mn < b2)) return;
       float m1 = v[0], m2 = INF;
       int ir = 0;
 #pragma unroll
@@ -208,6 +223,26 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     }
     const float* sg = smem + buf * 2 * WSL;
     const float* sq = sg + WSL;
+    if constexpr (S3) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ph = ((h * 4 + 2 * i) ^ sw) * 4, pl = ((h * 4 + 2 * i + 1) ^ sw) * 4;
+        const bf16x8w bh = as_bf16x8w(*reinterpret_cast<const float4*>(sq + (wave * 32 + c32) * WBK + ph));
+        const bf16x8w bl = as_bf16x8w(*reinterpret_cast<const float4*>(sq + (wave * 32 + c32) * WBK + pl));
+        bf16x8w ah[4], al[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          ah[rb] = as_bf16x8w(*reinterpret_cast<const float4*>(sg + (rb * 32 + c32) * WBK + ph));
+          al[rb] = as_bf16x8w(*reinterpret_cast<const float4*>(sg + (rb * 32 + c32) * WBK + pl));
+        }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bh, acc[rb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bl, acc[rb], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[rb], bh, acc[rb], 0, 0, 0);
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pch = ((h * 4 + j) ^ sw) * 4;  // lane half h owns k in [16h, 16h + 16) of the slice
@@ -284,13 +319,20 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
 }
 
 template <int KP, int M>
-static hipError_t wide_t(hipStream_t s, bool collect, const SearchPlan& pl, const float* qpad, const float* G,
-                         const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
+static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan& pl, const float* qpad,
+                         const float* G, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
-  if (collect)
+  if (s3) {
+    if (collect)
+      hipLaunchKernelGGL((search_wide_kernel<KP, M, true, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
+                         pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+    else
+      hipLaunchKernelGGL((search_wide_kernel<KP, M, false, true>), grid, block, 0, s, qpad, G, aux, n,
+                         pl.n_ptiles, pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+  } else if (collect)
     hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
   else
@@ -299,17 +341,17 @@ static hipError_t wide_t(hipStream_t s, bool collect, const SearchPlan& pl, cons
   return hipGetLastError();
 }
 
-hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, const SearchPlan& pl,
+hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, bool s3, const SearchPlan& pl,
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
                               const SearchWs& ws) {
   const bool l2 = metric == EF_METRIC_L2;
   switch (kp) {
     case 256:
-      return l2 ? wide_t<256, EF_METRIC_L2>(s, collect, pl, qpad, G, aux, n, bpad, ws)
-                : wide_t<256, EF_METRIC_COSINE>(s, collect, pl, qpad, G, aux, n, bpad, ws);
+      return l2 ? wide_t<256, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws)
+                : wide_t<256, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws);
     case 512:
-      return l2 ? wide_t<512, EF_METRIC_L2>(s, collect, pl, qpad, G, aux, n, bpad, ws)
-                : wide_t<512, EF_METRIC_COSINE>(s, collect, pl, qpad, G, aux, n, bpad, ws);
+      return l2 ? wide_t<512, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws)
+                : wide_t<512, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws);
     default:
       return hipErrorInvalidValue;
   }

@@ -74,14 +74,12 @@ def test_split_near_ties_below_bf16_resolution(split, k):
     n, b = 5000, 256
     g = rng.standard_normal((n, k)).astype(np.float32)
     q = rng.standard_normal((b, k)).astype(np.float32)
-    want = np.empty(b, np.int64)
     for i in range(b):
         d = rng.standard_normal(k).astype(np.float32) * 0.5
         lo, hi = rng.choice(n, 2, replace=False)
         lo, hi = min(lo, hi), max(lo, hi)
         g[lo] = q[i] + d
         g[hi] = q[i] + d * np.float32(1 - 2e-6)  # closer by ~4e-6 relative
-        want[i] = hi
     # exact fp64 winners (the planted pairs can collide with each other's rows)
     want = orc.l2_argmin(q, g)[0]
     k32, k3 = _keys_both(split, g, q, "l2")
@@ -135,10 +133,29 @@ def test_split_planted_large(split):
     np.testing.assert_array_equal(k3c, k32c)
 
 
-def test_split_option_ignored_for_wide(split):
-    """k > 128 keeps the fp32 wide kernels under the option (same keys)."""
-    rng = np.random.default_rng(3)
-    g = rng.standard_normal((3000, 300)).astype(np.float32)
-    q = rng.standard_normal((300, 300)).astype(np.float32)
+@pytest.mark.parametrize("k", [256, 300, 512])
+def test_split_wide_keys_equal_fp32(split, k):
+    """k > 128: the wide kernel streams split probes and split gallery slices."""
+    rng = np.random.default_rng(3 + k)
+    g = rng.standard_normal((3001, k)).astype(np.float32)
+    q = rng.standard_normal((1100, k)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        k32, k3 = _keys_both(split, g, q, metric)
+        np.testing.assert_array_equal(k3, k32)
+
+
+@pytest.mark.parametrize("k", [256, 512])
+def test_split_wide_near_ties(split, k):
+    rng = np.random.default_rng(17 + k)
+    n, b = 4000, 300
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    q = rng.standard_normal((b, k)).astype(np.float32)
+    for i in range(b):
+        d = rng.standard_normal(k).astype(np.float32) * 0.5
+        lo, hi = sorted(rng.choice(n, 2, replace=False))
+        g[lo] = q[i] + d
+        g[hi] = q[i] + d * np.float32(1 - 2e-6)
+    want = orc.l2_argmin(q, g)[0]
     k32, k3 = _keys_both(split, g, q, "l2")
     np.testing.assert_array_equal(k3, k32)
+    np.testing.assert_array_equal((k3 & 0xFFFFFFFF).astype(np.int64), want)
