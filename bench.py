@@ -523,8 +523,10 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 recognition line")
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
     ap.add_argument("--gallery", type=int, default=0, help="override the gallery size (per-rank studies)")
-    ap.add_argument("--search", default="fp32", choices=["fp32", "split_bf16"],
-                    help="headline gallery-scan arithmetic; the other one is timed as a side leg")
+    ap.add_argument("--search", default=None, choices=["fp32", "split_bf16"],
+                    help="headline gallery-scan arithmetic (default: fp32, the north star's; split_bf16 for "
+                         "config 5, whose bf16-MFMA + fp32-accumulate arithmetic it is); the other one is timed "
+                         "as a side leg")
     ap.add_argument("--no-split", action="store_true", help="skip the side leg of the other scan arithmetic")
     args = ap.parse_args()
 
@@ -599,7 +601,7 @@ def main():
         eng.timing(False)
         return reps, eng.timing_get("search"), eng.timing_get("project")
 
-    split_main = args.search == "split_bf16"
+    split_main = (args.search or ("split_bf16" if args.config == "c5" else "fp32")) == "split_bf16"
     eng.set_option("search_split_bf16", int(split_main))
     reps, (s_ms, s_n), (p_ms, p_n) = timed(step)
     el = float(np.median(reps))
