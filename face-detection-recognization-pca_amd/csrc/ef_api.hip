@@ -75,7 +75,7 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
     EF_HIP(c, launch_keys_none(c->stream, keys_dev, b, match_dev), "keys");
     return EF_OK;
   }
-  const SearchPlan pl = search_plan(bpad, c->n_gallery, c->g_kp);
+  const SearchPlan pl = search_plan(bpad, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
   // workspace carve-out (16-byte aligned pieces)
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t nkb = al((size_t)pl.nchunks * bpad * 8), nb2 = al((size_t)pl.nchunks * bpad * 4);

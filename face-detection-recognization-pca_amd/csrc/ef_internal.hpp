@@ -147,7 +147,7 @@ void timer_begin(ef_ctx* c, int kernel, TimerEvt* t);
 void timer_end(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
-SearchPlan search_plan(int64_t bpad, int64_t n, int kp);
+SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3);
 // G3: split-bf16 copy of G (EF_OPT_SEARCH_SPLIT_BF16) or null for the fp32 kernels; Q3: scratch
 // [bpad][kp] for the split probes (kp > 128 with G3 only)
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad, float* Q3,

@@ -616,21 +616,24 @@ __global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ x, i
 }
 
 // ------------------------------------------------------------------------ launchers
-SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
+SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3) {
   SearchPlan pl;
   const bool wide = kp > 128;
-  pl.n_ptiles = (int)(bpad / (wide ? kWideProbeTile : kSearchProbeTile));
-  const int64_t rows_per_tile = wide ? kWideRowTile : TG;
+  const bool w3 = wide && s3;  // split-bf16 wide kernel: 256 x 256 tiles, one workgroup per CU
+  pl.n_ptiles = (int)(bpad / (w3 ? kWide3ProbeTile : wide ? kWideProbeTile : kSearchProbeTile));
+  const int64_t rows_per_tile = w3 ? kWide3RowTile : wide ? kWideRowTile : TG;
   const int64_t tiles = (n + rows_per_tile - 1) / rows_per_tile;
   // ~512 workgroups = one resident wave of them (2 per CU): every chunk is swept by a
   // workgroup that starts at launch, so there is no tail round (measured: 90.1 % vs 89.6 %
   // at 1M rows, 82 % vs 80.5 % at 125k rows for 2048); the chunk count is a multiple of 8
   // so the XCD remap is a bijection.  EF_SEARCH_WGS overrides (experiments).
 #ifdef EF_DIAGNOSTICS
-  static const int64_t target = [] { const char* e = getenv("EF_SEARCH_WGS"); return e ? atoll(e) : 512; }();
+  static const int64_t target0 = [] { const char* e = getenv("EF_SEARCH_WGS"); return e ? atoll(e) : 512; }();
+  int64_t target = target0;
 #else
-  constexpr int64_t target = 512;
+  int64_t target = 512;
 #endif
+  if (w3) target = 256;
   int64_t want = (target + pl.n_ptiles - 1) / pl.n_ptiles;
   if (want > tiles) want = tiles;
   if (want < 1) want = 1;
@@ -642,13 +645,16 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp) {
   // at C5 = 8 MiB > 4 MiB L2: 27x the gallery bytes measured).  Deal blocks of 8 probe
   // tiles x cblk chunks to each XCD instead: 2 MiB of probes stay L2-resident and each
   // chunk is read by n_ptiles / 8 XCDs.
+  // The split-bf16 wide kernel's probe tiles are 256 x KP x 4 B (512 KiB at KP = 512): 4
+  // of them per XCD keep 2 MiB of probes L2-resident.
+  const int pb = w3 ? 4 : 8;
   pl.pblk = pl.n_ptiles;
   pl.cblk = 1;
-  if (wide && pl.n_ptiles % 8 == 0 && pl.n_ptiles > 8) {
+  if (wide && pl.n_ptiles % pb == 0 && pl.n_ptiles > pb) {
     const int64_t per_xcd = (int64_t)pl.nchunks * pl.n_ptiles / 8;
-    if (per_xcd % 8 == 0 && pl.nchunks % (per_xcd / 8) == 0) {
-      pl.pblk = 8;
-      pl.cblk = (int)(per_xcd / 8);
+    if (per_xcd % pb == 0 && pl.nchunks % (per_xcd / pb) == 0) {
+      pl.pblk = pb;
+      pl.cblk = (int)(per_xcd / pb);
     }
   }
   return pl;

@@ -55,6 +55,8 @@ __device__ __forceinline__ double score64(const float* __restrict__ q, const flo
 // Wide search (KP in {256, 512}): probes streamed through LDS with the gallery.
 constexpr int kWideRowTile = 128;    // gallery rows per tile
 constexpr int kWideProbeTile = 128;  // probes per workgroup
+constexpr int kWide3RowTile = 256;    // split-bf16 wide kernel: gallery rows per tile
+constexpr int kWide3ProbeTile = 256;  // split-bf16 wide kernel: probes per workgroup
 // s3: qpad and G are the split-bf16 copies (split-bf16 scan)
 hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, bool s3, const SearchPlan& pl,
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,

@@ -43,10 +43,7 @@ __device__ __forceinline__ bf16x8w as_bf16x8w(const float4& v) {
   return r;
 }
 
-// S3: qpad and G are the split-bf16 copies (ef_search.hip: per 8 elements 16 B of hi, 16 B
-// of lo) — same bytes per row, so the slice DMA is unchanged; each 32-k slice is two
-// 16-k fragments (chunks 4h + 2i = hi, 4h + 2i + 1 = lo of lane half h), 3 bf16 MFMAs each.
-template <int KP, int METRIC, bool COLLECT, bool S3 = false>
+template <int KP, int METRIC, bool COLLECT>
 __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
     int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
@@ -223,26 +220,6 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     }
     const float* sg = smem + buf * 2 * WSL;
     const float* sq = sg + WSL;
-    if constexpr (S3) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int ph = ((h * 4 + 2 * i) ^ sw) * 4, pl = ((h * 4 + 2 * i + 1) ^ sw) * 4;
-        const bf16x8w bh = as_bf16x8w(*reinterpret_cast<const float4*>(sq + (wave * 32 + c32) * WBK + ph));
-        const bf16x8w bl = as_bf16x8w(*reinterpret_cast<const float4*>(sq + (wave * 32 + c32) * WBK + pl));
-        bf16x8w ah[4], al[4];
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-          ah[rb] = as_bf16x8w(*reinterpret_cast<const float4*>(sg + (rb * 32 + c32) * WBK + ph));
-          al[rb] = as_bf16x8w(*reinterpret_cast<const float4*>(sg + (rb * 32 + c32) * WBK + pl));
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bh, acc[rb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bl, acc[rb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[rb], bh, acc[rb], 0, 0, 0);
-      }
-    } else
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pch = ((h * 4 + j) ^ sw) * 4;  // lane half h owns k in [16h, 16h + 16) of the slice
@@ -318,6 +295,295 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-bf16 wide scan, 256 gallery rows x 256 probes per workgroup (8 waves, 1 per CU).
+// The split scan does 16/3 x the arithmetic of the fp32 one per LDS byte, so the 128 x 128
+// tiles above would be bound by the L2 -> LDS stream (~25 B/clk/CU measured at C5); a
+// 256 x 256 tile halves the streamed bytes per MFMA.  Wave w owns probes 64(w & 3) ..+64
+// (two 32-probe B blocks) against rows 128(w >> 2) ..+128 (four 32-row A blocks): 8
+// accumulator chains, each A fragment feeding both probe blocks (24 MFMAs per 12
+// ds_read_b128 per 16 k).  The two row halves' running top-2 are merged through LDS at the
+// end.  Same SearchWs contract as search_wide_kernel.
+constexpr int W3R = 256;          // gallery rows per tile
+constexpr int W3P = 256;          // probes per workgroup
+constexpr int W3SL = W3R * WBK;   // floats per gallery slice (= per probe slice), 32 KiB
+static_assert(W3R == kWide3RowTile && W3P == kWide3ProbeTile, "plan and kernel tiles agree");
+
+template <int KP, int METRIC, bool COLLECT>
+__global__ __launch_bounds__(512, 1) void search_wide3_kernel(
+    const float* __restrict__ q3, const float* __restrict__ G3, const float* __restrict__ aux, int64_t n,
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
+  constexpr int NS = KP / WBK;
+  __shared__ __attribute__((aligned(16))) float smem[4 * W3SL + 2 * W3R];
+
+  const int total = gridDim.x;  // host guarantees total % 8 == 0
+  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+  const int bsz = cblk * pblk;
+  const int blk = lin / bsz, rr = lin - blk * bsz;
+  const int nbp = n_ptiles / pblk;
+  const int gc = (blk / nbp) * cblk + rr / pblk;
+  const int pt = (blk % nbp) * pblk + rr % pblk;
+
+  int n_amb = 0;
+  if constexpr (COLLECT) {
+    n_amb = *ws.amb_count;
+    if (pt * W3P >= n_amb) return;  // uniform: nothing queued for this probe tile
+  }
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int c32 = lane & 31;
+  const int pg = wave & 3, rh = wave >> 2;  // probe group (64 probes), row half (128 rows)
+
+  const int64_t tiles_total = (n + W3R - 1) / W3R;
+  const int64_t t0 = (int64_t)gc * tiles_per_chunk;
+  const int64_t t1 = t0 + tiles_per_chunk < tiles_total ? t0 + tiles_per_chunk : tiles_total;
+  int64_t sl0[2];  // this lane's probe slots
+  sl0[0] = (int64_t)pt * W3P + 64 * pg + c32;
+  sl0[1] = sl0[0] + 32;
+
+  if (t0 >= t1) {
+    if constexpr (!COLLECT) {
+      if (h == 0 && rh == 0) {
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {
+          ws.part_key[(int64_t)gc * bpad + sl0[pb]] = LLONG_MAX;
+          ws.part_b2[(int64_t)gc * bpad + sl0[pb]] = __builtin_inff();
+        }
+      }
+    }
+    return;
+  }
+
+  // DMA geometry (as search_wide_kernel): a slice is 32 pieces of 1 KiB (8 rows x 128 B)
+  // for the gallery and 32 for the probes; wave w issues pieces 4w..4w+3 of each.
+  const int prow = lane >> 3;
+  unsigned goff[4], qoff[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int slot = pt * W3P + (wave * 4 + jj) * 8 + prow;
+    int qrow = slot;
+    if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
+    const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 7)) * 16);
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
+  }
+  float thr[2] = {-__builtin_inff(), -__builtin_inff()};
+  if constexpr (COLLECT) {
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb)
+      if (sl0[pb] < n_amb) thr[pb] = ws.thr[sl0[pb]];
+  }
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qoff[jj]));
+  asm volatile("" ::"v"(thr[0]), "v"(thr[1]));
+
+  const unsigned lds_base = lds_addr(smem);
+  const int64_t n_it = (t1 - t0) * NS;
+  auto issue = [&](int64_t it, int buf) {
+    const int64_t t = t0 + it / NS;
+    const int sl = (int)(it % NS);
+    const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
+    const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * KP + sl * WBK);
+    const unsigned long long qb = (unsigned long long)(size_t)(q3 + sl * WBK);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = wave * 4 + jj;
+      unsigned go = goff[jj];
+      if (nrem < W3R) {  // tail tile: rows past the end re-read the last row (masked later)
+        const unsigned row = go / (KP * 4);
+        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
+      }
+      glds16s(go, gb, lds_base + (unsigned)((buf * 2 * W3SL + j * 256) * 4));
+      glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * W3SL + W3SL + j * 256) * 4));
+    }
+    if (sl == 0 && wave == 0) {  // the tile's ||g||^2 (L2) or 1/||g|| (cosine)
+      const unsigned long long ab = (unsigned long long)(size_t)(aux + t * W3R);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 64 * q + lane;
+        const unsigned ao = r < nrem ? (unsigned)r * 4 : (unsigned)(nrem - 1) * 4;
+        glds4s(ao, ab, lds_base + (unsigned)((4 * W3SL + ((t - t0) & 1) * W3R + 64 * q) * 4));
+      }
+    }
+  };
+
+  const float INF = __builtin_inff();
+  float b1[2] = {INF, INF}, b2[2] = {INF, INF};
+  int i1[2] = {INT_MAX, INT_MAX};
+  auto consume = [&](const f32x16& v, int rowbase, int pb) {
+    if constexpr (COLLECT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (v[r] <= thr[pb]) {
+          const int pos = atomicAdd(&ws.cand_cnt[sl0[pb]], 1);
+          if (pos < kCandMax) ws.cand[sl0[pb] * kCandMax + pos] = rowbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+        }
+      }
+    } else {
+      float mn = v[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mn = fminf(mn, v[r]);
+      if (!__any(mn < b2[pb])) return;  // exact skip (ef_search.hip consume)
+      float m1 = v[0], m2 = INF;
+      int ir = 0;
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        const bool lt = v[r] < m1;
+        m2 = __builtin_amdgcn_fmed3f(m1, v[r], m2);
+        ir = lt ? r : ir;
+        m1 = lt ? v[r] : m1;
+      }
+      const bool lt = m1 < b1[pb];
+      b2[pb] = lt ? fminf(b1[pb], m2) : fminf(b2[pb], m1);
+      i1[pb] = lt ? rowbase + (ir & 3) + 8 * (ir >> 2) + 4 * h : i1[pb];
+      b1[pb] = lt ? m1 : b1[pb];
+    }
+  };
+
+  issue(0, 0);
+  dma_wait_all();
+  __syncthreads();
+
+  const int sw = (c32 >> 1) & 7;  // swizzle key of rows 32x + c32
+  f32x16 acc[4][2];
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int buf = (int)(it & 1);
+    const int sl = (int)(it % NS);
+    const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
+    if (it + 1 < n_it) issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+    if (sl == 0) {
+      // L2: start from -||g||^2 / 2 and accumulate q.g (-2 acc = ||g||^2 - 2 q.g); cosine: 0
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        f32x16 a = {};
+        if constexpr (METRIC == EF_METRIC_L2) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 x = *reinterpret_cast<const float4*>(sAux + rb * 32 + 8 * q + 4 * h);
+            a[4 * q] = -0.5f * x.x;
+            a[4 * q + 1] = -0.5f * x.y;
+            a[4 * q + 2] = -0.5f * x.z;
+            a[4 * q + 3] = -0.5f * x.w;
+          }
+        }
+        acc[rb][0] = a;
+        acc[rb][1] = a;
+      }
+    }
+    const float* sg = smem + buf * 2 * W3SL + (128 * rh + c32) * WBK;
+    const float* sq = smem + buf * 2 * W3SL + W3SL + (64 * pg + c32) * WBK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ph = ((h * 4 + 2 * i) ^ sw) * 4, pl = ((h * 4 + 2 * i + 1) ^ sw) * 4;
+      bf16x8w bh[2], bl[2];
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        bh[pb] = as_bf16x8w(*reinterpret_cast<const float4*>(sq + pb * 32 * WBK + ph));
+        bl[pb] = as_bf16x8w(*reinterpret_cast<const float4*>(sq + pb * 32 * WBK + pl));
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const bf16x8w ah = as_bf16x8w(*reinterpret_cast<const float4*>(sg + rb * 32 * WBK + ph));
+        const bf16x8w al = as_bf16x8w(*reinterpret_cast<const float4*>(sg + rb * 32 * WBK + pl));
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[pb], acc[rb][pb], 0, 0, 0);
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[pb], acc[rb][pb], 0, 0, 0);
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[pb], acc[rb][pb], 0, 0, 0);
+        }
+      }
+    }
+    if (sl == NS - 1) {
+      const int64_t t = t0 + it / NS;
+      const int tbase = (int)(t * W3R) + 128 * rh;
+      const bool tail = (t + 1) * W3R > n;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+#pragma unroll
+        for (int pb = 0; pb < 2; ++pb) {
+          if constexpr (METRIC == EF_METRIC_L2) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rb][pb][r] *= -2.f;
+          } else {  // -(q.g) * (1/||g||)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 x = *reinterpret_cast<const float4*>(sAux + rb * 32 + 8 * q + 4 * h);
+              acc[rb][pb][4 * q] *= -x.x;
+              acc[rb][pb][4 * q + 1] *= -x.y;
+              acc[rb][pb][4 * q + 2] *= -x.z;
+              acc[rb][pb][4 * q + 3] *= -x.w;
+            }
+          }
+          if (tail) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (tbase + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h >= n) acc[rb][pb][r] = INF;
+          }
+          consume(acc[rb][pb], tbase + rb * 32, pb);  // blocks in row order (tie rule)
+        }
+      }
+    }
+    dma_wait_all();
+    __syncthreads();  // slice it+1 landed; everyone is done reading buffer buf
+  }
+
+  if constexpr (!COLLECT) {
+    // lane halves (same probe, disjoint rows), then the two row halves through LDS
+    float* xb = smem;  // [4 pg][2 pb][32] x (b1, b2, i1); the loop's last barrier freed LDS
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      const float ob1 = __shfl_xor(b1[pb], 32);
+      const int oi1 = __shfl_xor(i1[pb], 32);
+      const float ob2 = __shfl_xor(b2[pb], 32);
+      const bool other = ob1 < b1[pb] || (ob1 == b1[pb] && oi1 < i1[pb]);
+      const float lose = other ? b1[pb] : ob1;
+      b2[pb] = fminf(fminf(b2[pb], ob2), lose);
+      if (other) { b1[pb] = ob1; i1[pb] = oi1; }
+      if (rh == 1 && h == 0) {
+        const int o = ((pg * 2 + pb) * 32 + c32) * 3;
+        xb[o] = b1[pb];
+        xb[o + 1] = b2[pb];
+        xb[o + 2] = __int_as_float(i1[pb]);
+      }
+    }
+    __syncthreads();
+    if (rh == 0 && h == 0) {
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        const int o = ((pg * 2 + pb) * 32 + c32) * 3;
+        const float ob1 = xb[o], ob2 = xb[o + 1];
+        const int oi1 = __float_as_int(xb[o + 2]);
+        const bool other = ob1 < b1[pb] || (ob1 == b1[pb] && oi1 < i1[pb]);
+        const float lose = other ? b1[pb] : ob1;
+        b2[pb] = fminf(fminf(b2[pb], ob2), lose);
+        if (other) { b1[pb] = ob1; i1[pb] = oi1; }
+        const int64_t po = (int64_t)gc * bpad + sl0[pb];
+        ws.part_key[po] = i1[pb] == INT_MAX ? LLONG_MAX : pack_key(b1[pb], (unsigned)i1[pb]);
+        ws.part_b2[po] = b2[pb];
+      }
+    }
+  }
+}
+
+template <int KP, int M>
+static hipError_t wide3_t(hipStream_t s, bool collect, const SearchPlan& pl, const float* q3, const float* G3,
+                          const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
+  const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
+  if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
+      (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0 || bpad % W3P != 0)
+    return hipErrorInvalidValue;  // the block deal would not be a bijection
+  if (collect)
+    hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+  else
+    hipLaunchKernelGGL((search_wide3_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+  return hipGetLastError();
+}
+
 template <int KP, int M>
 static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan& pl, const float* qpad,
                          const float* G, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
@@ -325,14 +591,8 @@ static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan&
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
-  if (s3) {
-    if (collect)
-      hipLaunchKernelGGL((search_wide_kernel<KP, M, true, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                         pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
-    else
-      hipLaunchKernelGGL((search_wide_kernel<KP, M, false, true>), grid, block, 0, s, qpad, G, aux, n,
-                         pl.n_ptiles, pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
-  } else if (collect)
+  if (s3) return wide3_t<KP, M>(s, collect, pl, qpad, G, aux, n, bpad, ws);  // plan from search_plan(.., true)
+  if (collect)
     hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
   else

@@ -159,3 +159,15 @@ def test_split_wide_near_ties(split, k):
     k32, k3 = _keys_both(split, g, q, "l2")
     np.testing.assert_array_equal(k3, k32)
     np.testing.assert_array_equal((k3 & 0xFFFFFFFF).astype(np.int64), want)
+
+
+@pytest.mark.parametrize("b", [1024, 2048, 4096])
+def test_split_wide_xcd_deal(split, b):
+    """Batches of >= 8 split probe tiles take the blocked (4 probe tiles x cblk chunks)
+    XCD deal of the 256 x 256 split wide kernel; ragged last gallery tile."""
+    rng = np.random.default_rng(b)
+    g = rng.standard_normal((5003, 512)).astype(np.float32)
+    q = rng.standard_normal((b, 512)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        k32, k3 = _keys_both(split, g, q, metric)
+        np.testing.assert_array_equal(k3, k32)
