@@ -528,6 +528,8 @@ def main():
                          "config 5, whose bf16-MFMA + fp32-accumulate arithmetic it is); the other one is timed "
                          "as a side leg")
     ap.add_argument("--no-split", action="store_true", help="skip the side leg of the other scan arithmetic")
+    ap.add_argument("--split-opt", type=int, default=1, choices=[1, 2],
+                    help="EF_OPT_SEARCH_SPLIT_BF16 value of the split scan (2: the 32x32x16 kernel at k = 128)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -602,7 +604,8 @@ def main():
         return reps, eng.timing_get("search"), eng.timing_get("project")
 
     split_main = (args.search or ("split_bf16" if args.config == "c5" else "fp32")) == "split_bf16"
-    eng.set_option("search_split_bf16", int(split_main))
+    split_val = args.split_opt
+    eng.set_option("search_split_bf16", split_val if split_main else 0)
     reps, (s_ms, s_n), (p_ms, p_n) = timed(step)
     el = float(np.median(reps))
 
@@ -624,14 +627,14 @@ def main():
         # the other scan precision on the same step: split-bf16 when the headline is fp32
         # (and vice versa); its keys must equal the headline's bit for bit
         eng.set_stream(stream.cuda_stream)
-        eng.set_option("search_split_bf16", int(not split_main))
+        eng.set_option("search_split_bf16", 0 if split_main else split_val)
         keys2 = torch.empty_like(keys)
 
         def step2():
             shard.recognize_keys(P_dev, args.metric, keys=keys2)
 
         reps2, (s2_ms, s2_n), _ = timed(step2)
-        eng.set_option("search_split_bf16", int(split_main))
+        eng.set_option("search_split_bf16", split_val if split_main else 0)
         split_leg = {"scan": "split_bf16" if not split_main else "fp32", "reps": reps2,
                      "search_avg_ms": s2_ms / max(s2_n, 1), "launches": s2_n,
                      "keys_identical": bool(torch.equal(keys2, keys))}

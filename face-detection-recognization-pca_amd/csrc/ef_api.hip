@@ -566,7 +566,8 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
       c->opt_jpeg_chunk_bits = value;
       return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16:
-      c->opt_search_split_bf16 = value != 0;
+      if (value < 0 || value > 2) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1 or 2");
+      c->opt_search_split_bf16 = value;
       return EF_OK;
     default:
       return set_err(c, EF_E_INVALID, "ef_set_option: unknown option " + std::to_string(option));

@@ -190,9 +190,10 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
 #define EF_OPT_TM_INT64_SUMS 4   /* 1: int64 integral images in the template localiser [0: auto] */
 #define EF_OPT_HAAR_ORDERED 5    /* 1: sequential stage sums even when reassociation is exact [0] */
 #define EF_OPT_JPEG_CHUNK_BITS 6 /* entropy-decode chunk per GPU thread, bits (multiple of 32) [0: auto] */
-#define EF_OPT_SEARCH_SPLIT_BF16 7 /* 1: k <= 128 gallery scans on bf16 MFMA with split (hi + lo) fp32
-                                      operands and a widened error bound; identities and scores are
-                                      still fp64-resolved, so results equal the fp32 scan's [0] */
+#define EF_OPT_SEARCH_SPLIT_BF16 7 /* 1: gallery scans on bf16 MFMA with split (hi + lo) fp32 operands
+                                      and a widened error bound; identities and scores are still
+                                      fp64-resolved, so results equal the fp32 scan's [0]; 2: the same
+                                      with the 32x32x16 kernel at k in (64, 128] (comparison) */
 int ef_set_option(ef_ctx* ctx, int32_t option, int64_t value);
 int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 

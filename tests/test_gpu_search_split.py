@@ -171,3 +171,25 @@ def test_split_wide_xcd_deal(split, b):
     for metric in ("l2", "cosine"):
         k32, k3 = _keys_both(split, g, q, metric)
         np.testing.assert_array_equal(k3, k32)
+
+
+@pytest.mark.parametrize("k", [100, 128])
+def test_split_kernel_shapes_agree(split, k):
+    """k in (64, 128]: the default 16x16x32 split kernel and the 32x32x16 one (option 2)
+    return the fp32 scan's keys, on random probes and on sub-bf16 near-ties."""
+    rng = np.random.default_rng(k + 5)
+    n, b = 7001, 700
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    q = rng.standard_normal((b, k)).astype(np.float32)
+    for i in range(0, b, 2):
+        d = rng.standard_normal(k).astype(np.float32) * 0.5
+        lo, hi = sorted(rng.choice(n, 2, replace=False))
+        g[lo] = q[i] + d
+        g[hi] = q[i] + d * np.float32(1 - 2e-6)
+    for metric in ("l2", "cosine"):
+        k32, k16 = _keys_both(split, g, q, metric)
+        split.set_option("search_split_bf16", 2)
+        k3232 = split.search_keys(q, metric)
+        np.testing.assert_array_equal(k16, k32)
+        np.testing.assert_array_equal(k3232, k32)
+    assert split.get_option("search_split_bf16") == 2
