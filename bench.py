@@ -639,6 +639,25 @@ def main():
                      "search_avg_ms": s2_ms / max(s2_n, 1), "launches": s2_n,
                      "keys_identical": bool(torch.equal(keys2, keys))}
 
+    tol = None
+    if world == 1 and precision == "bf16":
+        # the bf16 projection's tolerance vs fp32 — max relative feature
+        # error and the argmin agreement rate of the two projections on the same step
+        eng.set_stream(stream.cuda_stream)
+        f16 = torch.empty((bsz, k), dtype=torch.float32, device=dev)
+        f32 = torch.empty_like(f16)
+        k16 = eng.recognize_keys(P_dev, args.metric, feats=f16).clone()
+        eng.set_model(mean, W, precision="fp32")
+        k32 = eng.recognize_keys(P_dev, args.metric, feats=f32).clone()
+        eng.set_model(mean, W, precision=precision)
+        torch.cuda.synchronize(dev)
+        rel = ((f16 - f32).norm(dim=1) / f32.norm(dim=1).clamp_min(1e-30)).max().item()
+        tol = {"features_max_rel_err_l2": rel,
+               "features_max_abs_err_over_max_abs": ((f16 - f32).abs().max() / f32.abs().max()).item(),
+               "argmin_agreement_bf16_vs_fp32_projection": float(((k16 & 0xFFFFFFFF) == (k32 & 0xFFFFFFFF))
+                                                                 .float().mean().item()),
+               "stated_bound": "|f_bf16 - f_fp32| <= 2^-8 sum|p - round(mu)||W| per feature (tests/test_gpu_project.py)"}
+
     if rank == 0:
         ms_step = el / args.steps * 1e3
         value = bsz * args.steps / el
@@ -698,6 +717,8 @@ def main():
             "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
             "check": {"planted_match": match},
         }
+        if tol:
+            rec["bf16_projection_tolerance"] = tol
         if split_leg:
             el2 = float(np.median(split_leg["reps"]))
             rec["scan_" + split_leg["scan"]] = {
