@@ -258,7 +258,10 @@ void ef_destroy(ef_ctx* c) {
                     &c->G3, &c->q3, &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
                     &c->p_stage, &c->proj_part, &c->feats_dev, &c->jpeg_ws, &c->jpeg_out, &c->jpeg_rows};
   for (DevBuf* b : bufs) release(*b);
-  if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
+  for (int i = 0; i < 2; ++i) {
+    if (c->jpeg_pinned[i]) (void)hipHostFree(c->jpeg_pinned[i]);
+    if (c->jpeg_up_done[i]) (void)hipEventDestroy(c->jpeg_up_done[i]);
+  }
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);
@@ -296,9 +299,11 @@ int ef_trim(ef_ctx* c) {
   release(c->jpeg_ws);
   release(c->jpeg_out);
   release(c->jpeg_rows);
-  if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
-  c->jpeg_pinned = nullptr;
-  c->jpeg_pinned_bytes = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (c->jpeg_pinned[i]) (void)hipHostFree(c->jpeg_pinned[i]);
+    c->jpeg_pinned[i] = nullptr;
+    c->jpeg_pinned_bytes[i] = 0;
+  }
   return EF_OK;
 }
 
@@ -565,6 +570,10 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
         return set_err(c, EF_E_INVALID, "EF_OPT_JPEG_CHUNK_BITS must be 0 or a multiple of 32 up to 2^24");
       c->opt_jpeg_chunk_bits = value;
       return EF_OK;
+    case EF_OPT_JPEG_PART_FILES:
+      if (value < 1) return set_err(c, EF_E_INVALID, "EF_OPT_JPEG_PART_FILES must be >= 1");
+      c->opt_jpeg_part_files = value;
+      return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16:
       if (value < 0 || value > 2) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1 or 2");
       c->opt_search_split_bf16 = value;
@@ -584,6 +593,7 @@ int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
     case EF_OPT_HAAR_ORDERED: *value = c->opt_haar_ordered; return EF_OK;
     case EF_OPT_JPEG_CHUNK_BITS: *value = c->opt_jpeg_chunk_bits; return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16: *value = c->opt_search_split_bf16; return EF_OK;
+    case EF_OPT_JPEG_PART_FILES: *value = c->opt_jpeg_part_files; return EF_OK;
     default: return EF_E_INVALID;
   }
 }

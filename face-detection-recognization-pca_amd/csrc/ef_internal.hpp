@@ -75,6 +75,7 @@ struct ef_ctx {
   int64_t opt_haar_ordered = 0;
   int64_t opt_jpeg_chunk_bits = 0;
   int64_t opt_search_split_bf16 = 0;
+  int64_t opt_jpeg_part_files = 8192;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -115,8 +116,11 @@ struct ef_ctx {
 
   // JPEG decode (ef_jpeg.hip): device workspace, host-output staging, pinned upload buffer
   ef::DevBuf jpeg_ws, jpeg_out, jpeg_rows;
-  void* jpeg_pinned = nullptr;
-  size_t jpeg_pinned_bytes = 0;
+  // two pinned upload slots: the ingest stages part i + 1 on a host thread while part i
+  // decodes; each slot's event marks the end of the upload that last read it
+  void* jpeg_pinned[2] = {nullptr, nullptr};
+  size_t jpeg_pinned_bytes[2] = {0, 0};
+  hipEvent_t jpeg_up_done[2] = {nullptr, nullptr};
   int jpeg_rounds = 0;  // synchronisation rounds of the last decode (diagnostics)
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare

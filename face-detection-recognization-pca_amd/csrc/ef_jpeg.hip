@@ -1267,57 +1267,80 @@ void make_chunks(Batch& B, int64_t opt_bits) {
   }
 }
 
-// Upload, entropy-decode, IDCT and colour-convert a built batch into dout (device), each
-// image at its out_off.  Stream-ordered on ctx's stream.
-int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* dout) {
-  hipStream_t s = c->stream;
+// A built batch staged for upload: one pinned slot holds [destuffed words | images |
+// Huffman tables | quant tables | segments | IDCT runs | pixel starts]; the chunk table
+// (known only after destuffing) is uploaded from B.chunk_seg.
+struct Staged {
+  int slot = 0;
+  char* h = nullptr;
+  size_t o_words = 0, o_imgs = 0, o_pool = 0, o_q = 0, o_seg = 0, o_bs = 0, o_ic = 0, o_ps = 0, o_cseg = 0;
+  size_t pin_need = 0;
+};
+
+// Host half of a decode: size / allocate pinned slot `slot` (waiting for the upload that last
+// read it), destuff the entropy segments into it, copy the tables, cut the chunks.  Touches
+// only this slot and B, so it may run on a host thread while another slot's batch decodes.
+// Returns EF_OK, or an error code with the message in *err (the caller records it).
+int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_t* offsets, Staged& S,
+                std::string* err, int64_t chunk_bits = 0) {
   StageTimer tm;
-  // layout: one pinned upload [destuffed words | images | Huffman tables | quant tables |
-  // segments | chunk->segment | IDCT runs | pixel starts] at the front of the device
-  // workspace, then device-only [chunk states S, E x2 | counts | block starts | DC preds |
-  // flag | coefficients | sample planes]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t off = 0;
-  const size_t o_words = off; off += al((size_t)B.words * 4 + 16);
-  const size_t o_imgs = off; off += al(B.imgs.size() * sizeof(JImage));
-  const size_t o_pool = off; off += al(std::max<size_t>(B.T.huff.size(), 1) * sizeof(HuffTab));
-  const size_t o_q = off; off += al(std::max<size_t>(B.T.quant.size(), 1) * 2);
-  const size_t o_seg = off; off += al(B.segs.size() * sizeof(JSeg));
-  const size_t o_bs = off; off += al(B.block_start.size() * 8);
-  const size_t o_ic = off; off += al(B.ic.size() * 4);
-  const size_t o_ps = off; off += al(B.row_start.size() * 8);
-  const size_t o_cseg = off;  // chunk table last: its size is known only after destuffing
-  // the previous call's upload may still be reading the pinned buffer
-  {
-    const hipError_t e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
+  S.slot = slot;
+  S.o_words = off; off += al((size_t)B.words * 4 + 16);
+  S.o_imgs = off; off += al(B.imgs.size() * sizeof(JImage));
+  S.o_pool = off; off += al(std::max<size_t>(B.T.huff.size(), 1) * sizeof(HuffTab));
+  S.o_q = off; off += al(std::max<size_t>(B.T.quant.size(), 1) * 2);
+  S.o_seg = off; off += al(B.segs.size() * sizeof(JSeg));
+  S.o_bs = off; off += al(B.block_start.size() * 8);
+  S.o_ic = off; off += al(B.ic.size() * 4);
+  S.o_ps = off; off += al(B.row_start.size() * 8);
+  S.o_cseg = off;  // chunk table last: its size is known only after destuffing
+  S.pin_need = off;
+  if (c->jpeg_up_done[slot]) {  // the upload that last read this slot
+    const hipError_t e = hipEventSynchronize(c->jpeg_up_done[slot]);
+    if (e != hipSuccess) { *err = hipGetErrorString(e); return EF_E_HIP; }
   }
-  const size_t pin_need = o_cseg;
-  if (c->jpeg_pinned_bytes < pin_need) {
-    if (c->jpeg_pinned) (void)hipHostFree(c->jpeg_pinned);
-    c->jpeg_pinned = nullptr;
-    c->jpeg_pinned_bytes = 0;
-    const hipError_t e = hipHostMalloc(&c->jpeg_pinned, pin_need + pin_need / 4 + 4096, hipHostMallocDefault);
+  if (c->jpeg_pinned_bytes[slot] < S.pin_need) {
+    if (c->jpeg_pinned[slot]) (void)hipHostFree(c->jpeg_pinned[slot]);
+    c->jpeg_pinned[slot] = nullptr;
+    c->jpeg_pinned_bytes[slot] = 0;
+    const size_t want = S.pin_need + S.pin_need / 4 + 4096;
+    const hipError_t e = hipHostMalloc(&c->jpeg_pinned[slot], want, hipHostMallocDefault);
     if (e != hipSuccess) {
-      c->jpeg_pinned = nullptr;
-      return hip_err(c, e, "hipHostMalloc (jpeg staging)");
+      c->jpeg_pinned[slot] = nullptr;
+      *err = std::string("hipHostMalloc (jpeg staging): ") + hipGetErrorString(e);
+      return EF_E_HIP;
     }
-    c->jpeg_pinned_bytes = pin_need + pin_need / 4 + 4096;
+    c->jpeg_pinned_bytes[slot] = want;
   }
-  char* h = static_cast<char*>(c->jpeg_pinned);
+  char* h = static_cast<char*>(c->jpeg_pinned[slot]);
+  S.h = h;
   tm.mark("pinned");
-  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + o_words));
+  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + S.o_words));
   tm.mark("destuff");
-  make_chunks(B, c->opt_jpeg_chunk_bits);
+  make_chunks(B, c->opt_jpeg_chunk_bits > 0 ? c->opt_jpeg_chunk_bits : chunk_bits);
+  std::memcpy(h + S.o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
+  if (!B.T.huff.empty()) std::memcpy(h + S.o_pool, B.T.huff.data(), B.T.huff.size() * sizeof(HuffTab));
+  if (!B.T.quant.empty()) std::memcpy(h + S.o_q, B.T.quant.data(), B.T.quant.size() * 2);
+  std::memcpy(h + S.o_seg, B.segs.data(), B.segs.size() * sizeof(JSeg));
+  std::memcpy(h + S.o_bs, B.block_start.data(), B.block_start.size() * 8);
+  std::memcpy(h + S.o_ic, B.ic.data(), B.ic.size() * 4);
+  std::memcpy(h + S.o_ps, B.row_start.data(), B.row_start.size() * 8);
+  tm.mark("tables");
+  return EF_OK;
+}
+
+// Device half: upload a staged batch, entropy-decode, IDCT and colour-convert it into dout
+// (device), each image at its out_off.  Stream-ordered on ctx's stream.
+int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
+  hipStream_t s = c->stream;
+  StageTimer tm;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char* h = S.h;
   const int nchunks = (int)B.chunk_seg.size();
-  std::memcpy(h + o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
-  if (!B.T.huff.empty()) std::memcpy(h + o_pool, B.T.huff.data(), B.T.huff.size() * sizeof(HuffTab));
-  if (!B.T.quant.empty()) std::memcpy(h + o_q, B.T.quant.data(), B.T.quant.size() * 2);
-  std::memcpy(h + o_seg, B.segs.data(), B.segs.size() * sizeof(JSeg));
-  std::memcpy(h + o_bs, B.block_start.data(), B.block_start.size() * 8);
-  std::memcpy(h + o_ic, B.ic.data(), B.ic.size() * 4);
-  std::memcpy(h + o_ps, B.row_start.data(), B.row_start.size() * 8);
-  const size_t up_bytes = o_cseg;
+  const size_t up_bytes = S.o_cseg;
+  size_t off = S.o_cseg;
   const size_t o_S = off + al((size_t)nchunks * 4);
   off = o_S;
   off += al((size_t)nchunks * 8);
@@ -1334,9 +1357,15 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
     const int rc = ensure(c, c->jpeg_ws, off);
     if (rc != EF_OK) return rc;
   }
+  if (!c->jpeg_up_done[S.slot]) {
+    const hipError_t e = hipEventCreateWithFlags(&c->jpeg_up_done[S.slot], hipEventDisableTiming);
+    if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
+  }
   char* base = static_cast<char*>(c->jpeg_ws.p);
-  tm.mark("tables");
+  const size_t o_seg = S.o_seg, o_imgs = S.o_imgs, o_pool = S.o_pool, o_words = S.o_words, o_cseg = S.o_cseg;
+  const size_t o_bs = S.o_bs, o_ic = S.o_ic, o_q = S.o_q, o_ps = S.o_ps;
   hipError_t e = hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(c->jpeg_up_done[S.slot], s);
   tm.mark("upload", s, true);
   if (e == hipSuccess)  // pageable; complete before the first round's flag read below
     e = hipMemcpyAsync(base + o_cseg, B.chunk_seg.data(), (size_t)nchunks * 4, hipMemcpyHostToDevice, s);
@@ -1351,13 +1380,13 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   X.chunk_bits = B.chunk_bits;
   X.warm_bits = B.warm_bits;
   X.cps = reinterpret_cast<Checkpoint*>(base + o_cps);
-  long long* S = reinterpret_cast<long long*>(base + o_S);
+  long long* S_ = reinterpret_cast<long long*>(base + o_S);
   long long* E[2] = {reinterpret_cast<long long*>(base + o_E0), reinterpret_cast<long long*>(base + o_E1)};
   int* cnt = reinterpret_cast<int*>(base + o_cnt);
   int* G = reinterpret_cast<int*>(base + o_G);
   int* P = reinterpret_cast<int*>(base + o_P);
   int* flag = reinterpret_cast<int*>(base + o_flag);
-  int* hflag = reinterpret_cast<int*>(h + pin_need);  // in the pinned buffer's slack
+  int* hflag = reinterpret_cast<int*>(h + S.pin_need);  // in the pinned slot's slack
   int max_chunks = 1;
   for (const JSeg& sg : B.segs) max_chunks = std::max(max_chunks, sg.nchunk);
   TimerEvt tev;
@@ -1367,7 +1396,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   const size_t lds_bytes = (size_t)lds_tables * kLookSize * 2;
   int rounds = 0;
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, 0, S, E[1],
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, 0, S_, E[1],
                        E[0], cnt, flag);
     e = hipGetLastError();
   }
@@ -1377,7 +1406,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   for (int r = 1; e == hipSuccess && r <= max_chunks; ++r) {
     e = hipMemsetAsync(flag, 0, 4, s);
     if (e != hipSuccess) break;
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S, E[cur],
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S_, E[cur],
                        E[cur ^ 1], cnt, flag);
     e = hipGetLastError();
     cur ^= 1;
@@ -1391,7 +1420,7 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   if (e == hipSuccess) {
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
                        (int)B.segs.size(), cnt, G, P);
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S, G,
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S_, G,
                        P, reinterpret_cast<short*>(base + o_coef));
     const JImage* d_imgs = X.imgs;
     short* d_coef = reinterpret_cast<short*>(base + o_coef);
@@ -1410,6 +1439,16 @@ int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offset
   tm.mark("kernels", s, true);
   if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   return EF_OK;
+}
+
+
+// Host and device halves in sequence (one slot).
+int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* dout) {
+  Staged S;
+  std::string err;
+  const int rc = stage_batch(c, 0, B, data, offsets, S, &err);
+  if (rc != EF_OK) return set_err(c, rc, "jpeg decode: " + err);
+  return launch_batch(c, B, S, dout);
 }
 
 }  // namespace
@@ -1476,49 +1515,91 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
   (void)hipSetDevice(c->device);
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   const int64_t row = (int64_t)out_h * out_w;
-  for (int32_t a = 0; a < count; a += 65535) {  // ef_preprocess's per-call image limit
-    const int32_t m = std::min<int32_t>(65535, count - a);
-    std::vector<int32_t> st(m), hh(m, 1), ww(m, 1), cc(m, 1);
+  // Parts of ~kIngestPart files: while part i uploads, synchronises and decodes on the
+  // device (its rounds block this thread on the stream), a host thread parses and destuffs
+  // part i + 1 into the other pinned slot.
+  // Parts keep the whole call's entropy-chunk size (a part sized on its own would cut
+  // twice as many, shorter chunks, whose warm-up and synchronisation cost more than the
+  // overlap wins).  Measured at 4096 face crops (profiles/r02/jpeg): one part 10.2 ms,
+  // two parts 10.7 ms, four 14.7 ms — each part pays its synchronisation rounds' host
+  // round trips and decodes fewer chunks at once — so calls up to EF_OPT_JPEG_PART_FILES
+  // (8192) files run as one part.
+  const int32_t kIngestPart = (int32_t)std::max<int64_t>(1, c->opt_jpeg_part_files);
+  struct Part {
+    int32_t a = 0, m = 0;
     Batch B;
-    StageTimer tm;
-    build_batch(data, offsets + a, sizes + a, m, mode, nullptr, st.data(), B);
-    tm.mark("parse");
-    int rc = ensure(c, c->jpeg_out, (size_t)B.dense_out + 256);
-    if (rc != EF_OK) return rc;
-    uint8_t* pix = static_cast<uint8_t*>(c->jpeg_out.p);
-    if (!B.imgs.empty()) {
-      rc = decode_batch(c, B, data, offsets + a, pix);
-      if (rc != EF_OK) return rc;
-    }
-    // a file the GPU decoder does not take becomes a 1x1 zero image: its row is zero
-    std::vector<int64_t> doff(m, B.dense_out);
-    for (size_t i = 0; i < B.imgs.size(); ++i) {
-      const int k = B.img_of[i];
-      doff[k] = B.imgs[i].out_off;
-      hh[k] = B.imgs[i].h;
-      ww[k] = B.imgs[i].w;
-      cc[k] = ch;
-    }
-    if ((int32_t)B.imgs.size() < m) {
-      const hipError_t e = hipMemsetAsync(pix + B.dense_out, 0, 16, c->stream);
-      if (e != hipSuccess) return hip_err(c, e, "jpeg ingest");
-    }
-    uint8_t* rows = out + (int64_t)a * row;
+    Staged S;
+    std::vector<int32_t> st;
+    int rc = EF_OK;
+    std::string err;
+  };
+  int64_t call_chunk_bits = 0;
+  auto prepare = [&](Part& P, int slot) {
+    (void)hipSetDevice(c->device);  // a fresh host thread starts on device 0
+    P.st.assign(P.m, 0);
+    build_batch(data, offsets + P.a, sizes + P.a, P.m, mode, nullptr, P.st.data(), P.B);
+    if (!P.B.imgs.empty()) P.rc = stage_batch(c, slot, P.B, data, offsets + P.a, P.S, &P.err, call_chunk_bits);
+  };
+  for (int32_t a0 = 0; a0 < count; a0 += 65535) {  // ef_preprocess's per-call image limit
+    const int32_t m0 = std::min<int32_t>(65535, count - a0);
+    uint8_t* rows_all = out + (int64_t)a0 * row;
     if (!(flags & EF_MEM_DEVICE)) {  // host rows: resize into device staging, then copy out
-      rc = ensure(c, c->jpeg_rows, (size_t)m * row);
+      const int rc = ensure(c, c->jpeg_rows, (size_t)m0 * row);
       if (rc != EF_OK) return rc;
-      rows = static_cast<uint8_t*>(c->jpeg_rows.p);
+      rows_all = static_cast<uint8_t*>(c->jpeg_rows.p);
     }
-    tm.mark("decode");
-    rc = ef_preprocess(c, pix, doff.data(), hh.data(), ww.data(), cc.data(), m, out_h, out_w, rows, EF_MEM_DEVICE);
-    if (rc != EF_OK) return rc;
-    tm.mark("preprocess");
+    const int32_t nparts = (m0 + kIngestPart - 1) / kIngestPart;
+    // make_chunks' rule on the call's file bytes (entropy bits ~ file bytes x 8)
+    int64_t bytes = 0;
+    for (int32_t i = 0; i < m0; ++i) bytes += std::max<int64_t>(sizes[a0 + i], 0);
+    call_chunk_bits = nparts > 1 ? std::max<int64_t>(2048, std::min<int64_t>((bytes * 8 / 131072 + 255) / 256 * 256, 16384)) : 0;
+    std::vector<Part> parts(nparts);
+    for (int32_t i = 0; i < nparts; ++i) {
+      parts[i].a = a0 + (int32_t)((int64_t)m0 * i / nparts);
+      parts[i].m = a0 + (int32_t)((int64_t)m0 * (i + 1) / nparts) - parts[i].a;
+    }
+    prepare(parts[0], 0);
+    for (int32_t i = 0; i < nparts; ++i) {
+      Part& P = parts[i];
+      std::thread next;
+      if (i + 1 < nparts) next = std::thread(prepare, std::ref(parts[i + 1]), (i + 1) & 1);
+      int rc = P.rc != EF_OK ? set_err(c, P.rc, "ef_jpeg_ingest: " + P.err) : EF_OK;
+      uint8_t* pix = nullptr;
+      if (rc == EF_OK) rc = ensure(c, c->jpeg_out, (size_t)P.B.dense_out + 256);
+      if (rc == EF_OK) {
+        pix = static_cast<uint8_t*>(c->jpeg_out.p);
+        if (!P.B.imgs.empty()) rc = launch_batch(c, P.B, P.S, pix);
+      }
+      std::vector<int32_t> hh(P.m, 1), ww(P.m, 1), cc(P.m, 1);
+      std::vector<int64_t> doff(P.m, P.B.dense_out);
+      if (rc == EF_OK) {
+        // a file the GPU decoder does not take becomes a 1x1 zero image: its row is zero
+        for (size_t j = 0; j < P.B.imgs.size(); ++j) {
+          const int k = P.B.img_of[j];
+          doff[k] = P.B.imgs[j].out_off;
+          hh[k] = P.B.imgs[j].h;
+          ww[k] = P.B.imgs[j].w;
+          cc[k] = ch;
+        }
+        if ((int32_t)P.B.imgs.size() < P.m) {
+          const hipError_t e = hipMemsetAsync(pix + P.B.dense_out, 0, 16, c->stream);
+          if (e != hipSuccess) rc = hip_err(c, e, "jpeg ingest");
+        }
+      }
+      if (rc == EF_OK)
+        rc = ef_preprocess(c, pix, doff.data(), hh.data(), ww.data(), cc.data(), P.m, out_h, out_w,
+                           rows_all + (int64_t)(P.a - a0) * row, EF_MEM_DEVICE);
+      if (next.joinable()) next.join();  // before any return: the thread uses parts[i + 1]
+      if (rc != EF_OK) return rc;
+      if (status) std::memcpy(status + P.a, P.st.data(), (size_t)P.m * 4);
+      P.B = Batch();  // release the part's host tables
+    }
     if (!(flags & EF_MEM_DEVICE)) {
-      hipError_t e = hipMemcpyAsync(out + (int64_t)a * row, rows, (size_t)m * row, hipMemcpyDeviceToHost, c->stream);
+      hipError_t e = hipMemcpyAsync(out + (int64_t)a0 * row, rows_all, (size_t)m0 * row, hipMemcpyDeviceToHost,
+                                    c->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) return hip_err(c, e, "jpeg ingest");
     }
-    if (status) std::memcpy(status + a, st.data(), (size_t)m * 4);
   }
   return EF_OK;
 }

@@ -194,6 +194,8 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
                                       and a widened error bound; identities and scores are still
                                       fp64-resolved, so results equal the fp32 scan's [0]; 2: the same
                                       with the 32x32x16 kernel at k in (64, 128] (comparison) */
+#define EF_OPT_JPEG_PART_FILES 8   /* ef_jpeg_ingest decodes in parts of this many files, staging
+                                      part i + 1 on a host thread while part i decodes [8192] */
 int ef_set_option(ef_ctx* ctx, int32_t option, int64_t value);
 int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 

@@ -99,3 +99,40 @@ def test_ingest_into_device_tensor_large_batch(eng):
     rows = out.cpu().numpy()
     for i in range(0, n, 97):
         np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(blobs[i], "bgr"), (64, 64)))
+
+
+def test_ingest_parts_host_output_status(eng):
+    """The ingest decodes in parts (EF_OPT_JPEG_PART_FILES; the next part staged on a host thread):
+    statuses and rows land at every part's offsets, host and device outputs agree, and
+    files the decoder does not take (progressive) give zero rows in any part."""
+    import torch
+    n = 2500
+    blobs = [J.encode(J.smooth_image(60 + k % 29, 50 + k % 31, 3, k), quality=70 + k % 25, subsampling=k % 3)
+             for k in range(n)]
+    bad = [5, 1023, 1024, 1700, 2499]
+    for i in bad:
+        blobs[i] = _progressive()
+    eng.set_option("jpeg_part_files", 1024)  # three parts
+    try:
+        rows, st = eng.ingest_jpegs(blobs, (64, 64), "gray")
+        one_rows, one_st = None, None
+        eng.set_option("jpeg_part_files", 8192)  # one part
+        one_rows, one_st = eng.ingest_jpegs(blobs, (64, 64), "gray")
+    finally:
+        eng.set_option("jpeg_part_files", 8192)
+    np.testing.assert_array_equal(one_st, st)
+    np.testing.assert_array_equal(one_rows, rows)
+    assert [i for i in range(n) if st[i] != 0] == bad
+    assert all(st[i] == -10 for i in bad)
+    assert not rows[bad].any()
+    out = torch.empty((n, 64 * 64), dtype=torch.uint8, device="cuda")
+    eng.set_option("jpeg_part_files", 1000)
+    try:
+        _, st2 = eng.ingest_jpegs(blobs, (64, 64), "gray", out=out)
+    finally:
+        eng.set_option("jpeg_part_files", 8192)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st2, st)
+    np.testing.assert_array_equal(out.cpu().numpy(), rows)
+    for i in [0, 1022, 1025, 1699, 1701, 2498]:
+        np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(blobs[i], "gray"), (64, 64)))

@@ -193,3 +193,21 @@ def test_split_kernel_shapes_agree(split, k):
         np.testing.assert_array_equal(k16, k32)
         np.testing.assert_array_equal(k3232, k32)
     assert split.get_option("search_split_bf16") == 2
+
+
+@pytest.mark.parametrize("k", [64, 128, 512])
+def test_candidate_overflow_cluster(split, k):
+    """A cluster of 200 rows within 1e-6 of each other around the probes: every row of the
+    cluster is inside the scan's bound, more than the 32 kept candidates, so the resolve
+    pass re-scores the whole gallery in fp64 — fp32 and split scans both return the fp64
+    argmin (np.argmin semantics)."""
+    rng = np.random.default_rng(k + 99)
+    n, b = 3000, 64
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    base = rng.standard_normal(k).astype(np.float32)
+    g[100:300] = base + (rng.standard_normal((200, k)) * 1e-6).astype(np.float32)
+    q = (base + rng.standard_normal((b, k)).astype(np.float32) * 0.01).astype(np.float32)
+    want = orc.l2_argmin(q, g)[0]
+    k32, k3 = _keys_both(split, g, q, "l2")
+    np.testing.assert_array_equal((k32 & 0xFFFFFFFF).astype(np.int64), want)
+    np.testing.assert_array_equal(k3, k32)
