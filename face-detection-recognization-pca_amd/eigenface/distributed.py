@@ -79,6 +79,9 @@ class ShardedGallery:
         self.engine = engine
         if engine is not None and gallery_local is not None:
             engine.set_gallery(gallery_local, global_offset=self.lo)
+        # one rank with the engine's own search: its keys are already global (no records,
+        # no merge launch)
+        self._direct = world == 1 and engine is not None and local_matches is None and local_project is None
         self._local = local_matches or (lambda q, m: engine.search_matches(q, m))
         self._project = local_project or (lambda p, out=None: engine.project(p, out=out))
         self._fbuf = {}
@@ -117,6 +120,8 @@ class ShardedGallery:
 
     def search_keys(self, Q, metric="l2", keys=None):
         """Global packed keys of the best row per probe (all ranks get the same keys)."""
+        if self._direct:
+            return self.engine.search_keys(Q, metric, keys=keys)
         b = int(Q.shape[0])
         return self._gather_merge(self._local(Q, metric), b, keys)
 
@@ -172,6 +177,8 @@ class ShardedGallery:
         the engine's fused ef_recognize_matches runs the whole batch."""
         import torch
 
+        if self._direct:
+            return self.engine.recognize_keys(P, metric, keys=keys)
         b = int(P.shape[0])
         if self.world == 1 or not shard_projection or not isinstance(P, torch.Tensor):
             return self._gather_merge(self.engine.recognize_matches(P, metric), b, keys)
