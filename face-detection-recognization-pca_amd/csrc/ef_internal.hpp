@@ -50,6 +50,9 @@ struct SearchPlan {
   // wide kernel: (chunk, probe tile) pairs are dealt to XCDs in blocks of cblk chunks x
   // pblk probe tiles, so one XCD's L2 holds pblk probe tiles instead of all of them
   int pblk = 0, cblk = 1;
+  // collect pass (queued probes only): c_grid workgroups stride over (c_chunks chunks of
+  // c_tpc tiles) x (queued probe tiles) items
+  int c_chunks = 1, c_tpc = 1, c_grid = 8;
 };
 
 // ---- device buffer ------------------------------------------------------------------

@@ -108,18 +108,8 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
   float* const sG0 = smem;
   float* const sAux0 = smem + 2 * TGS;
 
-  // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD a contiguous run of
-  // (chunk, probe-tile) pairs so the probe tiles of one chunk are co-resident on it.
-  const int total = gridDim.x;  // host guarantees total % 8 == 0
-  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  const int gc = lin / n_ptiles;
-  const int pt = lin - gc * n_ptiles;
-
-  int n_amb = 0;
-  if constexpr (COLLECT) {
-    n_amb = *ws.amb_count;
-    if (pt * 256 >= n_amb) return;  // uniform: nothing queued for this probe tile
-  }
+  // one (gallery chunk gc, probe tile pt) work item
+  auto body = [&](const int gc, const int pt, const int n_amb) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -421,6 +411,22 @@ __global__ __launch_bounds__(512, 4) void search_kernel(
       ws.part_b2[o + s0] = b2;
     }
   }
+  };  // body
+  if constexpr (COLLECT) {
+    // collect pass: n_ptiles carries the collect plan's chunk count; the grid strides over
+    // the (chunk, queued probe tile) items, so a handful of queued probes still spread over
+    // the whole grid instead of one workgroup per main-pass chunk
+    const int n_amb = *ws.amb_count;
+    const int items = ((n_amb + 256 - 1) / 256) * n_ptiles;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item % n_ptiles, item / n_ptiles, n_amb);
+  } else {
+    // XCD-aware mapping: blocks b and b+8 share an XCD; give each XCD a contiguous run of
+    // (chunk, probe-tile) pairs so the probe tiles of one chunk are co-resident on it.
+    const int total = gridDim.x;  // host guarantees total % 8 == 0
+    const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int gc = lin / n_ptiles;
+    body(gc, lin - gc * n_ptiles, 0);
+  }
 }
 
 // Split-bf16 scan on v_mfma_f32_16x16x32_bf16, KP = 128 (the C3 shape).  Same workgroup,
@@ -443,15 +449,8 @@ __global__ __launch_bounds__(512, 4) void search16_kernel(
   __shared__ __attribute__((aligned(16))) float smem[2 * TGS + 2 * TG];
   float* const sAux0 = smem + 2 * TGS;
 
-  const int total = gridDim.x;  // host guarantees total % 8 == 0
-  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  const int gc = lin / n_ptiles;
-  const int pt = lin - gc * n_ptiles;
-  int n_amb = 0;
-  if constexpr (COLLECT) {
-    n_amb = *ws.amb_count;
-    if (pt * 256 >= n_amb) return;
-  }
+  // one (gallery chunk gc, probe tile pt) work item
+  auto body = [&](const int gc, const int pt, const int n_amb) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -661,6 +660,20 @@ __global__ __launch_bounds__(512, 4) void search16_kernel(
         ws.part_b2[o] = b2[pb];
       }
     }
+  }
+  };  // body
+  if constexpr (COLLECT) {
+    // collect pass: n_ptiles carries the collect plan's chunk count; the grid strides over
+    // the (chunk, queued probe tile) items, so a handful of queued probes still spread over
+    // the whole grid instead of one workgroup per main-pass chunk
+    const int n_amb = *ws.amb_count;
+    const int items = ((n_amb + 256 - 1) / 256) * n_ptiles;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item % n_ptiles, item / n_ptiles, n_amb);
+  } else {
+    const int total = gridDim.x;  // host guarantees total % 8 == 0
+    const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int gc = lin / n_ptiles;
+    body(gc, lin - gc * n_ptiles, 0);
   }
 }
 
@@ -889,6 +902,11 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3) {
   // chunk is read by n_ptiles / 8 XCDs.
   // The split-bf16 wide kernel's probe tiles are 256 x KP x 4 B (512 KiB at KP = 512): 4
   // of them per XCD keep 2 MiB of probes L2-resident.
+  // collect plan: ~512 chunks (a few queued probes then spread over the whole chip; with
+  // every probe tile queued the grid strides over all items, a main pass's work)
+  pl.c_tpc = (int)std::max<int64_t>(1, (tiles + 511) / 512);
+  pl.c_chunks = (int)((tiles + pl.c_tpc - 1) / pl.c_tpc);
+  pl.c_grid = w3 ? 256 : 512;
   const int pb = w3 ? 4 : 8;
   pl.pblk = pl.n_ptiles;
   pl.cblk = 1;
@@ -948,11 +966,11 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
     hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
                        g_offset, gmax2, ws, keys);
     if (k16)
-      hipLaunchKernelGGL((search16_kernel<M, true>), grid, block, 0, s, qpad, G3, aux, n, pl.n_ptiles,
-                         pl.tiles_per_chunk, bpad, ws);
+      hipLaunchKernelGGL((search16_kernel<M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G3, aux, n,
+                         pl.c_chunks, pl.c_tpc, bpad, ws);
     else
-      hipLaunchKernelGGL((search_kernel<KP, M, true, true>), grid, block, 0, s, qpad, G3, aux, n, pl.n_ptiles,
-                         pl.tiles_per_chunk, bpad, ws);
+      hipLaunchKernelGGL((search_kernel<KP, M, true, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G3,
+                         aux, n, pl.c_chunks, pl.c_tpc, bpad, ws);
     hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
     return hipGetLastError();
   }
@@ -1000,8 +1018,8 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
     e = launch_search_wide(s, KP, M, true, false, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
-    hipLaunchKernelGGL((search_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, bpad, ws);
+    hipLaunchKernelGGL((search_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,
+                       pl.c_chunks, pl.c_tpc, bpad, ws);
   }
   hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
   return hipGetLastError();

@@ -53,20 +53,8 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
   // slice, when the DMA of the next tile's first slice is already in flight)
   __shared__ __attribute__((aligned(16))) float smem[4 * WSL + 2 * WR];
 
-  const int total = gridDim.x;  // host guarantees total % 8 == 0
-  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  // (chunk, probe tile) blocks of cblk x pblk, one block per XCD (see search_plan)
-  const int bsz = cblk * pblk;
-  const int blk = lin / bsz, r = lin - blk * bsz;
-  const int nbp = n_ptiles / pblk;
-  const int gc = (blk / nbp) * cblk + r / pblk;
-  const int pt = (blk % nbp) * pblk + r % pblk;
-
-  int n_amb = 0;
-  if constexpr (COLLECT) {
-    n_amb = *ws.amb_count;
-    if (pt * WP >= n_amb) return;  // uniform: nothing queued for this probe tile
-  }
+  // one (gallery chunk gc, probe tile pt) work item
+  auto body = [&](const int gc, const int pt, const int n_amb) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -293,6 +281,23 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
       ws.part_b2[o] = b2;
     }
   }
+  };  // body
+  if constexpr (COLLECT) {
+    // collect pass: n_ptiles carries the collect plan's chunk count; the grid strides over
+    // the (chunk, queued probe tile) items, so a handful of queued probes still spread over
+    // the whole grid instead of one workgroup per main-pass chunk
+    const int n_amb = *ws.amb_count;
+    const int items = ((n_amb + 128 - 1) / 128) * n_ptiles;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item % n_ptiles, item / n_ptiles, n_amb);
+  } else {
+    const int total = gridDim.x;  // host guarantees total % 8 == 0
+    const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    // (chunk, probe tile) blocks of cblk x pblk, one block per XCD (see search_plan)
+    const int bsz = cblk * pblk;
+    const int blk = lin / bsz, r = lin - blk * bsz;
+    const int nbp = n_ptiles / pblk;
+    body((blk / nbp) * cblk + r / pblk, (blk % nbp) * pblk + r % pblk, 0);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -316,19 +321,8 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
   constexpr int NS = KP / WBK;
   __shared__ __attribute__((aligned(16))) float smem[4 * W3SL + 2 * W3R];
 
-  const int total = gridDim.x;  // host guarantees total % 8 == 0
-  const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-  const int bsz = cblk * pblk;
-  const int blk = lin / bsz, rr = lin - blk * bsz;
-  const int nbp = n_ptiles / pblk;
-  const int gc = (blk / nbp) * cblk + rr / pblk;
-  const int pt = (blk % nbp) * pblk + rr % pblk;
-
-  int n_amb = 0;
-  if constexpr (COLLECT) {
-    n_amb = *ws.amb_count;
-    if (pt * W3P >= n_amb) return;  // uniform: nothing queued for this probe tile
-  }
+  // one (gallery chunk gc, probe tile pt) work item
+  auto body = [&](const int gc, const int pt, const int n_amb) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -453,7 +447,12 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
     const int buf = (int)(it & 1);
     const int sl = (int)(it % NS);
     const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
-    if (it + 1 < n_it) issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+#if EF_WIDE_ABL == 3
+    if (it + 1 < 2)  // diagnostic builds only: no slice DMA after the first (results invalid)
+#else
+    if (it + 1 < n_it)
+#endif
+      issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
     if (sl == 0) {
       // L2: start from -||g||^2 / 2 and accumulate q.g (-2 acc = ||g||^2 - 2 q.g); cosine: 0
 #pragma unroll
@@ -566,6 +565,22 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
       }
     }
   }
+  };  // body
+  if constexpr (COLLECT) {
+    // collect pass: n_ptiles carries the collect plan's chunk count; the grid strides over
+    // the (chunk, queued probe tile) items, so a handful of queued probes still spread over
+    // the whole grid instead of one workgroup per main-pass chunk
+    const int n_amb = *ws.amb_count;
+    const int items = ((n_amb + 256 - 1) / 256) * n_ptiles;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item % n_ptiles, item / n_ptiles, n_amb);
+  } else {
+    const int total = gridDim.x;  // host guarantees total % 8 == 0
+    const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int bsz = cblk * pblk;
+    const int blk = lin / bsz, rr = lin - blk * bsz;
+    const int nbp = n_ptiles / pblk;
+    body((blk / nbp) * cblk + rr / pblk, (blk % nbp) * pblk + rr % pblk, 0);
+  }
 }
 
 template <int KP, int M>
@@ -576,8 +591,8 @@ static hipError_t wide3_t(hipStream_t s, bool collect, const SearchPlan& pl, con
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0 || bpad % W3P != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
   if (collect)
-    hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+    hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux, n,
+                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
   else
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
@@ -593,8 +608,8 @@ static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan&
     return hipErrorInvalidValue;  // the block deal would not be a bijection
   if (s3) return wide3_t<KP, M>(s, collect, pl, qpad, G, aux, n, bpad, ws);  // plan from search_plan(.., true)
   if (collect)
-    hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+    hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,
+                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
   else
     hipLaunchKernelGGL((search_wide_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);

@@ -10,6 +10,6 @@ for spec in "$@"; do
   mkdir -p build/v_$tag
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall $flags -c csrc/ef_search_wide.hip -o build/v_$tag/ef_search_wide.o
   objs=$(ls build/*.o | grep -v ef_search_wide.o)
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs build/v_$tag/ef_search_wide.o -o eigenface/_lib/libeigenface_$tag.so -lrocblas
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs build/v_$tag/ef_search_wide.o -o eigenface/_lib/libeigenface_$tag.so -ldl
   echo built $tag
 done
