@@ -9,17 +9,19 @@ from .engine import Engine, FitResult, decode_keys, device_count, merge_matches_
 from .pca import (  # noqa: F401
     EigenfacePCA,
     get_engine,
+    load_gallery_cache,
     manual_pca,
     recognize_face,
     recognize_face_dual_model,
     recognize_face_with_model,
     recognize_faces,
     recognize_faces_dual_model,
+    save_gallery_cache,
 )
 
 __all__ = [
     "Engine", "FitResult", "decode_keys", "device_count", "EigenfacePCA", "get_engine",
     "manual_pca", "recognize_face", "recognize_face_with_model", "recognize_faces",
     "recognize_face_dual_model", "recognize_faces_dual_model", "merge_matches_host", "EigenfaceError",
-    "NativeLibraryError", "LIB_PATH",
+    "NativeLibraryError", "LIB_PATH", "save_gallery_cache", "load_gallery_cache",
 ]

@@ -7,9 +7,11 @@ functions of the reference's hot path, all executed by libeigenface on the GPU.
                                    fit/transform/fit_transform surface
 * ``recognize_face_with_model``  — scan-template-v4.py:270-287
 * ``recognize_face``             — useless/scan.py:100-132
+* ``save_gallery_cache`` / ``load_gallery_cache`` — raw ``.npy`` gallery features
 """
 from __future__ import annotations
 
+import os
 import threading
 
 import numpy as np
@@ -113,12 +115,21 @@ class EigenfacePCA:
 
     # --------------------------------------------------------------- recognize
     def set_gallery(self, features=None):
-        """Gallery rows for ``recognize`` (default: the training features)."""
+        """Gallery rows for ``recognize`` (default: the training features); a path loads a
+        raw ``.npy`` feature cache (memory-mapped, see ``save_gallery_cache``)."""
         eng = get_engine(self.device)
+        if isinstance(features, (str, os.PathLike)):
+            features = load_gallery_cache(features)
         self._gallery_src = self.face_features_ if features is None else np.asarray(features)
         self._gallery_token = object()
         eng.set_gallery(np.asarray(self._gallery_src, dtype=np.float32), owner=self._gallery_token)
         return self
+
+    def save_gallery(self, path):
+        """Write the current gallery (default: the training features) as a raw ``.npy``
+        cache, so a large gallery is reloaded instead of re-projected."""
+        save_gallery_cache(path, self.face_features_ if self._gallery_src is None else self._gallery_src)
+        return path
 
     def recognize(self, P, metric="cosine", threshold=None):
         """Batched recognise: returns (idx, score); with ``threshold`` (cosine
@@ -133,6 +144,21 @@ class EigenfacePCA:
         if threshold is not None:
             idx = np.where(best >= threshold, idx, -1)
         return idx, best
+
+
+def save_gallery_cache(path, features):
+    """Gallery features as a raw float32 ``.npy`` file (SURVEY §5 checkpoint/resume: the 1M
+    gallery is not re-projected on restart).  Plain array data, no pickle."""
+    np.save(path, np.ascontiguousarray(features, dtype=np.float32), allow_pickle=False)
+
+
+def load_gallery_cache(path, mmap=True):
+    """The cache written by ``save_gallery_cache``: a read-only memory map by default, which
+    ``Engine.set_gallery`` uploads without an extra host copy."""
+    a = np.load(path, mmap_mode="r" if mmap else None, allow_pickle=False)
+    if a.ndim != 2 or a.dtype != np.float32:
+        raise ValueError(f"{path}: expected a 2-D float32 feature array, got {a.dtype} {a.shape}")
+    return a
 
 
 def manual_pca(data_matrix, n_components=None, device=0):

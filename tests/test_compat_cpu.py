@@ -61,3 +61,19 @@ def test_decode_image_is_bgr(tmp_path):
     Image.fromarray(rgb[..., 0]).save(tmp_path / "g.png")
     assert decode_image(str(tmp_path / "g.png")).shape == (50, 40)
     assert decode_image(str(tmp_path / "missing.png")) is None
+
+
+def test_gallery_cache_roundtrip(tmp_path):
+    """Raw .npy gallery-feature cache: float32, no pickle, memory-mapped load."""
+    import numpy as np
+    from eigenface import load_gallery_cache, save_gallery_cache
+    g = np.random.default_rng(0).standard_normal((1000, 50))
+    p = tmp_path / "gallery.npy"
+    save_gallery_cache(p, g)
+    a = load_gallery_cache(p)
+    assert isinstance(a, np.memmap) and a.dtype == np.float32 and a.shape == (1000, 50)
+    np.testing.assert_array_equal(a, g.astype(np.float32))
+    np.save(tmp_path / "bad.npy", np.zeros(5))
+    import pytest
+    with pytest.raises(ValueError):
+        load_gallery_cache(tmp_path / "bad.npy")

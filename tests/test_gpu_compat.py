@@ -244,3 +244,20 @@ def test_dual_model_recognition_matches_reference_rule():
         assert got[0] == (rd[0] if rd[1] >= rl[1] else rl[0]) or abs(rd[1] - rl[1]) < 1e-6
         np.testing.assert_allclose(got[3:], [rd[1], rl[1]], atol=2e-6)
         np.testing.assert_allclose(got[1], max(rd[1], rl[1]), atol=2e-6)
+
+
+def test_gallery_cache_recognize(tmp_path):
+    """EigenfacePCA.save_gallery / set_gallery(path): the memory-mapped cache gives the same
+    identities as the in-memory gallery."""
+    import numpy as np
+    from eigenface import EigenfacePCA
+    from oracle import eigenface_oracle as orc
+    x, _ = orc.synth_faces(300, 32, r=24, seed=3)
+    m = EigenfacePCA(20).fit(x)
+    idx0, s0 = m.recognize(x[:50], "cosine")
+    p = m.save_gallery(tmp_path / "g.npy")
+    m2 = EigenfacePCA(20).fit(x)
+    m2.set_gallery(p)
+    idx1, s1 = m2.recognize(x[:50], "cosine")
+    np.testing.assert_array_equal(idx1, idx0)
+    np.testing.assert_array_equal(s1, s0)
