@@ -156,6 +156,16 @@ struct Tables {
   std::vector<HuffTab> huff;
   std::vector<unsigned short> quant;  // 64 entries (natural order) per table
   std::unordered_map<std::string, int> huff_idx, quant_idx;
+  std::vector<const std::string*> huff_key;  // key of each table in `huff` (for merging)
+  // a table another Tables derived: index under its key, added if new
+  int merge_huff(const std::string& key, const HuffTab& t) {
+    auto it = huff_idx.find(key);
+    if (it != huff_idx.end()) return it->second;
+    const int idx = (int)huff.size();
+    huff.push_back(t);
+    huff_key.push_back(&huff_idx.emplace(key, idx).first->first);
+    return idx;
+  }
   int huff_table(const RawHuff& r, bool dc) {  // index, or -1 for an invalid table
     int cnt = 0;
     for (int l = 1; l <= 16; ++l) cnt += r.bits[l];
@@ -167,7 +177,8 @@ struct Tables {
     HuffTab t;
     const int idx = derive(r, t, dc) ? (int)huff.size() : -1;
     if (idx >= 0) huff.push_back(t);
-    huff_idx.emplace(std::move(key), idx);
+    const std::string* kp = &huff_idx.emplace(std::move(key), idx).first->first;
+    if (idx >= 0) huff_key.push_back(kp);
     return idx;
   }
   int quant_table(const unsigned short* q) {
@@ -1163,45 +1174,95 @@ struct Batch {
   int64_t coef_blocks = 0, plane_bytes = 0, blocks = 0, rows = 0, dense_out = 0;
 };
 
-// out_offsets: images land there (device layout); null: packed densely
+// out_offsets: images land there (device layout); null: packed densely.
+// The per-file marker parse runs on host threads (one Tables and segment list per thread),
+// merged in file order afterwards: the same images, segments and layout as a sequential
+// parse, with the batch tables deduplicated in the order the accepted files use them.
 void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int count, int mode,
                  const int64_t* out_offsets, int32_t* status, Batch& B) {
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
-  for (int i = 0; i < count; ++i) {
-    JImage im{};
-    const size_t seg0 = B.segs.size();
-    int st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], (int)B.imgs.size(), im, B.T, B.segs, true)
-                          : EF_JPEG_E_CORRUPT;
-    if (st == 0 && (int64_t)im.w * im.h > ((int64_t)1 << 31)) st = EF_JPEG_E_UNSUPPORTED;
-    if (st == 0 && B.T.huff.size() >= (size_t)kMaxTables) st = EF_JPEG_E_UNSUPPORTED;  // int32 table offsets
-    if (status) status[i] = st;
-    if (st != 0) {
-      B.segs.resize(seg0);
-      continue;
+  struct FileRes {
+    JImage im;
+    int st = 0, seg_beg = 0, seg_end = 0;
+  };
+  std::vector<FileRes> R((size_t)std::max(count, 0));
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nt = count >= 512 ? (int)std::min<unsigned>(16u, hw) : 1;
+  std::vector<Tables> TT(nt);
+  std::vector<std::vector<JSeg>> SS(nt);
+  auto work = [&](int t, int a, int e) {
+    for (int i = a; i < e; ++i) {
+      FileRes& f = R[i];
+      f.im = JImage{};
+      f.seg_beg = (int)SS[t].size();
+      f.st = sizes[i] > 0 ? parse(data + offsets[i], sizes[i], i, f.im, TT[t], SS[t], true) : EF_JPEG_E_CORRUPT;
+      if (f.st != 0) SS[t].resize(f.seg_beg);
+      f.seg_end = (int)SS[t].size();
     }
-    for (size_t k = seg0; k < B.segs.size(); ++k) {  // destuffed bytes never exceed the raw ones
-      B.segs[k].word_off = B.words;
-      B.words += (B.segs[k].end - B.segs[k].beg + 3) / 4 + 1;
-    }
-    im.mode = mode;
-    const int nneed = mode == EF_JPEG_GRAY ? 1 : im.nc;  // grey output needs the luma plane only
-    for (int k = 0; k < im.nc; ++k) {
-      im.c[k].coef_off = B.coef_blocks * 64;
-      B.coef_blocks += (int64_t)im.c[k].bw * im.c[k].bh;
-      im.c[k].plane_off = B.plane_bytes;
-      if (k < nneed) {
-        B.plane_bytes += (int64_t)im.c[k].bw * 8 * im.c[k].bh * 8;
-        B.block_start.push_back(B.blocks);
-        B.ic.push_back((int)(B.imgs.size() << 2) | k);
-        B.blocks += (int64_t)im.c[k].bw * im.c[k].bh;
+  };
+  std::vector<int> t_beg(nt + 1);
+  for (int t = 0; t <= nt; ++t) t_beg[t] = (int)((int64_t)count * t / nt);
+  if (nt == 1) {
+    work(0, 0, count);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(work, t, t_beg[t], t_beg[t + 1]);
+    for (auto& x : th) x.join();
+  }
+  // merge in file order: thread-local table indices -> batch tables, then the layout
+  for (int t = 0; t < nt; ++t) {
+    // tables enter the batch lazily, in the order the accepted files use them
+    std::vector<int> hmap(TT[t].huff.size(), -1), qmap(TT[t].quant.size() / 64, -1);
+    auto H = [&](int j) {
+      if (hmap[j] < 0) hmap[j] = B.T.merge_huff(*TT[t].huff_key[j], TT[t].huff[j]);
+      return hmap[j];
+    };
+    auto Q = [&](int j) {
+      if (qmap[j] < 0) qmap[j] = B.T.quant_table(TT[t].quant.data() + 64 * j);
+      return qmap[j];
+    };
+    for (int i = t_beg[t]; i < t_beg[t + 1]; ++i) {
+      FileRes& f = R[i];
+      JImage& im = f.im;
+      int st = f.st;
+      if (st == 0) {
+        for (int k = 0; k < im.nc; ++k) {
+          im.c[k].dc = H(im.c[k].dc);
+          im.c[k].ac = H(im.c[k].ac);
+        }
+        for (int k = 0; k < im.nc; ++k) im.c[k].q = Q(im.c[k].q);
       }
+      if (st == 0 && (int64_t)im.w * im.h > ((int64_t)1 << 31)) st = EF_JPEG_E_UNSUPPORTED;
+      if (st == 0 && B.T.huff.size() >= (size_t)kMaxTables) st = EF_JPEG_E_UNSUPPORTED;  // int32 table offsets
+      if (status) status[i] = st;
+      if (st != 0) continue;
+      for (int k = f.seg_beg; k < f.seg_end; ++k) {  // destuffed bytes never exceed the raw ones
+        JSeg sg = SS[t][k];
+        sg.img = (int)B.imgs.size();
+        sg.word_off = B.words;
+        B.words += (sg.end - sg.beg + 3) / 4 + 1;
+        B.segs.push_back(sg);
+      }
+      im.mode = mode;
+      const int nneed = mode == EF_JPEG_GRAY ? 1 : im.nc;  // grey output needs the luma plane only
+      for (int k = 0; k < im.nc; ++k) {
+        im.c[k].coef_off = B.coef_blocks * 64;
+        B.coef_blocks += (int64_t)im.c[k].bw * im.c[k].bh;
+        im.c[k].plane_off = B.plane_bytes;
+        if (k < nneed) {
+          B.plane_bytes += (int64_t)im.c[k].bw * 8 * im.c[k].bh * 8;
+          B.block_start.push_back(B.blocks);
+          B.ic.push_back((int)(B.imgs.size() << 2) | k);
+          B.blocks += (int64_t)im.c[k].bw * im.c[k].bh;
+        }
+      }
+      im.out_off = out_offsets ? out_offsets[i] : B.dense_out;
+      B.dense_out += (int64_t)im.w * im.h * ch;
+      B.row_start.push_back(B.rows);
+      B.rows += im.h;
+      B.img_of.push_back(i);
+      B.imgs.push_back(im);
     }
-    im.out_off = out_offsets ? out_offsets[i] : B.dense_out;
-    B.dense_out += (int64_t)im.w * im.h * ch;
-    B.row_start.push_back(B.rows);
-    B.rows += im.h;
-    B.img_of.push_back(i);
-    B.imgs.push_back(im);
   }
 }
 
