@@ -657,9 +657,9 @@ def _pack_blobs(blobs):
     if _BYTES_OFF is None:
         _BYTES_OFF = _bytes_data_offset()
     n = len(blobs)
-    sizes = np.fromiter((len(b) for b in blobs), np.int64, n)
-    if _BYTES_OFF and all(type(b) is bytes for b in blobs):  # payload address = id + header
-        addrs = np.fromiter((id(b) for b in blobs), np.int64, n) + _BYTES_OFF
+    sizes = np.fromiter(map(len, blobs), np.int64, n)
+    if _BYTES_OFF and set(map(type, blobs)) == {bytes}:  # payload address = id + header
+        addrs = np.fromiter(map(id, blobs), np.int64, n) + _BYTES_OFF
         keep = blobs
     else:
         keep = [np.frombuffer(b, np.uint8) if len(b) else np.zeros(1, np.uint8) for b in blobs]
