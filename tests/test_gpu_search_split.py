@@ -211,3 +211,29 @@ def test_candidate_overflow_cluster(split, k):
     k32, k3 = _keys_both(split, g, q, "l2")
     np.testing.assert_array_equal((k32 & 0xFFFFFFFF).astype(np.int64), want)
     np.testing.assert_array_equal(k3, k32)
+
+
+@pytest.mark.parametrize("k", [64, 128, 512])
+def test_split_match_records_equal_fp32(split, k):
+    """The exact cross-shard merge consumes match records (fp64 score, tie scale, key):
+    the split scan's records equal the fp32 scan's field for field, per shard, and the
+    merged keys equal the single-gallery keys."""
+    rng = np.random.default_rng(k + 2)
+    g = rng.standard_normal((4000, k)).astype(np.float32)
+    q = rng.standard_normal((600, k)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        recs = {}
+        for opt in (0, 1):
+            split.set_option("search_split_bf16", opt)
+            parts = []
+            for lo, hi in [(0, 1500), (1500, 4000)]:
+                split.set_gallery(g[lo:hi], global_offset=lo)
+                parts.append(split.search_matches(q, metric))
+            recs[opt] = parts
+            from eigenface import merge_matches_host
+            merged = merge_matches_host(np.concatenate(parts), len(q))
+            split.set_gallery(g)
+            np.testing.assert_array_equal(merged, split.search_keys(q, metric))
+        for a, b in zip(recs[0], recs[1]):
+            for f in ("score", "scale", "key"):
+                np.testing.assert_array_equal(a[f], b[f])
