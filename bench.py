@@ -9,9 +9,14 @@ One step = project 4096 uint8 probe faces (p - mean).W + search the gallery + (N
 two all-gathers and the merge.  Inputs are resident in HBM before timing.  Data are
 synthetic (eigenface.synth): planted probes, so the step's result is also checked.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--backend nccl|gloo]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+With WORLD_SIZE unset and --gpus N > 1 the script is its own launcher: the parent process
+(which makes no GPU call) starts N rank processes of this file with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, waits for all of them and exits
+non-zero if any rank fails.  Under torchrun, --gpus must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -510,9 +515,61 @@ def haar_bench(eng, with_cpu: bool, frames=10):
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv, timeout_s=None) -> int:
+    """Start n rank processes of this script (the torchrun environment contract) from a
+    parent that has made no GPU call, wait for all, and return the first non-zero exit
+    code (0 when every rank succeeded).  When one rank fails the others are stopped, so
+    a rank blocked in a collective cannot hang the job."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    t0 = time.time()
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the others")
+                for q in alive:
+                    q.terminate()
+        if timeout_s and time.time() - t0 > timeout_s and alive:
+            log(f"[launcher] timeout after {timeout_s} s; stopping {len(alive)} rank(s)")
+            for q in alive:
+                q.terminate()
+            rc = rc or 124
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo exchanges through "
+                         "the host and lets ranks share one GPU, for tests)")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="self-launch (N > 1 without torchrun): stop every rank after this many seconds (0: none)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--repeats", type=int, default=5,
@@ -533,19 +590,43 @@ def main():
     ap.add_argument("--split-opt", type=int, default=1, choices=[1, 2],
                     help="EF_OPT_SEARCH_SPLIT_BF16 value of the split scan (2: the 32x32x16 kernel at k = 128)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # be the launcher: no torch / GPU call in this process
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout or None))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            ap.error(f"--gpus {args.gpus} disagrees with WORLD_SIZE={world} from the launcher")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        log("bench.py: no GPU visible")
+        sys.exit(2)
+    if local >= ndev:
+        if args.backend == "nccl":  # RCCL needs one GPU per rank
+            log(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPU(s) are visible; "
+                "use --backend gloo to let ranks share a GPU")
+            sys.exit(2)
+        log(f"[rank {rank}] sharing GPU {local % ndev} (gloo, {ndev} GPU(s) visible)")
+    dev_index = local % ndev
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    local = dev_index
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from eigenface import Engine, decode_keys, synth
     from eigenface.distributed import ShardedGallery, shard_range
@@ -598,7 +679,7 @@ def main():
                 dist.barrier()
             el = time.perf_counter() - t0
             if world > 1:
-                t = torch.tensor([el], dtype=torch.float64, device=dev)
+                t = torch.tensor([el], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 el = float(t.item())
             reps.append(el)
@@ -613,6 +694,15 @@ def main():
 
     idx, best = decode_keys(keys.cpu().numpy(), args.metric)
     match = float((idx == targets).mean())
+    ranks_agree = None
+    if world > 1:  # every rank must hold the same merged keys
+        h = torch.tensor([int(np.bitwise_xor.reduce(keys.cpu().numpy() * np.int64(0x9E3779B1)))
+                          & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64,
+                         device=dev if args.backend == "nccl" else "cpu")
+        lo_t, hi_t = h.clone(), h.clone()
+        dist.all_reduce(lo_t, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi_t, op=dist.ReduceOp.MAX)
+        ranks_agree = bool(lo_t.item() == hi_t.item())
 
     host_rate = None
     if world == 1:  # PCIe-inclusive rate (never `value`)
@@ -709,15 +799,18 @@ def main():
                 "workload": f"{args.config.upper()}: gallery {n_total} x k={k}, {side}x{side} uint8 faces, "
                             f"probe batch {bsz}, metric {args.metric}, projection {precision}",
                 "gallery": n_total, "face": f"{side}x{side}", "k": k, "batch": bsz,
-                "parallelism": f"gallery row-shard x{world}: projection split + RCCL all-gather of "
-                               "features, local search, RCCL all-gather of fp64 match records + exact merge"
+                "parallelism": (f"gallery row-shard x{world}: projection split + "
+                                f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-gather of features, "
+                                "local search, all-gather of fp64 match records + exact merge")
                                if world > 1 else "1 GPU",
+                "rows_per_rank": hi - lo,
+                "backend": args.backend if world > 1 else None,
             },
             "roofline": dict(roof(split_main, search_avg_ms), traffic=traffic, traffic_source=traffic_src,
                              launches=s_n),
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
             "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
-            "check": {"planted_match": match},
+            "check": {"planted_match": match, "ranks_agree": ranks_agree},
         }
         if tol:
             rec["bf16_projection_tolerance"] = tol

@@ -10,6 +10,15 @@
 // reference's best-over-models loop (scan-template-v4.py:297-319, strict '>' in model
 // order) by an order-independent exact reduction.
 //
+// What "exact" covers: the merged row equals the single-gallery arg-best whenever the
+// competing rows' fp64 scores are exactly equal (lowest global index wins, np.argmin's
+// rule) or differ by more than the 1e-12 relative tie window.  Inside that window — fp64
+// rounding noise of the score evaluation itself, where np.argmin's own answer depends on
+// summation order — a shard reports the lowest index of ITS window (measured from its own
+// minimum, scaled by its own max‖g‖²), so a row that is in the global window but not in
+// its shard's can lose to another shard's row.  Closing that would need a second
+// exchange round for a difference below fp64 evaluation error; it is not done.
+//
 // RCCL is loaded at run time (dlopen): a process that already mapped a librccl (torch's)
 // reuses it, and libeigenface keeps no link-time dependency on it.
 #include <dlfcn.h>

@@ -8,10 +8,12 @@
 // probe features Qp[bpad][KP] (bpad a multiple of 256).
 //
 // Pass 1 — search_kernel (the hot kernel, v_mfma_f32_32x32x2_f32, exact fp32):
-//   * workgroup = 4 waves = 256 probes; each wave keeps 64 probes (two 32-probe
-//     B-operand blocks, KP/2 fp32 VGPRs each) in registers for the whole sweep;
-//   * the workgroup sweeps one chunk of the gallery in 32-row tiles staged through
-//     double-buffered LDS (register-staged prefetch of tile t+1 under tile t's MFMAs);
+//   * workgroup = 8 waves = 256 probes; each wave keeps 32 probes (one 32-probe
+//     B-operand block, KP/2 fp32 VGPRs, pre-scaled) in registers for the whole sweep;
+//   * the workgroup sweeps one chunk of the gallery in 64-row tiles (two 32-row MFMA
+//     blocks = two independent accumulator chains per wave) staged through
+//     double-buffered LDS by LDS-DMA (global_load_lds, ef_dma.hpp), tile t+1's DMA in
+//     flight under tile t's MFMAs;
 //   * the gallery tile is the MFMA A operand so each lane's 16 accumulators hold 16
 //     gallery rows of ONE probe: the arg-best is an in-lane running (best, index,
 //     runner-up) with no cross-lane traffic until one __shfl_xor(32) at the end;
@@ -37,7 +39,8 @@
 // elements: 16 B of hi, 16 B of lo), so the tile DMA and the LDS reads are those of the
 // fp32 kernel.  The pass-2 bound covers the dropped terms (lo.lo', e) and the longer
 // chain; the winner is still re-scored from the fp32 gallery in fp64, so keys and match
-// records equal the fp32 path's bit for bit whenever both resolve (tests/test_gpu_search.py).
+// records equal the fp32 path's bit for bit whenever both resolve
+// (tests/test_gpu_search_split.py; at the full C3 size, tests/test_gpu_c3_full.py).
 #include "ef_search_common.hpp"
 
 #include <climits>

@@ -438,32 +438,50 @@ def recognize_faces_all_models(face_imgs, models, threshold=0.8, device=0):
     best_conf = np.zeros(n)
     if n == 0:
         return []
-    rows = preprocess_faces(face_imgs, device)
+    # one launch for the batch; if a crop is unusable (the reference's per-face resize
+    # raises inside the per-model try, :312-314), find it and give it the sentinel
+    try:
+        rows = preprocess_faces(face_imgs, device)
+        ok = np.arange(n)
+    except Exception:  # noqa: BLE001
+        good, parts = [], []
+        for i, img in enumerate(face_imgs):
+            try:
+                parts.append(preprocess_faces([img], device))
+                good.append(i)
+            except Exception as e:  # noqa: BLE001
+                print(f"Error recognizing face {i}: {e}")
+        if not good:
+            return [(-1, "unknown", 0.0)] * n
+        rows, ok = np.concatenate(parts), np.asarray(good)
     for person_name, info in models.items():
         md = info["model_data"] if "model_data" in info else info
         if md is None:
             continue
-        try:
+        try:  # everything per model inside the try, as the reference (:302-314)
             f = extract_faces_features(rows, md, device)
             eng = _gallery_engine(md["face_features"], device)
             idx, sim = eng.search(f.astype(np.float32), "cosine")
+            labels, pmap = md["face_labels"], md["person_id_map"]
+            upd = []
+            for j, i in enumerate(ok):
+                conf = float(sim[j])
+                if not conf > best_conf[i]:
+                    continue
+                pid, name = -1, "unknown"
+                if idx[j] >= 0 and conf >= threshold:  # recognize_face_with_model (:278-284)
+                    pid = labels[idx[j]]
+                    for nm, v in pmap.items():
+                        if v == pid:
+                            name = nm
+                            break
+                upd.append((i, conf, (pid, name if name != "unknown" else person_name, conf)))
         except Exception as e:  # reference: print and continue (:312-314)
             print(f"Error recognizing with model {person_name}: {e}")
             continue
-        labels, pmap = md["face_labels"], md["person_id_map"]
-        for i in range(n):
-            conf = float(sim[i])
-            if not conf > best_conf[i]:
-                continue
-            pid, name = -1, "unknown"
-            if idx[i] >= 0 and conf >= threshold:  # recognize_face_with_model (:278-284)
-                pid = labels[idx[i]]
-                for nm, v in pmap.items():
-                    if v == pid:
-                        name = nm
-                        break
+        for i, conf, rec in upd:  # a model that fails half-way changes nothing
             best_conf[i] = conf
-            best[i] = (pid, name if name != "unknown" else person_name, conf)
+            best[i] = rec
     return [b if b else (-1, "unknown", 0.0) for b in best]
 
 

@@ -8,7 +8,9 @@ over xGMI with backend "nccl", gloo on CPU) lets every rank merge them exactly w
 ``ef_matches_merge``: the lowest global index among the ranks whose fp64 score is within
 1e-12 of the best.  A MIN over the packed fp32 keys alone would order two ranks' winners
 only to fp32 resolution and break sub-ulp differences by index; the fp64 record makes the
-sharded arg-best equal the single-engine one.
+sharded arg-best equal the single-engine one for exact ties and for any
+two rows whose fp64 scores differ by more than the 1e-12 relative tie window (inside it —
+fp64 evaluation noise — each shard resolves its own window first; csrc/ef_comm.hip).
 
 The projection model is replicated; the probe batch's projection is split by rows across
 ranks and the (B x k) fp32 features are all-gathered (2 MiB at B = 4096, k = 128), so no

@@ -388,12 +388,16 @@ class Engine:
 
     def _matches(self, X, metric, out, search):
         mt = _metric(metric)
+        if self.gallery_k is None:
+            raise RuntimeError("no gallery: call set_gallery first")
+        if not search and self.model_k is None:
+            raise RuntimeError("recognize needs a model and a gallery")
         if _is_dev(X):
             import torch
             if search:
                 x, xp = _dev(X, torch.float32)
                 if x.ndim != 2 or x.shape[1] != self.gallery_k:
-                    raise ValueError(f"Q must be (b, {self.gallery_k})")
+                    raise ValueError(f"Q must be (b, {self.gallery_k}), got {tuple(x.shape)}")
             else:
                 x, xp, dtype = self._dev_pixels(X)
             b = x.shape[0]
@@ -408,10 +412,16 @@ class Engine:
             return out
         if search:
             x, xp = _host(X, np.float32)
+            want = self.gallery_k
         else:
             x = np.asarray(X)
             dtype = N.EF_U8 if x.dtype == np.uint8 else N.EF_F32
             x, xp = _host(x, np.uint8 if dtype == N.EF_U8 else np.float32)
+            want = self.model_d
+        # the C side reads b * want elements from the host pointer: a narrower or 1-D
+        # input would be read past its end
+        if x.ndim != 2 or x.shape[1] != want:
+            raise ValueError(f"{'Q' if search else 'P'} must be (b, {want}), got {x.shape}")
         b = x.shape[0]
         res = np.empty(b, dtype=N.MATCH_DTYPE)
         if search:
@@ -424,9 +434,20 @@ class Engine:
         """Device merge (ef_matches_merge, EF_MEM_DEVICE) of gathered records: ``parts`` is
         an (nparts*b, 3) int64 tensor (part-major) -> int64 keys[b]."""
         import torch
+        b = int(b)
+        if not (isinstance(parts, torch.Tensor) and parts.is_cuda):
+            raise TypeError("parts must be a device tensor (use merge_matches_host for host records)")
+        if parts.dtype != torch.int64 or parts.ndim != 2 or parts.shape[1] != 3 or not parts.is_contiguous():
+            raise ValueError(f"parts must be a contiguous (nparts*b, 3) int64 tensor, got "
+                             f"{parts.dtype} {tuple(parts.shape)}")
+        if b < 0 or (b and parts.shape[0] % b) or (b == 0 and parts.shape[0]):
+            raise ValueError(f"parts has {parts.shape[0]} records, not a multiple of b = {b}")
         nparts = parts.shape[0] // b if b else 0
         if keys is None:
             keys = torch.empty(b, dtype=torch.int64, device=parts.device)
+        elif not (keys.dtype == torch.int64 and tuple(keys.shape) == (b,) and keys.is_contiguous()
+                  and keys.device == parts.device):
+            raise ValueError(f"keys must be a contiguous int64 tensor of shape ({b},) on {parts.device}")
         if b:
             self._chk(self._lib.ef_matches_merge(self._h, parts.data_ptr(), nparts, b, keys.data_ptr(), None,
                                                  N.EF_MEM_DEVICE))
@@ -617,7 +638,13 @@ def merge_matches_host(parts, b):
     array of N.MATCH_DTYPE (nparts*b, part-major) or its (nparts*b, 3) int64 view."""
     p = np.ascontiguousarray(parts)
     if p.dtype != np.dtype(N.MATCH_DTYPE):
-        p = np.ascontiguousarray(p, dtype=np.int64).view(N.MATCH_DTYPE).reshape(-1)
+        p = np.ascontiguousarray(p, dtype=np.int64)
+        if p.ndim != 2 or p.shape[1] != 3:
+            raise ValueError(f"parts must be (nparts*b, 3) int64 or MATCH_DTYPE records, got {p.shape}")
+        p = p.view(N.MATCH_DTYPE).reshape(-1)
+    b = int(b)
+    if b < 0 or (b and p.shape[0] % b) or (b == 0 and p.shape[0]):
+        raise ValueError(f"{p.shape[0]} records is not a multiple of b = {b}")
     nparts = p.shape[0] // b if b else 0
     keys = np.empty(b, dtype=np.int64)
     if b:

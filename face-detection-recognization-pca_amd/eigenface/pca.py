@@ -180,20 +180,44 @@ def manual_pca(data_matrix, n_components=None, device=0):
 # ------------------------------------------------------------------ recognize
 class _ArrayToken:
     """Owner token of an uploaded host array: the array itself (kept alive, so its id
-    cannot be reused) plus a digest of its bytes (so in-place edits re-upload)."""
+    cannot be reused), its data pointer, shape and dtype, plus a digest of its bytes (so
+    in-place edits re-upload).  The digest covers every byte of arrays up to
+    FULL_DIGEST_BYTES (≈1 ms); above that it covers a strided sample of ~1 MiB of rows
+    plus the first and last row, so a per-call check of a 1M-row gallery costs
+    microseconds instead of a full hash.  After editing a large array in place outside
+    that sample, call :func:`invalidate_uploads`."""
+
+    FULL_DIGEST_BYTES = 16 << 20
 
     def __init__(self, a):
         self.a = a
+        self.ptr = a.__array_interface__["data"][0]
         self.shape, self.dtype = a.shape, a.dtype
         self.digest = _digest(a)
 
     def matches(self, a):
-        return a is self.a and a.shape == self.shape and a.dtype == self.dtype and _digest(a) == self.digest
+        return (a is self.a and a.shape == self.shape and a.dtype == self.dtype
+                and a.__array_interface__["data"][0] == self.ptr and _digest(a) == self.digest)
 
 
 def _digest(a):
     import hashlib
+    a = np.asarray(a)
+    if a.nbytes > _ArrayToken.FULL_DIGEST_BYTES and a.ndim >= 1 and a.shape[0] > 2:
+        rows = a.shape[0]
+        row_bytes = max(1, a.nbytes // rows)
+        step = max(1, rows * row_bytes // (1 << 20))
+        a = np.concatenate([a[::step], a[-1:]])
     return hashlib.blake2b(np.ascontiguousarray(a).view(np.uint8), digest_size=16).digest()
+
+
+def invalidate_uploads(device: int = 0):
+    """Forget which host arrays the device's resident model and gallery came from: the
+    next recognise call re-uploads them (needed only after an in-place edit of a large
+    array that the sampled digest of :class:`_ArrayToken` may miss)."""
+    eng = get_engine(device)
+    eng.model_owner = None
+    eng.gallery_owner = None
 
 
 def _gallery_engine(features, device):

@@ -1,0 +1,64 @@
+"""bench.py's launcher logic without a GPU: --gpus must agree with a torchrun WORLD_SIZE,
+and the self-launch (WORLD_SIZE unset, --gpus N > 1) starts N rank processes with the
+torchrun environment and propagates a failing rank's exit code."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def test_gpus_must_match_world_size():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4"], capture_output=True, text=True, timeout=120,
+                       env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and "disagrees with WORLD_SIZE=2" in r.stderr
+
+
+def test_gpus_must_be_positive():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "0"], capture_output=True, text=True, timeout=120,
+                       env=_env())
+    assert r.returncode == 2
+
+
+def test_self_launch_sets_rank_env_and_propagates_failure():
+    """Here every rank finds no GPU and exits 2: the parent must report it (not 0), and
+    each rank must have seen its own RANK / LOCAL_RANK and the common WORLD_SIZE."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--launch-timeout", "200"], capture_output=True,
+                       text=True, timeout=300, env=_env())
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "no GPU visible" in r.stderr
+
+
+def test_launch_ranks_passes_environment(tmp_path, monkeypatch):
+    """launch_ranks itself: the children get the torchrun contract variables."""
+    sys.path.insert(0, ROOT)
+    import importlib
+    bench = importlib.import_module("bench")
+    script = tmp_path / "child.py"
+    script.write_text("import os, sys\n"
+                      "out = os.path.join(%r, 'r' + os.environ['RANK'])\n"
+                      "open(out, 'w').write(' '.join(os.environ[k] for k in "
+                      "('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))\n"
+                      "sys.exit(0 if os.environ['RANK'] != '1' else 5)\n" % str(tmp_path))
+    monkeypatch.setattr(bench, "__file__", str(script))
+    rc = bench.launch_ranks(3, [], timeout_s=60)
+    assert rc == 5
+    port = None
+    for r in range(3):
+        f = tmp_path / f"r{r}"
+        if not f.exists():  # rank 1 failing may stop a later rank before it writes
+            continue
+        rank, local, world, addr, p = f.read_text().split()
+        assert (rank, local, world, addr) == (str(r), str(r), "3", "127.0.0.1")
+        assert port in (None, p)
+        port = p

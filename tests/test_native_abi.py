@@ -151,3 +151,45 @@ def test_host_match_merge_is_exact():
     np.testing.assert_array_equal(idx, [107, 5, 9, -1, 111])
     assert best[4] == np.float32(4.0)
     assert out[3] == none
+
+
+def _hostless_engine(model_d=None, model_k=None, gallery_k=None):
+    """An Engine whose context was never created (no GPU here): the input checks run
+    before any C call, so a call that reaches the library would fail on the NULL ctx."""
+    from eigenface import Engine
+    e = object.__new__(Engine)
+    from eigenface import _native
+    e._lib = _native.lib()
+    e._h = ctypes.c_void_p()
+    e.model_d, e.model_k, e.gallery_k, e.gallery_n = model_d, model_k, gallery_k, 0
+    return e
+
+
+def test_match_record_api_checks_shapes_before_the_c_call():
+    """search_matches / recognize_matches on host arrays: the C side reads b x k (or
+    b x d) elements from the pointer, so a narrower or 1-D input must raise first."""
+    e = _hostless_engine()
+    with pytest.raises(RuntimeError):
+        e.search_matches(np.zeros((4, 8), np.float32))
+    e = _hostless_engine(gallery_k=8)
+    with pytest.raises(RuntimeError):
+        e.recognize_matches(np.zeros((4, 16), np.uint8))
+    e = _hostless_engine(model_d=16, model_k=8, gallery_k=8)
+    for bad in (np.zeros((4, 7), np.float32), np.zeros(8, np.float32), np.zeros((2, 4, 8), np.float32)):
+        with pytest.raises(ValueError):
+            e.search_matches(bad)
+    for bad in (np.zeros((4, 15), np.uint8), np.zeros(16, np.uint8), np.zeros((4, 8), np.float32)):
+        with pytest.raises(ValueError):
+            e.recognize_matches(bad)
+
+
+def test_host_merge_checks_record_shapes():
+    from eigenface import _native as N, merge_matches_host
+    recs = np.zeros(6, dtype=N.MATCH_DTYPE)
+    with pytest.raises(ValueError):
+        merge_matches_host(recs, 4)  # 6 records are not a multiple of b = 4
+    with pytest.raises(ValueError):
+        merge_matches_host(np.zeros((6, 2), np.int64), 3)
+    recs["key"] = N.EF_KEY_NONE
+    recs["score"] = np.inf
+    assert (merge_matches_host(recs, 3) == N.EF_KEY_NONE).all()
