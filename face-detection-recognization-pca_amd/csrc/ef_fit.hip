@@ -447,12 +447,16 @@ int complete_null_components(ef_ctx* c, int64_t n, int64_t d, int kk, const doub
 
 }  // namespace
 
-extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint32_t flags,
-                      double* mean_out, double* var_out, double* scale_out, double* comps_out,
-                      double* eig_out, double* proj_out, double* tv_out, int32_t* k_out, int32_t* iters_out) {
+extern "C" int ef_fit_ex(ef_ctx* c, const void* Xv, int32_t x_dtype, int64_t n, int64_t d, int32_t k,
+                         uint32_t flags, double* mean_out, double* var_out, double* scale_out, double* comps_out,
+                         double* eig_out, double* proj_out, double* tv_out, int32_t* k_out, int32_t* iters_out) {
   if (!c) return EF_E_INVALID;
-  if (!X || n < 2 || d < 1 || k < 1 || !mean_out || !comps_out || !eig_out)
+  if (!Xv || n < 2 || d < 1 || k < 1 || !mean_out || !comps_out || !eig_out)
     return set_err(c, EF_E_INVALID, "ef_fit: bad arguments (need X, n >= 2, d >= 1, k >= 1, outputs)");
+  if (x_dtype != EF_U8 && x_dtype != EF_F32 && x_dtype != EF_F64)
+    return set_err(c, EF_E_INVALID, "ef_fit: x_dtype must be EF_U8, EF_F32 or EF_F64");
+  const bool u8 = x_dtype == EF_U8;
+  const size_t esize = u8 ? 1 : (x_dtype == EF_F32 ? 4 : 8);
   (void)hipSetDevice(c->device);
   hipStream_t s = c->stream;
   const bool dev = flags & EF_MEM_DEVICE;
@@ -462,13 +466,18 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   const int kk = (int)(k < dim ? k : dim);
 
   Bufs B;
-  const uint8_t* Xd = X;
+  const void* Xdv = Xv;
   if (!dev) {
     uint8_t* xb;
-    EF_TRY(B.get(c, (size_t)n * d, &xb));
-    EF_HIP(c, hipMemcpyAsync(xb, X, (size_t)n * d, hipMemcpyHostToDevice, s), "H2D X");
-    Xd = xb;
+    EF_TRY(B.get(c, (size_t)n * d * esize, &xb));
+    EF_HIP(c, hipMemcpyAsync(xb, Xv, (size_t)n * d * esize, hipMemcpyHostToDevice, s), "H2D X");
+    Xdv = xb;
   }
+  // uint8 pixels take the exact integer kernels; float input the fp64 loaders
+  const uint8_t* Xd = u8 ? static_cast<const uint8_t*>(Xdv) : nullptr;
+  auto pix = [&](bool trans, const double* mu, const double* wv) {
+    return Operand::pixels(Xdv, x_dtype, d, trans, mu, wv);
+  };
   unsigned long long *S1, *S2;
   double *mean, *var, *scale, *w, *C, *work, *U, *lam, *E = nullptr, *comps, *En, *proj = nullptr, *tv;
   EF_TRY(B.get(c, (size_t)d, &S1));
@@ -488,17 +497,23 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   // K1: exact column statistics -> mean / var / scale / centring weights.  On the int8
   // covariance path the operand transpose produces the sums in the same pass over X.
   const double inv = 1.0 / (double)(n - 1);
-  const bool int8_path = !gram || !stdz;
+  const bool int8_path = u8 && (!gram || !stdz);
   uint8_t* At = nullptr;
-  EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
-  EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
-  const bool fused = int8_path && !gram && cov_i8_fused_stats(Xd, d);
-  if (int8_path) {
-    EF_TRY(B.get(c, (size_t)dim * cov_i8_kpad(gram ? d : n) + kSyrkPadBytes, &At));
-    EF_HIP(c, launch_cov_i8_prep(s, Xd, n, d, gram, At, fused ? S1 : nullptr, fused ? S2 : nullptr), "cov prep");
+  if (u8) {
+    EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
+    EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
+    const bool fused = int8_path && !gram && cov_i8_fused_stats(Xd, d);
+    if (int8_path) {
+      EF_TRY(B.get(c, (size_t)dim * cov_i8_kpad(gram ? d : n) + kSyrkPadBytes, &At));
+      EF_HIP(c, launch_cov_i8_prep(s, Xd, n, d, gram, At, fused ? S1 : nullptr, fused ? S2 : nullptr), "cov prep");
+    }
+    if (!fused) EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
+    EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
+  } else {
+    double* part;
+    EF_TRY(B.get(c, colstats_float_work_elems(n, d), &part));
+    EF_HIP(c, launch_colstats_float(s, Xdv, x_dtype, n, d, stdz ? 1 : 0, part, mean, var, scale, w), "colstats (float)");
   }
-  if (!fused) EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
-  EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
   const double* wp = stdz ? w : nullptr;
 
   // K2+K3: covariance.  Exact integer product on the int8 matrix cores whenever the
@@ -522,11 +537,11 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
     B.drop(s, slabs);
     if (S64) B.drop(s, S64);
   } else if (gram)
-    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::pixels(Xd, d, true, mean, wp), n, n, d,
+    EF_HIP(c, gemm64(s, pix(false, mean, wp), pix(true, mean, wp), n, n, d,
                      inv, C, n, work, kWorkElems),
            "Gram");
   else
-    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, true, mean, wp), Operand::pixels(Xd, d, false, mean, wp), d, d, n,
+    EF_HIP(c, gemm64(s, pix(true, mean, wp), pix(false, mean, wp), d, d, n,
                      inv, C, d, work, kWorkElems),
            "covariance");
   EF_HIP(c, launch_trace(s, C, dim, dim, tv), "trace");
@@ -538,7 +553,7 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   // K5: back-project (Gram path), unit columns + sign rule
   if (gram) {
     EF_TRY(B.get(c, (size_t)d * kk, &E));
-    EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, true, mean, wp), Operand::dense(U, kk, false), d, kk, n, 1.0, E, kk,
+    EF_HIP(c, gemm64(s, pix(true, mean, wp), Operand::dense(U, kk, false), d, kk, n, 1.0, E, kk,
                      work, kWorkElems),
            "E = A^T.U");
     EF_HIP(c, launch_normalize_sign(s, E, d, kk, kk, comps, En), "normalize");
@@ -554,12 +569,12 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
 #else
     constexpr bool f64proj = false;
 #endif
-    if (proj_i8_supported(Xd, n, d, kk) && !f64proj) {  // exact int8 digits (ef_proj_i8.hip)
+    if (u8 && proj_i8_supported(Xd, n, d, kk) && !f64proj) {  // exact int8 digits (ef_proj_i8.hip)
       uint8_t* pw;
       EF_TRY(B.get(c, proj_i8_work_bytes(n, d, kk), &pw));
       EF_HIP(c, launch_proj_i8(s, Xd, n, d, mean, wp, En, kk, pw, proj), "F = A.E (int8 digits)");
     } else {
-      EF_HIP(c, gemm64(s, Operand::pixels(Xd, d, false, mean, wp), Operand::dense(En, kk, false), n, kk, d, 1.0,
+      EF_HIP(c, gemm64(s, pix(false, mean, wp), Operand::dense(En, kk, false), n, kk, d, 1.0,
                        proj, kk, work, kWorkElems),
              "F = A.E");
     }
@@ -576,5 +591,58 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
   EF_HIP(c, hipStreamSynchronize(s), "sync");
   if (k_out) *k_out = kk;
   if (iters_out) *iters_out = iters;
+  return EF_OK;
+}
+
+extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint32_t flags,
+                      double* mean_out, double* var_out, double* scale_out, double* comps_out,
+                      double* eig_out, double* proj_out, double* tv_out, int32_t* k_out, int32_t* iters_out) {
+  return ef_fit_ex(c, X, EF_U8, n, d, k, flags, mean_out, var_out, scale_out, comps_out, eig_out, proj_out, tv_out,
+                   k_out, iters_out);
+}
+
+// Column statistics alone (ManualStandardScaler.fit, scripts/manual/train-v2.py:58-64, and
+// StandardScaler.fit): exact integer sums for uint8, two-pass fp64 for float input.
+extern "C" int ef_colstats(ef_ctx* c, const void* Xv, int32_t x_dtype, int64_t n, int64_t d, uint32_t flags,
+                           double* mean_out, double* var_out) {
+  if (!c) return EF_E_INVALID;
+  if (!Xv || n < 1 || d < 1 || !mean_out)
+    return set_err(c, EF_E_INVALID, "ef_colstats: bad arguments (need X, n >= 1, d >= 1, mean_out)");
+  if (x_dtype != EF_U8 && x_dtype != EF_F32 && x_dtype != EF_F64)
+    return set_err(c, EF_E_INVALID, "ef_colstats: x_dtype must be EF_U8, EF_F32 or EF_F64");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->stream;
+  const bool dev = flags & EF_MEM_DEVICE;
+  const size_t esize = x_dtype == EF_U8 ? 1 : (x_dtype == EF_F32 ? 4 : 8);
+  Bufs B;
+  const void* Xdv = Xv;
+  if (!dev) {
+    uint8_t* xb;
+    EF_TRY(B.get(c, (size_t)n * d * esize, &xb));
+    EF_HIP(c, hipMemcpyAsync(xb, Xv, (size_t)n * d * esize, hipMemcpyHostToDevice, s), "H2D X");
+    Xdv = xb;
+  }
+  double *mean, *var, *scale, *w;
+  EF_TRY(B.get(c, (size_t)d, &mean));
+  EF_TRY(B.get(c, (size_t)d, &var));
+  EF_TRY(B.get(c, (size_t)d, &scale));
+  EF_TRY(B.get(c, (size_t)d, &w));
+  if (x_dtype == EF_U8) {
+    unsigned long long *S1, *S2;
+    EF_TRY(B.get(c, (size_t)d, &S1));
+    EF_TRY(B.get(c, (size_t)d, &S2));
+    EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
+    EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
+    EF_HIP(c, launch_colstats(s, static_cast<const uint8_t*>(Xdv), n, d, S1, S2), "colstats");
+    EF_HIP(c, launch_stats_finalize(s, S1, S2, n, d, 0, mean, var, scale, w), "stats");
+  } else {
+    double* part;
+    EF_TRY(B.get(c, colstats_float_work_elems(n, d), &part));
+    EF_HIP(c, launch_colstats_float(s, Xdv, x_dtype, n, d, 0, part, mean, var, scale, w), "colstats (float)");
+  }
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  EF_HIP(c, hipMemcpyAsync(mean_out, mean, d * sizeof(double), kind, s), "out mean");
+  if (var_out) EF_HIP(c, hipMemcpyAsync(var_out, var, d * sizeof(double), kind, s), "out var");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
   return EF_OK;
 }

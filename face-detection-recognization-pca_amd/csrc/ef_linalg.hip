@@ -8,6 +8,7 @@
 
 #include <climits>
 #include <cmath>
+#include <type_traits>
 
 namespace ef {
 
@@ -52,6 +53,63 @@ __global__ void stats_finalize_kernel(const unsigned long long* __restrict__ S1,
   const double bound = dn * eps * v + (dn * mu * eps) * (dn * mu * eps);
   const double sc = (v <= bound) ? 1.0 : sqrt(v);
   mean[c] = mu;
+  var[c] = v;
+  scale[c] = sc;
+  w[c] = standardize ? 1.0 / sc : 1.0;
+}
+
+// Float input (ManualStandardScaler output, float64 faces): fp64 column statistics in two
+// passes, partial sums per row block (part[blk][d]) summed in a fixed order.
+// Pass 1: part[blk][c] = sum x.  Pass 2: part[blk][c] = sum (x - mean), part2 = sum (x - mean)^2.
+template <class T>
+__global__ void colsum_float_kernel(const T* __restrict__ X, int64_t n, int64_t d, int64_t rows_per,
+                                    const double* __restrict__ mean, double* __restrict__ part,
+                                    double* __restrict__ part2) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = r0 + rows_per < n ? r0 + rows_per : n;
+  double s1 = 0.0, s2 = 0.0;
+  if (!mean) {
+    for (int64_t r = r0; r < r1; ++r) s1 += (double)X[r * d + c];
+  } else {
+    const double m = mean[c];
+    for (int64_t r = r0; r < r1; ++r) {
+      const double t = (double)X[r * d + c] - m;
+      s1 += t;
+      s2 = fma(t, t, s2);
+    }
+    part2[(int64_t)blockIdx.y * d + c] = s2;
+  }
+  part[(int64_t)blockIdx.y * d + c] = s1;
+}
+
+__global__ void colmean_float_kernel(const double* __restrict__ part, int nblk, int64_t n, int64_t d,
+                                     double* __restrict__ mean) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * d + c];
+  mean[c] = s / (double)n;
+}
+
+__global__ void colvar_float_kernel(const double* __restrict__ part, const double* __restrict__ part2, int nblk,
+                                    int64_t n, int64_t d, int standardize, const double* __restrict__ mean,
+                                    double* __restrict__ var, double* __restrict__ scale, double* __restrict__ w) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += part[(int64_t)b * d + c];
+    s2 += part2[(int64_t)b * d + c];
+  }
+  const double dn = (double)n;
+  double v = (s2 - s1 * s1 / dn) / dn;
+  if (v < 0.0) v = 0.0;
+  const double mu = mean[c];
+  const double eps = 2.220446049250313e-16;
+  const double bound = dn * eps * v + (dn * mu * eps) * (dn * mu * eps);  // sklearn _is_constant_feature
+  const double sc = (v <= bound) ? 1.0 : sqrt(v);
   var[c] = v;
   scale[c] = sc;
   w[c] = standardize ? 1.0 / sc : 1.0;
@@ -170,24 +228,37 @@ static hipError_t gemm_t(hipStream_t s, const LA& A, const LB& B, int64_t M, int
   return hipGetLastError();
 }
 
+// Calls fn(loader) with the operand's loader; kfast: the contiguous tile index is k.
+template <class Fn>
+static hipError_t with_loader(const Operand& o, bool kfast, Fn&& fn) {
+  if (!o.u8) return fn(DenseLd{o.p, o.ld, o.trans, kfast});
+  switch (o.elem) {
+    case EF_U8:
+      return fn(PixLd<uint8_t>{static_cast<const uint8_t*>(o.x), o.ld, o.trans, o.mu, o.w, kfast});
+    case EF_F32:
+      return fn(PixLd<float>{static_cast<const float*>(o.x), o.ld, o.trans, o.mu, o.w, kfast});
+    case EF_F64:
+      return fn(PixLd<double>{static_cast<const double*>(o.x), o.ld, o.trans, o.mu, o.w, kfast});
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 hipError_t gemm64(hipStream_t s, const Operand& A, const Operand& B, int64_t M, int64_t N, int64_t K,
                   double alpha, double* C, int64_t ldc, double* work, size_t work_elems) {
-  if (A.u8) {
-    const U8Ld a{A.x, A.ld, A.trans, A.mu, A.w, A.trans == 0};
-    if (B.u8) {
-      const U8Ld b{B.x, B.ld, B.trans, B.mu, B.w, B.trans != 0};
-      return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
-    }
-    const DenseLd b{B.p, B.ld, B.trans, B.trans != 0};
-    return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
-  }
-  const DenseLd a{A.p, A.ld, A.trans, A.trans == 0};
-  if (B.u8) {
-    const U8Ld b{B.x, B.ld, B.trans, B.mu, B.w, B.trans != 0};
-    return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
-  }
-  const DenseLd b{B.p, B.ld, B.trans, B.trans != 0};
-  return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+  // the two pixel operands of a product are always the same matrix (same element type)
+  if (A.u8 && B.u8 && A.elem != B.elem) return hipErrorInvalidValue;
+  return with_loader(A, A.trans == 0, [&](const auto& a) {
+    return with_loader(B, B.trans != 0, [&](const auto& b) {
+      if constexpr (!std::is_same_v<std::decay_t<decltype(a)>, std::decay_t<decltype(b)>> &&
+                    !std::is_same_v<std::decay_t<decltype(a)>, DenseLd> &&
+                    !std::is_same_v<std::decay_t<decltype(b)>, DenseLd>) {
+        return hipErrorInvalidValue;  // mixed pixel types: never instantiated as a kernel
+      } else {
+        return gemm_t(s, a, b, M, N, K, alpha, C, ldc, work, work_elems);
+      }
+    });
+  });
 }
 
 // ------------------------------------------------------------- K4: Jacobi in LDS
@@ -826,6 +897,42 @@ hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d
   ny = (n + rows_per - 1) / rows_per;
   hipLaunchKernelGGL(colstats_kernel, dim3((unsigned)cgroups, (unsigned)ny), dim3(256), 0, s, X, n, d,
                      rows_per, S1, S2);
+  return hipGetLastError();
+}
+
+static int64_t colstats_float_blocks(int64_t n, int64_t d) {
+  int64_t ny = (262144 + d - 1) / d;
+  if (ny > n) ny = n;
+  if (ny < 1) ny = 1;
+  if (ny > 1024) ny = 1024;
+  return ny;
+}
+
+size_t colstats_float_work_elems(int64_t n, int64_t d) { return (size_t)2 * colstats_float_blocks(n, d) * d; }
+
+hipError_t launch_colstats_float(hipStream_t s, const void* X, int elem, int64_t n, int64_t d, int standardize,
+                                 double* part, double* mean, double* var, double* scale, double* w) {
+  int64_t ny = colstats_float_blocks(n, d);
+  const int64_t rows_per = (n + ny - 1) / ny;
+  ny = (n + rows_per - 1) / rows_per;
+  const dim3 grid((unsigned)((d + 255) / 256), (unsigned)ny);
+  const unsigned cb = (unsigned)((d + 255) / 256);
+  double* part2 = part + ny * d;
+  for (int pass = 0; pass < 2; ++pass) {
+    const double* m = pass ? mean : nullptr;
+    if (elem == EF_F32)
+      hipLaunchKernelGGL(colsum_float_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(X), n, d,
+                         rows_per, m, part, part2);
+    else if (elem == EF_F64)
+      hipLaunchKernelGGL(colsum_float_kernel<double>, grid, dim3(256), 0, s, static_cast<const double*>(X), n, d,
+                         rows_per, m, part, part2);
+    else
+      return hipErrorInvalidValue;
+    if (pass == 0)
+      hipLaunchKernelGGL(colmean_float_kernel, dim3(cb), dim3(256), 0, s, part, (int)ny, n, d, mean);
+  }
+  hipLaunchKernelGGL(colvar_float_kernel, dim3(cb), dim3(256), 0, s, part, part2, (int)ny, n, d, standardize, mean,
+                     var, scale, w);
   return hipGetLastError();
 }
 

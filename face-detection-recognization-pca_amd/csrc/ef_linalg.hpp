@@ -18,9 +18,12 @@ struct DenseLd {
   }
 };
 
-// Stored M = X[sample][pixel] uint8; value = (x - mu[pixel]) * w[pixel] (w may be null).
-struct U8Ld {
-  const uint8_t* x;
+// Stored M = X[sample][pixel] of element type T (uint8 pixels, or float / double for
+// already-scaled data such as ManualStandardScaler's output); value = (x - mu[pixel]) *
+// w[pixel] (w may be null).
+template <class T>
+struct PixLd {
+  const T* x;
   int64_t ld;
   int trans;
   const double* mu;
@@ -33,12 +36,15 @@ struct U8Ld {
     return w ? v * w[px] : v;
   }
 };
+using U8Ld = PixLd<uint8_t>;
 
-// Host-side operand description for gemm64.
+// Host-side operand description for gemm64.  elem: EF_U8 / EF_F32 / EF_F64 for a pixel
+// operand (x), -1 for a dense fp64 matrix (p).
 struct Operand {
-  bool u8 = false;
+  bool u8 = false;  // pixel operand (any element type): read through PixLd
+  int elem = -1;
   const double* p = nullptr;
-  const uint8_t* x = nullptr;
+  const void* x = nullptr;
   int64_t ld = 0;
   int trans = 0;
   bool sym = false;  // symmetric: either orientation may be read (tall GEMM walks its rows)
@@ -56,15 +62,19 @@ struct Operand {
     o.trans = trans;
     return o;
   }
-  static Operand pixels(const uint8_t* x, int64_t ld, bool trans, const double* mu, const double* w) {
+  static Operand pixels(const void* x, int elem, int64_t ld, bool trans, const double* mu, const double* w) {
     Operand o;
     o.u8 = true;
+    o.elem = elem;
     o.x = x;
     o.ld = ld;
     o.trans = trans;
     o.mu = mu;
     o.w = w;
     return o;
+  }
+  static Operand pixels(const uint8_t* x, int64_t ld, bool trans, const double* mu, const double* w) {
+    return pixels(x, EF_U8, ld, trans, mu, w);
   }
 };
 
@@ -150,6 +160,14 @@ hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                           const double* E, int kk, void* work, double* F);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
+// Float input (EF_F32 / EF_F64): column mean and population variance in fp64 by two
+// passes with the one-batch form of sklearn's _incremental_mean_and_var (extmath.py:
+// mean = sum/n; var = (sum t^2 - (sum t)^2/n)/n with t = x - mean), partial sums per row
+// block added in a fixed order (deterministic); then the StandardScaler rule as
+// launch_stats_finalize.  part: colstats_float_work_elems(n, d) doubles.
+size_t colstats_float_work_elems(int64_t n, int64_t d);
+hipError_t launch_colstats_float(hipStream_t s, const void* X, int elem, int64_t n, int64_t d, int standardize,
+                                 double* part, double* mean, double* var, double* scale, double* w);
 hipError_t launch_stats_finalize(hipStream_t s, const unsigned long long* S1, const unsigned long long* S2,
                                  int64_t n, int64_t d, int standardize, double* mean, double* var,
                                  double* scale, double* w);

@@ -72,6 +72,9 @@ _SIGS = {
     "ef_synchronize": ([vp], C.c_int),
     "ef_trim": ([vp], C.c_int),
     "ef_fit": ([vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+    "ef_fit_ex": ([vp, vp, i32, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)],
+                  C.c_int),
+    "ef_colstats": ([vp, vp, i32, i64, i64, u32, vp, vp], C.c_int),
     "ef_model_set": ([vp, vp, vp, i64, i32, u32], C.c_int),
     "ef_project": ([vp, vp, i32, i64, vp, u32], C.c_int),
     "ef_gallery_set": ([vp, vp, i64, i32, i64, u32], C.c_int),
@@ -141,7 +144,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 3:
+        if h.ef_api_version() != 4:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

@@ -185,17 +185,37 @@ class Engine:
         return int(n.value), int(r.value)
 
     # ------------------------------------------------------------------------ fit
-    def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
-        """GPU eigenfaces fit of uint8 faces X (n x d); see include/eigenface.h ef_fit.
+    @staticmethod
+    def _fit_input(X):
+        """(array, pointer, EF dtype, on device) of fit input: uint8 pixels (exact integer
+        kernels) or float32 / float64 data (fp64 loaders; include/eigenface.h ef_fit_ex)."""
+        if _is_dev(X):
+            import torch
+            codes = {torch.uint8: N.EF_U8, torch.float32: N.EF_F32, torch.float64: N.EF_F64}
+            if X.dtype not in codes:
+                raise TypeError(f"fit input must be uint8, float32 or float64, got {X.dtype}")
+            x, xp = _dev(X, X.dtype)
+            return x, xp, codes[X.dtype], True
+        a = np.asarray(X)
+        if a.dtype == np.uint8:
+            code, dt = N.EF_U8, np.uint8
+        elif a.dtype == np.float32:
+            code, dt = N.EF_F32, np.float32
+        else:
+            code, dt = N.EF_F64, np.float64
+        x, xp = _host(a, dt)
+        return x, xp, code, False
 
-        X may be a host array or a device (torch uint8) tensor; for a device X the
-        outputs stay on the device (float64 torch tensors, EF_MEM_DEVICE)."""
-        dev = _is_dev(X)
+    def fit(self, X, n_components: int, standardize: bool = False, projection: bool = True) -> FitResult:
+        """GPU eigenfaces fit of faces X (n x d); see include/eigenface.h ef_fit / ef_fit_ex.
+
+        X is uint8 pixels, or float32 / float64 data (e.g. ManualStandardScaler output,
+        scripts/manual/train-v2.py:194-197).  It may be a host array or a device torch
+        tensor; for a device X the outputs stay on the device (float64 torch tensors,
+        EF_MEM_DEVICE)."""
+        x, xp, xdt, dev = self._fit_input(X)
         if dev:
             import torch
-            x, xp = _dev(X, torch.uint8)
-        else:
-            x, xp = _host(X, np.uint8)
         if x.ndim != 2:
             raise ValueError("X must be 2-D (n_samples, n_pixels)")
         n, d = (int(v) for v in x.shape)
@@ -220,12 +240,31 @@ class Engine:
         k_out = C.c_int32(0)
         it = C.c_int32(0)
         flags = (N.EF_FIT_STANDARDIZE if standardize else 0) | (N.EF_MEM_DEVICE if dev else 0)
-        self._chk(self._lib.ef_fit(
-            self._h, xp, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
+        self._chk(self._lib.ef_fit_ex(
+            self._h, xp, xdt, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
             ptr(proj) if proj is not None else None, ptr(tv), C.byref(k_out), C.byref(it)))
         if dev:
             self.synchronize()
         return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
+
+    def colstats(self, X):
+        """Column mean and population variance (float64) of X (n x d, uint8 / float32 /
+        float64; ef_colstats): np.mean / np.var(axis=0) on the GPU — exact integer sums for
+        uint8, two-pass fp64 for floats.  Host input -> numpy, device input -> tensors."""
+        x, xp, xdt, dev = self._fit_input(X)
+        if x.ndim != 2 or x.shape[0] < 1 or x.shape[1] < 1:
+            raise ValueError("X must be 2-D (n_samples >= 1, n_features >= 1)")
+        n, d = (int(v) for v in x.shape)
+        if dev:
+            import torch
+            mean = torch.empty(d, dtype=torch.float64, device=x.device)
+            var = torch.empty(d, dtype=torch.float64, device=x.device)
+            self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, N.EF_MEM_DEVICE, mean.data_ptr(), var.data_ptr()))
+            self.synchronize()
+            return mean, var
+        mean, var = np.empty(d), np.empty(d)
+        self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, 0, mean.ctypes.data, var.ctypes.data))
+        return mean, var
 
     # ----------------------------------------------------------------- projection
     def set_model(self, mean, W, precision="fp32", owner=None):

@@ -33,16 +33,23 @@ def get_engine(device: int = 0) -> Engine:
 
 
 def _as_pixels(X):
-    """The GPU fit consumes uint8 pixels (train-v4.py:68,73); float inputs
-    (useless/train.py:40 flattens to float64) must be integral 0..255."""
+    """Fit input: uint8 pixels (train-v4.py:68,73) go to the exact integer kernels, and so
+    do float arrays holding integral 0..255 values (useless/train.py:40 flattens the uint8
+    pixels to float64) — same numbers, exact products.  Any other float data (e.g.
+    standardised faces, scripts/manual/train-v2.py:194-197) is fitted as float64 on the
+    fp64 GEMM path (ef_fit_ex)."""
     x = np.asarray(X)
     if x.dtype == np.uint8:
         return x
+    if x.dtype == np.float32 and not np.all(np.isfinite(x)):
+        raise ValueError("fit input contains NaN or inf")
     xf = np.asarray(x, dtype=np.float64)
+    if not np.all(np.isfinite(xf)):
+        raise ValueError("fit input contains NaN or inf")
     xu = np.clip(np.rint(xf), 0, 255)
-    if not np.array_equal(xu, xf):
-        raise ValueError("GPU fit expects 8-bit pixel values (integers in 0..255)")
-    return xu.astype(np.uint8)
+    if np.array_equal(xu, xf):
+        return xu.astype(np.uint8)
+    return x if x.dtype == np.float32 else xf
 
 
 class EigenfacePCA:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 3
+#define EF_API_VERSION 4
 
 /* status codes */
 #define EF_OK 0
@@ -108,6 +108,23 @@ int ef_fit(ef_ctx* ctx, const uint8_t* X, int64_t n, int64_t d, int32_t k, uint3
            double* mean_out, double* var_out, double* scale_out, double* components_out,
            double* eigvals_out, double* proj_out, double* total_var_out, int32_t* k_out,
            int32_t* iters_out);
+/* ef_fit for any element type: x_dtype EF_U8 (= ef_fit), EF_F32 or EF_F64 — manual_pca's
+ * float64 faces (useless/train.py:40, :56-128) and ManualPCA.fit on standardised,
+ * non-integral data (scripts/manual/train-v2.py:16-42, fed by ManualStandardScaler :53-72).
+ * Float input: fp64 two-pass column statistics, covariance / Gram, back-projection and
+ * training projection on the fp64 MFMA GEMM with centring (and 1/scale) in the operand
+ * loads; uint8 input keeps the exact integer kernels. */
+int ef_fit_ex(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d, int32_t k, uint32_t flags,
+              double* mean_out, double* var_out, double* scale_out, double* components_out,
+              double* eigvals_out, double* proj_out, double* total_var_out, int32_t* k_out,
+              int32_t* iters_out);
+/* Column mean and population variance of X (n x d, EF_U8 / EF_F32 / EF_F64), float64 out:
+ * ManualStandardScaler.fit (np.mean / np.std, scripts/manual/train-v2.py:58-64) and
+ * StandardScaler.fit's statistics (train-v4.py:131).  uint8: exact integer sums; float:
+ * two passes in fp64 (sum, then sum of (x - mean) and (x - mean)^2, sklearn's
+ * _incremental_mean_and_var form).  var_out may be NULL. */
+int ef_colstats(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d, uint32_t flags,
+                double* mean_out, double* var_out);
 
 /* --------------------------------------------------------------- projection
  * Recognition model f = (p - mean) . W  (useless/scan.py:93-96; sklearn

@@ -43,6 +43,9 @@ __all__ = [
     "synth_basis",
     "synth_mean_face",
     "planted_probes",
+    "manual_standard_scaler",
+    "manual_pca_cov",
+    "cosine_similarity_vec",
 ]
 
 
@@ -91,6 +94,47 @@ def manual_model_info_evr(eigenvalues):
     """
     lam = np.asarray(eigenvalues, dtype=np.float64)
     return (lam / lam.sum())[:10]
+
+
+# --------------------------------------------------------------------------
+# Fit: the "manual" trainer's classes (scripts/manual/train-v2.py:9-72)
+# --------------------------------------------------------------------------
+def manual_standard_scaler(x):
+    """``ManualStandardScaler.fit_transform`` (scripts/manual/train-v2.py:58-72):
+    ``mean = np.mean(X, 0)``, ``scale = np.std(X, 0)`` with exact zeros set to 1,
+    ``Z = (X - mean) / scale``.  Returns ``(Z, mean, scale)`` float64."""
+    x = np.asarray(x, dtype=np.float64)
+    mean = np.mean(x, axis=0)
+    scale = np.std(x, axis=0)
+    scale[scale == 0] = 1
+    return (x - mean) / scale, mean, scale
+
+
+def manual_pca_cov(x, n_components):
+    """``ManualPCA.fit`` + ``transform`` (scripts/manual/train-v2.py:16-47): mean (:19),
+    centre (:22), the full d x d ``np.cov`` (:25), ``eigh`` (:28), descending (:31-33),
+    top-k rows (:36), ratio over the sum of ALL eigenvalues (:39-40); features
+    ``(X - mean) . components^T``.  Eigenvector signs are normalised to sklearn's
+    svd_flip rule (largest-|.| entry positive) since eigh's are arbitrary.  Returns
+    ``(components (k, d), mean, evr (k,), eigenvalues (k,), features (n, k))``."""
+    x = np.asarray(x, dtype=np.float64)
+    mean = np.mean(x, axis=0)
+    xc = x - mean
+    lam, vec = np.linalg.eigh(np.cov(xc.T))
+    order = np.argsort(lam)[::-1]
+    lam, vec = lam[order], vec[:, order]
+    comps, _ = _svd_flip_rows(vec[:, :n_components].T)
+    evr = lam[:n_components] / np.sum(lam)
+    return comps, mean, evr, lam[:n_components], xc @ comps.T
+
+
+def cosine_similarity_vec(v1, v2):
+    """useless/scan.py:58-78 for two vectors (0.0 when a norm is 0)."""
+    a, b = np.asarray(v1, dtype=np.float64), np.asarray(v2, dtype=np.float64)
+    na, nb = np.linalg.norm(a), np.linalg.norm(b)
+    if na == 0 or nb == 0:
+        return 0.0
+    return float(np.dot(a, b) / (na * nb))
 
 
 # --------------------------------------------------------------------------

@@ -257,8 +257,56 @@ def make_c1_synth(ref_train=None, ref_mscan=None):
     print("c1_synth: eigenvalues", lam[:3], "sims", [round(float(x[1]), 6) for x in res])
 
 
+def make_manual_v2():
+    """G8: the manual trainer's classes (scripts/manual/train-v2.py:9-72) and the manual
+    scanner's helpers (useless/scan.py:58-98), imported from the reference and run on
+    exact-integer synthetic faces — a Gram-shaped set (n < d) and a covariance-shaped one
+    (n >= d): ManualStandardScaler.fit_transform -> ManualPCA(k).fit_transform, plus
+    ManualPCA.transform / project_face_to_eigenspace of probes and cosine_similarity of
+    vector pairs (including a zero vector)."""
+    sys.modules.setdefault("cv2", _cv2_placeholder())
+    ref_m = _load("ref_manual_train_v2", "scripts/manual/train-v2.py")
+    ref_mscan = _load("ref_manual_scan", "useless/scan.py")
+    res = {}
+    for tag, (n, side, r, seed, k) in {"gram": (150, 20, 40, 21, 20), "cov": (400, 16, 40, 22, 24)}.items():
+        X = orc.int_synth_faces(n, side, r=r, seed=seed)
+        sc = ref_m.ManualStandardScaler()
+        Z = sc.fit_transform(X.astype(np.float64))
+        pca = ref_m.ManualPCA(n_components=k)
+        F = pca.fit_transform(Z)
+        sgn = np.sign(pca.components_[np.arange(k), np.argmax(np.abs(pca.components_), axis=1)])
+        probes = np.clip(X[:6].astype(np.int64) + np.random.default_rng(seed).integers(-9, 10, (6, X.shape[1])),
+                         0, 255).astype(np.uint8)
+        Fp = pca.transform(sc.transform(probes.astype(np.float64)))
+        # the manual scanner's projection with (d, k) eigenfaces, raw pixels
+        E = (pca.components_ * sgn[:, None]).T
+        P = np.stack([ref_mscan.project_face_to_eigenspace(v.astype(np.float64), E, sc.mean_) for v in probes])
+        res.update({f"{tag}_n": n, f"{tag}_side": side, f"{tag}_r": r, f"{tag}_seed": seed, f"{tag}_k": k,
+                    f"{tag}_scaler_mean": sc.mean_, f"{tag}_scaler_scale": sc.scale_,
+                    f"{tag}_components": pca.components_ * sgn[:, None],
+                    f"{tag}_evr": pca.explained_variance_ratio_, f"{tag}_features": F * sgn[None, :],
+                    f"{tag}_probes": probes, f"{tag}_probe_features": Fp * sgn[None, :],
+                    f"{tag}_projected": P})
+        o_c, o_m, o_evr, _, o_f = orc.manual_pca_cov(orc.manual_standard_scaler(X)[0], k)
+        print(tag, "oracle vs reference: comps", float(np.max(np.abs(o_c - pca.components_ * sgn[:, None]))),
+              "evr", float(np.max(np.abs(o_evr - pca.explained_variance_ratio_))))
+    rng = np.random.default_rng(31)
+    a = rng.standard_normal((6, 50))
+    b = rng.standard_normal((6, 50))
+    b[1] = 3.0 * a[1]       # parallel: similarity 1
+    b[2] = -a[2]            # anti-parallel: -1
+    a[3] = 0.0              # zero vector: 0.0 (:73-74)
+    b[4] = a[4] + 1e-9      # near-identical
+    cs = np.array([ref_mscan.cosine_similarity(x, y) for x, y in zip(a, b)], dtype=np.float64)
+    res.update(cos_a=a, cos_b=b, cos_sim=cs)
+    np.savez_compressed(os.path.join(HERE, "manual_v2.npz"), **res)
+    print("manual_v2: cos", cs)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "c1":
         make_c1_synth()
+    elif len(sys.argv) > 1 and sys.argv[1] == "manual_v2":
+        make_manual_v2()
     else:
         main()

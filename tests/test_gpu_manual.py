@@ -1,0 +1,137 @@
+"""Float input on the fit boundary (ef_fit_ex / ef_colstats) and the manual surface
+(eigenface.manual: ManualPCA, ManualStandardScaler, project_face_to_eigenspace,
+cosine_similarity) against the reference's own outputs (tests/golden/manual_v2.npz, made
+by running scripts/manual/train-v2.py and useless/scan.py) and the fp64 oracle.
+
+Tolerances: statistics 1e-12 relative; eigenvalues / ratios 1e-9 relative; components
+1e-6 absolute (unit vectors, gapped spectrum); fp64 training features 1e-6 of their
+max; fp32 projections (transform, project_face_to_eigenspace) 2e-6 x sum|p - mu||w|;
+cosine 1e-6 (fp32 inputs, fp64 score)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import eigenface_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(tag):
+    g = golden("manual_v2.npz")
+    X = orc.int_synth_faces(int(g[f"{tag}_n"]), int(g[f"{tag}_side"]), r=int(g[f"{tag}_r"]),
+                            seed=int(g[f"{tag}_seed"]))
+    return g, X
+
+
+def _proj_bound(P, mean, W):
+    return 2e-6 * (np.abs(P.astype(np.float64) - mean) @ np.abs(W)) + 1e-9
+
+
+@pytest.mark.parametrize("tag", ["gram", "cov"])
+def test_manual_trainer_matches_reference(eng, tag):
+    from eigenface import ManualPCA, ManualStandardScaler
+    g, X = _data(tag)
+    k = int(g[f"{tag}_k"])
+    sc = ManualStandardScaler()
+    Z = sc.fit_transform(X)
+    np.testing.assert_allclose(sc.mean_, g[f"{tag}_scaler_mean"], rtol=1e-13)
+    np.testing.assert_allclose(sc.scale_, g[f"{tag}_scaler_scale"], rtol=1e-12)
+    assert not np.array_equal(Z, np.rint(Z))  # standardised data: the float fit path
+    pca = ManualPCA(n_components=k)
+    F = pca.fit_transform(Z)
+    np.testing.assert_allclose(pca.explained_variance_ratio_, g[f"{tag}_evr"], rtol=1e-9)
+    np.testing.assert_allclose(pca.components_, g[f"{tag}_components"], atol=1e-6)
+    ref_F = g[f"{tag}_features"]
+    np.testing.assert_allclose(F, ref_F, atol=1e-6 * np.abs(ref_F).max())
+    # transform of new faces: scaler (host elementwise) + GPU projection
+    probes = g[f"{tag}_probes"]
+    Zp = sc.transform(probes)
+    Fp = pca.transform(Zp)
+    W = pca.components_.T
+    assert np.all(np.abs(Fp - g[f"{tag}_probe_features"]) <= _proj_bound(Zp, pca.mean_, W))
+    # useless/scan.py:80-98 on raw pixels with (d, k) eigenfaces
+    from eigenface import project_face_to_eigenspace
+    E = g[f"{tag}_components"].T
+    P = project_face_to_eigenspace(probes, E, g[f"{tag}_scaler_mean"])
+    assert P.shape == (len(probes), k)
+    assert np.all(np.abs(P - g[f"{tag}_projected"]) <= _proj_bound(probes, g[f"{tag}_scaler_mean"], E))
+    p1 = project_face_to_eigenspace(probes[0].astype(np.float64), E, g[f"{tag}_scaler_mean"])
+    assert p1.shape == (k,)
+    np.testing.assert_allclose(p1, P[0], atol=1e-4 * np.abs(P[0]).max())
+
+
+def test_cosine_similarity_matches_reference(eng):
+    from eigenface import cosine_similarity
+    g = golden("manual_v2.npz")
+    got = np.array([cosine_similarity(a, b) for a, b in zip(g["cos_a"], g["cos_b"])])
+    np.testing.assert_allclose(got, g["cos_sim"], atol=1e-6)
+    assert got[3] == 0.0  # zero vector branch (useless/scan.py:73-74)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("n,d,k", [(120, 600, 16), (700, 256, 24)])
+def test_float_fit_vs_oracle(eng, dtype, n, d, k):
+    """Engine.fit on non-integral float input (Gram path n < d, covariance path n >= d):
+    manual_pca semantics against the fp64 oracle on the same (dtype-rounded) numbers."""
+    rng = np.random.default_rng(n + d)
+    basis = np.linalg.qr(rng.standard_normal((d, 40)))[0]
+    X = (rng.standard_normal((n, 40)) * (30.0 / np.sqrt(np.arange(1, 41)))) @ basis.T
+    X = (X + 0.3 * rng.standard_normal((n, d)) + 5.0).astype(dtype)
+    r = eng.fit(X, k, standardize=False)
+    o_eig, o_mean, o_proj, o_lam = orc.manual_pca(X.astype(np.float64), k)
+    np.testing.assert_allclose(r.mean, o_mean, rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(r.eigenvalues, o_lam, rtol=1e-9)
+    s = np.sign((r.components.T * o_eig).sum(0))
+    assert np.all(s == 1)  # both follow the svd_flip rule
+    np.testing.assert_allclose(r.components.T, o_eig, atol=1e-6)
+    np.testing.assert_allclose(r.projection, o_proj, atol=1e-6 * np.abs(o_proj).max())
+
+
+@pytest.mark.parametrize("n,d", [(200, 300), (500, 144)])
+def test_float_standardized_fit_vs_oracle(eng, n, d):
+    """EF_FIT_STANDARDIZE on float input: StandardScaler (sklearn constant-feature rule)
+    + PCA(full) (train-v4.py:126-146) against the oracle."""
+    rng = np.random.default_rng(d)
+    X = rng.standard_normal((n, 12)) @ rng.standard_normal((12, d)) * 3.0 + rng.standard_normal((n, d))
+    X[:, 5] = 2.5  # a constant feature: scale 1
+    r = eng.fit(X, 10, standardize=True)
+    o = orc.train_pca_model(X, 10)
+    mean, var, scale = orc.standard_scaler_fit(X)
+    np.testing.assert_allclose(r.mean, mean, rtol=1e-13)
+    np.testing.assert_allclose(r.var, var, rtol=1e-11, atol=1e-13)
+    np.testing.assert_allclose(r.scale, scale, rtol=1e-11)
+    assert r.scale[5] == 1.0
+    np.testing.assert_allclose(r.eigenvalues, o["pca"]["explained_variance_"], rtol=1e-9)
+    np.testing.assert_allclose(r.components, o["pca"]["components_"], atol=1e-6)
+    np.testing.assert_allclose(r.projection, o["face_features"], atol=1e-6 * np.abs(o["face_features"]).max())
+
+
+def test_colstats_uint8_exact_and_float_two_pass(eng):
+    rng = np.random.default_rng(3)
+    X8 = rng.integers(0, 256, (3001, 517), dtype=np.uint8)
+    X8[:, 7] = 9
+    m, v = eng.colstats(X8)
+    x = X8.astype(np.float64)
+    np.testing.assert_allclose(m, x.mean(0), rtol=1e-15)
+    np.testing.assert_allclose(v, x.var(0), rtol=1e-14)
+    assert v[7] == 0.0
+    Xf = rng.standard_normal((777, 300)) * 1e3 + 1e6  # large offset: the two-pass form matters
+    m, v = eng.colstats(Xf)
+    np.testing.assert_allclose(m, Xf.mean(0), rtol=1e-14)
+    np.testing.assert_allclose(v, Xf.var(0), rtol=1e-9)
+
+
+def test_manual_pca_accepts_float_data(eng):
+    """manual_pca (useless/train.py:56-128) on non-integral float64 data (formerly
+    rejected): the float path, equal to the oracle; integral floats still take the exact
+    uint8 path and give the same numbers as uint8 input."""
+    from eigenface import manual_pca
+    x8, _ = orc.synth_faces(90, 16, r=12, seed=5)
+    e1, m1, p1, l1 = manual_pca(x8.astype(np.float64), 8)
+    e2, m2, p2, l2 = manual_pca(x8, 8)
+    np.testing.assert_array_equal(l1, l2)
+    xf = x8.astype(np.float64) / 255.0 - 0.5
+    e, m, p, lam = manual_pca(xf, 8)
+    o_e, o_m, o_p, o_l = orc.manual_pca(xf, 8)
+    np.testing.assert_allclose(lam, o_l, rtol=1e-9)
+    np.testing.assert_allclose(e, o_e * np.sign((e * o_e).sum(0)), atol=1e-6)
