@@ -943,7 +943,8 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
     hipError_t e = launch_split_rows(s, qpad, bpad, KP, Q3);
     if (e != hipSuccess) return e;
     timer_begin(c, EF_KERNEL_SEARCH, tev);
-    e = launch_search_wide(s, KP, M, false, true, pl, Q3, G3, aux, n, bpad, ws);
+    const int variant = c->opt_search_split_bf16 == 2 ? 2 : 1;  // 16x16x32 unless the 32x32x16 kernel is asked for
+    e = launch_search_wide(s, KP, M, false, variant, pl, Q3, G3, aux, n, bpad, ws);
     timer_end(c, tev);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
@@ -951,7 +952,7 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
     const dim3 pgrid((unsigned)((b + 3) / 4));
     hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
                        g_offset, gmax2, ws, keys);
-    e = launch_search_wide(s, KP, M, true, true, pl, Q3, G3, aux, n, bpad, ws);
+    e = launch_search_wide(s, KP, M, true, variant, pl, Q3, G3, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
     return hipGetLastError();
@@ -996,7 +997,7 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
   if constexpr (wide) {
-    const hipError_t e = launch_search_wide(s, KP, M, false, false, pl, qpad, G, aux, n, bpad, ws);
+    const hipError_t e = launch_search_wide(s, KP, M, false, 0, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
 #ifdef EF_DIAGNOSTICS
@@ -1025,7 +1026,7 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
                      gmax2, ws, keys);
   // queued (fp32-ambiguous) probes: collect + fp64 resolve; both exit at once when none
   if constexpr (wide) {
-    e = launch_search_wide(s, KP, M, true, false, pl, qpad, G, aux, n, bpad, ws);
+    e = launch_search_wide(s, KP, M, true, 0, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
     hipLaunchKernelGGL((search_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,

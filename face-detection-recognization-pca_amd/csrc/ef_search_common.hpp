@@ -57,8 +57,9 @@ constexpr int kWideRowTile = 128;    // gallery rows per tile
 constexpr int kWideProbeTile = 128;  // probes per workgroup
 constexpr int kWide3RowTile = 256;    // split-bf16 wide kernel: gallery rows per tile
 constexpr int kWide3ProbeTile = 256;  // split-bf16 wide kernel: probes per workgroup
-// s3: qpad and G are the split-bf16 copies (split-bf16 scan)
-hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, bool s3, const SearchPlan& pl,
+// s3: qpad and G are the split-bf16 copies (split-bf16 scan); 1 = the 16x16x32 kernel,
+// 2 = the 32x32x16 one (EF_OPT_SEARCH_SPLIT_BF16), 0 = the fp32 scan
+hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, int s3, const SearchPlan& pl,
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
                               const SearchWs& ws);
 

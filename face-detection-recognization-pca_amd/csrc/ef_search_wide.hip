@@ -37,6 +37,14 @@ constexpr int WSL = WR * WBK;       // floats per gallery slice (= per probe sli
 static_assert(WR == 128 && WP == 128, "4 waves x 32 probes, 4 x 32-row blocks");
 
 typedef short bf16x8w __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// min of three floats as one v_min3_f32, without the compiler's IEEE-mode canonicalisation
+// of each input (scores are finite or +inf, never NaN)
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ bf16x8w as_bf16x8w(const float4& v) {
   bf16x8w r;
   __builtin_memcpy(&r, &v, 16);
@@ -583,30 +591,355 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-bf16 wide scan on v_mfma_f32_16x16x32_bf16 (EF_OPT_SEARCH_SPLIT_BF16 = 1; 2 keeps
+// search_wide3_kernel).  Same plan, tiles, DMA and SearchWs contract as search_wide3_kernel:
+// 256 rows x 256 probes per workgroup, 8 waves, wave w = probes 64 (w & 3) ..+64 (four
+// 16-probe B blocks pb) x rows 128 (w >> 2) ..+128 (eight 16-row A blocks rb).  Per 32-k
+// slice lane (qd = lane >> 4, r16 = lane & 15) supplies row r16 of each A block and probe
+// r16 of each B block for elements 8 qd .. 8 qd + 7 of the slice — chunk 2 qd (hi) and
+// 2 qd + 1 (lo) of the 128-B slice row: 16 + 8 ds_read_b128 feed 96 MFMAs of 16 cycles
+// (the 32x32x16 kernel: the same 24 reads for 48 MFMAs of 32 cycles).  Under the chip's
+// clock on random bf16 operands the 16x16x32 shape delivers ~1.12-1.15x the FLOP/s of
+// 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).
+// LDS swizzle: ds_read_b128 serves lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... in one
+// LDS cycle each (MI355X_MICROARCH.md §LDS): rows 0-3 / 12-15 at chunk c meet rows 4-11 at
+// chunk c + 2.  Physical chunk = logical ^ s(row) with s(row) = (row >> 1) & 5 (s in
+// {0, 1, 4, 5}, so c ^ s and (c + 2) ^ s' never coincide within a lane group and the row
+// pairs 2m, 2m + 1 fill both 32-bank halves): every group covers all 64 banks.  The wide3
+// swizzle (row >> 1) & 7 would be 2-way conflicted here.
+// Accumulator layout: acc[rb][pb][r] = row 16 rb + 4 qd + r of probe 16 pb + r16.
+template <int KP, int METRIC, bool COLLECT>
+__global__ __launch_bounds__(512, 1) void search_wide16_kernel(
+    const float* __restrict__ q3, const float* __restrict__ G3, const float* __restrict__ aux, int64_t n,
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
+  constexpr int NS = KP / WBK;
+  __shared__ __attribute__((aligned(16))) float smem[4 * W3SL + 2 * W3R];
+
+  auto body = [&](const int gc, const int pt, const int n_amb) {
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qd = lane >> 4, r16 = lane & 15;
+  const int pg = wave & 3, rh = wave >> 2;
+
+  const int64_t tiles_total = (n + W3R - 1) / W3R;
+  const int64_t t0 = (int64_t)gc * tiles_per_chunk;
+  const int64_t t1 = t0 + tiles_per_chunk < tiles_total ? t0 + tiles_per_chunk : tiles_total;
+  int64_t sl0[4];  // this lane's probe slots (probe 16 pb + r16 of the wave's 64)
+#pragma unroll
+  for (int pb = 0; pb < 4; ++pb) sl0[pb] = (int64_t)pt * W3P + 64 * pg + 16 * pb + r16;
+
+  if (t0 >= t1) {
+    if constexpr (!COLLECT) {
+      if (qd == 0 && rh == 0) {
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          ws.part_key[(int64_t)gc * bpad + sl0[pb]] = LLONG_MAX;
+          ws.part_b2[(int64_t)gc * bpad + sl0[pb]] = __builtin_inff();
+        }
+      }
+    }
+    return;
+  }
+
+  // DMA geometry of search_wide3_kernel with this kernel's swizzle: lane l of piece j
+  // carries row 8 j + (l >> 3), physical chunk l & 7 = logical chunk (l & 7) ^ s(row),
+  // s(row) = (row >> 1) & 5 = (4 jj + (l >> 4)) & 5.
+  const int prow = lane >> 3;
+  unsigned goff[4], qoff[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int slot = pt * W3P + (wave * 4 + jj) * 8 + prow;
+    int qrow = slot;
+    if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
+    const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 5)) * 16);
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
+  }
+  float thr[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  if constexpr (COLLECT) {
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb)
+      if (sl0[pb] < n_amb) thr[pb] = ws.thr[sl0[pb]];
+  }
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qoff[jj]));
+  asm volatile("" ::"v"(thr[0]), "v"(thr[1]), "v"(thr[2]), "v"(thr[3]));
+
+  const unsigned lds_base = lds_addr(smem);
+  const int64_t n_it = (t1 - t0) * NS;
+  // DMA piece p (0..7) of slice it into buffer buf: p >> 1 = this wave's piece jj, p & 1 =
+  // gallery (0) or probes (1)
+  auto issue_piece = [&](int64_t it, int buf, int p) {
+    const int64_t t = t0 + it / NS;
+    const int sl = (int)(it % NS);
+    const int jj = p >> 1, j = wave * 4 + jj;
+    if ((p & 1) == 0) {
+      const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
+      const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * KP + sl * WBK);
+      unsigned go = goff[jj];
+      if (nrem < W3R) {  // tail tile: rows past the end re-read the last row (masked later)
+        const unsigned row = go / (KP * 4);
+        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
+      }
+      glds16s(go, gb, lds_base + (unsigned)((buf * 2 * W3SL + j * 256) * 4));
+    } else {
+      const unsigned long long qb = (unsigned long long)(size_t)(q3 + sl * WBK);
+      glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * W3SL + W3SL + j * 256) * 4));
+    }
+  };
+  auto issue = [&](int64_t it, int buf) {
+    const int64_t t = t0 + it / NS;
+    const int sl = (int)(it % NS);
+    const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
+#if !EF_WIDE_INTERLEAVE
+#pragma unroll
+    for (int p = 0; p < 8; ++p) issue_piece(it, buf, p);
+#endif
+    if (sl == 0 && wave == 0) {  // the tile's ||g||^2 (L2) or 1/||g|| (cosine)
+      const unsigned long long ab = (unsigned long long)(size_t)(aux + t * W3R);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 64 * q + lane;
+        const unsigned ao = r < nrem ? (unsigned)r * 4 : (unsigned)(nrem - 1) * 4;
+        glds4s(ao, ab, lds_base + (unsigned)((4 * W3SL + ((t - t0) & 1) * W3R + 64 * q) * 4));
+      }
+    }
+  };
+
+  const float INF = __builtin_inff();
+  float b1[4] = {INF, INF, INF, INF}, b2[4] = {INF, INF, INF, INF};
+  int i1[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+  // v[rb][r] = row rowbase + 16 rb + 4 qd + r (increasing with (rb, r): first-min in lane)
+  auto consume = [&](const f32x4 (&v)[8], int rowbase, int pb) {
+    if constexpr (COLLECT) {
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (v[rb][r] <= thr[pb]) {
+            const int pos = atomicAdd(&ws.cand_cnt[sl0[pb]], 1);
+            if (pos < kCandMax) ws.cand[sl0[pb] * kCandMax + pos] = rowbase + 16 * rb + 4 * qd + r;
+          }
+        }
+    } else {
+      // 32 values in 16 v_min3 (fminf would re-canonicalise every MFMA result first:
+      // one v_max_f32 x, x per input in IEEE mode)
+      float mn = v[0][0];
+#pragma unroll
+      for (int e = 1; e + 1 < 32; e += 2) mn = min3_raw(mn, v[e >> 2][e & 3], v[(e + 1) >> 2][(e + 1) & 3]);
+      mn = fminf(mn, v[7][3]);
+      if (!__any(mn < b2[pb])) return;  // exact skip (ef_search.hip consume)
+      float m1 = INF, m2 = INF;
+      int ir = 0;
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = v[rb][r];
+          const bool lt = x < m1;
+          m2 = __builtin_amdgcn_fmed3f(m1, x, m2);
+          ir = lt ? 16 * rb + r : ir;
+          m1 = lt ? x : m1;
+        }
+      const bool lt = m1 < b1[pb];
+      b2[pb] = lt ? fminf(b1[pb], m2) : fminf(b2[pb], m1);
+      i1[pb] = lt ? rowbase + ir + 4 * qd : i1[pb];
+      b1[pb] = lt ? m1 : b1[pb];
+    }
+  };
+
+  issue(0, 0);
+  dma_wait_all();
+  __syncthreads();
+
+  const int sw = (r16 >> 1) & 5;  // s(row) of every row / probe this lane reads
+  const int ph = ((2 * qd) ^ sw) * 4, pl = ((2 * qd + 1) ^ sw) * 4;
+  f32x4 acc[8][4];
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int buf = (int)(it & 1);
+    const int sl = (int)(it % NS);
+    const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
+#if EF_WIDE_ABL == 3
+    if (it + 1 < 2)  // diagnostic builds only: no slice DMA after the first (results invalid)
+#else
+    if (it + 1 < n_it)
+#endif
+      issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+    if (sl == 0) {
+      // L2: start from -||g||^2 / 2 and accumulate q.g (-2 acc = ||g||^2 - 2 q.g); cosine: 0
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (METRIC == EF_METRIC_L2) {
+          const float4 x = *reinterpret_cast<const float4*>(sAux + 16 * rb + 4 * qd);
+          a = f32x4{-0.5f * x.x, -0.5f * x.y, -0.5f * x.z, -0.5f * x.w};
+        }
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) acc[rb][pb] = a;
+      }
+    }
+    const float* sg = smem + buf * 2 * W3SL + (128 * rh + r16) * WBK;
+    const float* sq = smem + buf * 2 * W3SL + W3SL + (64 * pg + r16) * WBK;
+    bf16x8w bh[4], bl[4];
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      bh[pb] = as_bf16x8w(*reinterpret_cast<const float4*>(sq + 16 * pb * WBK + ph));
+      bl[pb] = as_bf16x8w(*reinterpret_cast<const float4*>(sq + 16 * pb * WBK + pl));
+    }
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      const bf16x8w ah = as_bf16x8w(*reinterpret_cast<const float4*>(sg + 16 * rb * WBK + ph));
+      const bf16x8w al = as_bf16x8w(*reinterpret_cast<const float4*>(sg + 16 * rb * WBK + pl));
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[pb], acc[rb][pb], 0, 0, 0);
+        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[pb], acc[rb][pb], 0, 0, 0);
+        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[pb], acc[rb][pb], 0, 0, 0);
+      }
+#if EF_WIDE_INTERLEAVE
+      // one DMA piece of slice it + 1 per 12 MFMAs instead of a burst of 8 at the top
+      // (buffer buf ^ 1 was released by the previous slice's barrier)
+      if (it + 1 < n_it) issue_piece(it + 1, buf ^ 1, rb);
+#endif
+    }
+    if (sl == NS - 1) {
+      const int64_t t = t0 + it / NS;
+      const int tbase = (int)(t * W3R) + 128 * rh;
+      const bool tail = (t + 1) * W3R > n;
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb) {
+        const float4 x = *reinterpret_cast<const float4*>(sAux + 16 * rb + 4 * qd);
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          if constexpr (METRIC == EF_METRIC_L2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[rb][pb][r] *= -2.f;
+          } else {  // -(q.g) * (1/||g||)
+            acc[rb][pb][0] *= -x.x;
+            acc[rb][pb][1] *= -x.y;
+            acc[rb][pb][2] *= -x.z;
+            acc[rb][pb][3] *= -x.w;
+          }
+          if (tail) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (tbase + 16 * rb + 4 * qd + r >= n) acc[rb][pb][r] = INF;
+          }
+        }
+      }
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const f32x4 v[8] = {acc[0][pb], acc[1][pb], acc[2][pb], acc[3][pb],
+                            acc[4][pb], acc[5][pb], acc[6][pb], acc[7][pb]};
+#if EF_WIDE_ABL == 2
+        {  // diagnostic builds only: the screen's min without the top-2 update (every
+           // accumulator stays live, so no MFMA is dead code)
+          float mn = v[0][0];
+#pragma unroll
+          for (int e = 1; e + 1 < 32; e += 2) mn = min3_raw(mn, v[e >> 2][e & 3], v[(e + 1) >> 2][(e + 1) & 3]);
+          b1[pb] = fminf(b1[pb], fminf(mn, v[7][3]));
+        }
+#else
+        consume(v, tbase, pb);
+#endif
+      }
+    }
+#if EF_WIDE_ABL != 1
+    dma_wait_all();
+    __syncthreads();  // slice it+1 landed; everyone is done reading buffer buf
+#endif
+  }
+
+  if constexpr (!COLLECT) {
+    // the four row quarters (lanes r16, +16, +32, +48), then the two row halves via LDS
+    float* xb = smem;  // [4 pg][4 pb][16] x (b1, b2, i1); the loop's last barrier freed LDS
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+#pragma unroll
+      for (int off = 16; off <= 32; off <<= 1) {
+        const float ob1 = __shfl_xor(b1[pb], off);
+        const int oi1 = __shfl_xor(i1[pb], off);
+        const float ob2 = __shfl_xor(b2[pb], off);
+        const bool other = ob1 < b1[pb] || (ob1 == b1[pb] && oi1 < i1[pb]);
+        const float lose = other ? b1[pb] : ob1;
+        b2[pb] = fminf(fminf(b2[pb], ob2), lose);
+        if (other) { b1[pb] = ob1; i1[pb] = oi1; }
+      }
+      if (rh == 1 && qd == 0) {
+        const int o = ((pg * 4 + pb) * 16 + r16) * 3;
+        xb[o] = b1[pb];
+        xb[o + 1] = b2[pb];
+        xb[o + 2] = __int_as_float(i1[pb]);
+      }
+    }
+    __syncthreads();
+    if (rh == 0 && qd == 0) {
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const int o = ((pg * 4 + pb) * 16 + r16) * 3;
+        const float ob1 = xb[o], ob2 = xb[o + 1];
+        const int oi1 = __float_as_int(xb[o + 2]);
+        const bool other = ob1 < b1[pb] || (ob1 == b1[pb] && oi1 < i1[pb]);
+        const float lose = other ? b1[pb] : ob1;
+        b2[pb] = fminf(fminf(b2[pb], ob2), lose);
+        if (other) { b1[pb] = ob1; i1[pb] = oi1; }
+        const int64_t po = (int64_t)gc * bpad + sl0[pb];
+        ws.part_key[po] = i1[pb] == INT_MAX ? LLONG_MAX : pack_key(b1[pb], (unsigned)i1[pb]);
+        ws.part_b2[po] = b2[pb];
+      }
+    }
+  }
+  };  // body
+  if constexpr (COLLECT) {
+    const int n_amb = *ws.amb_count;
+    const int items = ((n_amb + 256 - 1) / 256) * n_ptiles;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item % n_ptiles, item / n_ptiles, n_amb);
+  } else {
+    const int total = gridDim.x;  // host guarantees total % 8 == 0
+    const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int bsz = cblk * pblk;
+    const int blk = lin / bsz, rr = lin - blk * bsz;
+    const int nbp = n_ptiles / pblk;
+    body((blk / nbp) * cblk + rr / pblk, (blk % nbp) * pblk + rr % pblk, 0);
+  }
+}
+
 template <int KP, int M>
-static hipError_t wide3_t(hipStream_t s, bool collect, const SearchPlan& pl, const float* q3, const float* G3,
-                          const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
+static hipError_t wide3_t(hipStream_t s, bool collect, bool w16, const SearchPlan& pl, const float* q3,
+                          const float* G3, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0 || bpad % W3P != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
-  if (collect)
+  if (w16) {
+    if (collect)
+      hipLaunchKernelGGL((search_wide16_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux,
+                         n, pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
+    else
+      hipLaunchKernelGGL((search_wide16_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
+                         pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+  } else if (collect) {
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux, n,
                        pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
-  else
+  } else {
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
                        pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+  }
   return hipGetLastError();
 }
 
 template <int KP, int M>
-static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan& pl, const float* qpad,
+static hipError_t wide_t(hipStream_t s, bool collect, int s3, const SearchPlan& pl, const float* qpad,
                          const float* G, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
-  if (s3) return wide3_t<KP, M>(s, collect, pl, qpad, G, aux, n, bpad, ws);  // plan from search_plan(.., true)
+  // plan from search_plan(.., true); s3 = 1: the 16x16x32 kernel, 2: the 32x32x16 one
+  if (s3) return wide3_t<KP, M>(s, collect, s3 != 2, pl, qpad, G, aux, n, bpad, ws);
   if (collect)
     hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,
                        pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
@@ -616,7 +949,7 @@ static hipError_t wide_t(hipStream_t s, bool collect, bool s3, const SearchPlan&
   return hipGetLastError();
 }
 
-hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, bool s3, const SearchPlan& pl,
+hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, int s3, const SearchPlan& pl,
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
                               const SearchWs& ws) {
   const bool l2 = metric == EF_METRIC_L2;

@@ -13,7 +13,11 @@ an exact-integer generator, so the GPU test regenerates the identical pixels on 
   pixel of every component enters the check;
 * ``comps_px`` = components_ at 256 fixed pixel positions;
 * ``features`` = fit_transform rows 0..63;
-* ``scaler_mean`` / ``scaler_scale``.
+* ``scaler_mean`` / ``scaler_scale``;
+* ``top_idx`` / ``top_val`` (k x 2): per component, the pixels of its two largest |entries|
+  and their (svd_flip-signed) values — the sklearn sign rule (extmath.py:946-952) keys on
+  the first, so a component whose two are nearly tied may legitimately come out with the
+  other sign from a fit whose rounding differs; the GPU test allows a flip only there.
 
 The oracle itself is pinned against the reference's own outputs at smaller shapes
 (tests/golden/make_goldens.py, tests/test_oracle_golden.py), and pca_cov_fit against
@@ -51,6 +55,7 @@ def main():
     print(f"oracle fit in {time.time() - t0:.1f} s")
     R, px = probe_matrices(X.shape[1])
     comps = res["components_"]
+    top_idx = np.argsort(-np.abs(comps), axis=1, kind="stable")[:, :2]
     np.savez_compressed(
         os.path.join(HERE, "fit_c3.npz"),
         n=N, side=SIDE, r=R_FACT, seed=SEED, k=K,
@@ -58,6 +63,7 @@ def main():
         comps_R=comps @ R, comps_px=comps[:, px], px=px,
         features=res["fit_transform"][:64],
         scaler_mean=res["scaler"][0], scaler_scale=res["scaler"][2],
+        top_idx=top_idx, top_val=np.take_along_axis(comps, top_idx, axis=1),
     )
     lam = res["explained_variance_"]
     print("top eigenvalues", lam[:4], "lambda_128", lam[-1], "min rel gap",

@@ -173,10 +173,12 @@ def test_split_wide_xcd_deal(split, b):
         np.testing.assert_array_equal(k3, k32)
 
 
-@pytest.mark.parametrize("k", [100, 128])
+@pytest.mark.parametrize("k", [100, 128, 256, 300, 512])
 def test_split_kernel_shapes_agree(split, k):
-    """k in (64, 128]: the default 16x16x32 split kernel and the 32x32x16 one (option 2)
-    return the fp32 scan's keys, on random probes and on sub-bf16 near-ties."""
+    """k in (64, 128] and the wide scans (k > 128): the default 16x16x32 split kernels
+    (search16_kernel, search_wide16_kernel) and the 32x32x16 ones (option 2:
+    search_kernel<S3>, search_wide3_kernel) return the fp32 scan's keys, on random probes
+    and on sub-bf16 near-ties."""
     rng = np.random.default_rng(k + 5)
     n, b = 7001, 700
     g = rng.standard_normal((n, k)).astype(np.float32)

@@ -7,7 +7,7 @@ O=gpurun_out/$1
 CFG=${2:-c3}
 mkdir -p $O
 B="bench.py --config $CFG --no-cpu --no-fit --no-image --no-c2 --no-split --search split_bf16 --steps 5 --warmup 2 --repeats 1"
-R="search(16)?_(wide3_)?kernel"
+R="search(16)?_(wide3_|wide16_)?kernel"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B > $O/t.txt 2>&1 || exit $?
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$R" --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $B > $O/pf.txt 2>&1 || exit $?
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$R" --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $B > $O/pw.txt 2>&1 || exit $?
