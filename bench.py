@@ -170,6 +170,20 @@ def pmc_traffic(config):
     return None, None
 
 
+def bf16_ceiling(loop):
+    """TFLOP/s a bare bf16 MFMA loop of this shape (operands re-read from LDS, 2 waves per
+    SIMD, every CU busy, random data) holds under the chip's power-limited clock: the
+    newest committed tools/micro/bf16_clock.cpp capture (profiles/r*/bf16_clock.json)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bf16_clock.json")), reverse=True):
+        for line in open(f):
+            if line.startswith("{"):
+                rec = json.loads(line)
+                if rec.get("loop") == loop and rec.get("threads_per_cu") == 512:
+                    return rec["tflops"], os.path.relpath(f, ROOT)
+    return None
+
+
 def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu=20_000):
     """Headline secondary metric "covariance+SVD fit sec" on config 3's shape: train-v4.py's
     train_pca_model semantics (StandardScaler + PCA, k=128) on 1M synthetic 128x128 uint8
@@ -762,13 +776,21 @@ def main():
             if split:
                 mflops = 3.0 * 2.0 * bsz * (hi - lo) * kpad
                 a = mflops / (avg_ms * 1e-3) / 1e12
-                return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
-                        + "<split-bf16> (3 x bf16 MFMA per fp32 "
-                        "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
-                        "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
-                        "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
-                        "algorithmic_flops_per_launch": flops_launch,
-                        "algorithmic_TFLOPs": round(flops_launch / (avg_ms * 1e-3) / 1e12, 2)}
+                shape16 = args.split_opt != 2 and k > 64
+                kname = ("search16_kernel" if shape16 else "search_kernel<S3>") if k <= 128 else \
+                    ("search_wide16_kernel" if shape16 else "search_wide3_kernel")
+                rec = {"bound": "mfma", "kernel": kname + " (split-bf16: 3 x bf16 MFMA per fp32 "
+                       "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
+                       "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
+                       "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
+                       "algorithmic_flops_per_launch": flops_launch,
+                       "algorithmic_TFLOPs": round(flops_launch / (avg_ms * 1e-3) / 1e12, 2)}
+                ceil = bf16_ceiling("16x16x32 lds" if shape16 else "32x32x16 lds")
+                if ceil:  # the power-limited rate of a bare LDS-fed loop of the same MFMA shape
+                    rec["power_limited_ceiling_TFLOPs"] = ceil[0]
+                    rec["frac_of_power_limited_ceiling"] = round(a / ceil[0], 4)
+                    rec["ceiling_source"] = ceil[1]
+                return rec
             a = flops_launch / (avg_ms * 1e-3) / 1e12
             return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
                     + " (fp32 MFMA distance GEMM + fused arg-best)", "achieved": round(a, 2),

@@ -574,6 +574,9 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
       if (value < 1) return set_err(c, EF_E_INVALID, "EF_OPT_JPEG_PART_FILES must be >= 1");
       c->opt_jpeg_part_files = value;
       return EF_OK;
+    case EF_OPT_FIT_CHEBYSHEV:
+      c->opt_fit_chebyshev = value != 0;
+      return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16:
       if (value < 0 || value > 2) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1 or 2");
       c->opt_search_split_bf16 = value;
@@ -594,6 +597,7 @@ int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
     case EF_OPT_JPEG_CHUNK_BITS: *value = c->opt_jpeg_chunk_bits; return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16: *value = c->opt_search_split_bf16; return EF_OK;
     case EF_OPT_JPEG_PART_FILES: *value = c->opt_jpeg_part_files; return EF_OK;
+    case EF_OPT_FIT_CHEBYSHEV: *value = c->opt_fit_chebyshev; return EF_OK;
     default: return EF_E_INVALID;
   }
 }

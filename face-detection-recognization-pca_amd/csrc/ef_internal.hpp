@@ -79,6 +79,7 @@ struct ef_ctx {
   int64_t opt_jpeg_chunk_bits = 0;
   int64_t opt_search_split_bf16 = 0;
   int64_t opt_jpeg_part_files = 8192;
+  int64_t opt_fit_chebyshev = 1;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;

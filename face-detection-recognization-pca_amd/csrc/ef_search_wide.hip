@@ -26,6 +26,9 @@ namespace ef {
 #ifndef EF_WIDE_ABL
 #define EF_WIDE_ABL 0
 #endif
+#ifndef EF_WIDE_STAGGER  // wide16: n > 0 = the upper four waves issue their DMA after A block n - 1
+#define EF_WIDE_STAGGER 2  // measured: 8.96 -> 8.76 ms at C5 (1: 8.83, 4: 9.03, 6: 9.36)
+#endif
 #ifndef EF_WIDE_INTERLEAVE
 #define EF_WIDE_INTERLEAVE 0
 #endif
@@ -694,10 +697,8 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     const int64_t t = t0 + it / NS;
     const int sl = (int)(it % NS);
     const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
-#if !EF_WIDE_INTERLEAVE
 #pragma unroll
     for (int p = 0; p < 8; ++p) issue_piece(it, buf, p);
-#endif
     if (sl == 0 && wave == 0) {  // the tile's ||g||^2 (L2) or 1/||g|| (cosine)
       const unsigned long long ab = (unsigned long long)(size_t)(aux + t * W3R);
 #pragma unroll
@@ -763,11 +764,17 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     const int sl = (int)(it % NS);
     const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
 #if EF_WIDE_ABL == 3
-    if (it + 1 < 2)  // diagnostic builds only: no slice DMA after the first (results invalid)
+    const bool more = it + 1 < 2;  // diagnostic builds only: no slice DMA after the first (results invalid)
 #else
-    if (it + 1 < n_it)
+    const bool more = it + 1 < n_it;
 #endif
-      issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+#if EF_WIDE_STAGGER
+    // waves w and w + 4 share a SIMD: the upper four issue their DMA burst half-way through
+    // the slice, so each SIMD's MFMA pipe is fed by one wave while the other issues
+    if (more && wave < 4) issue(it + 1, buf ^ 1);
+#else
+    if (more) issue(it + 1, buf ^ 1);  // lands under this slice's MFMAs
+#endif
     if (sl == 0) {
       // L2: start from -||g||^2 / 2 and accumulate q.g (-2 acc = ||g||^2 - 2 q.g); cosine: 0
 #pragma unroll
@@ -799,10 +806,8 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
         acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[pb], acc[rb][pb], 0, 0, 0);
         acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[pb], acc[rb][pb], 0, 0, 0);
       }
-#if EF_WIDE_INTERLEAVE
-      // one DMA piece of slice it + 1 per 12 MFMAs instead of a burst of 8 at the top
-      // (buffer buf ^ 1 was released by the previous slice's barrier)
-      if (it + 1 < n_it) issue_piece(it + 1, buf ^ 1, rb);
+#if EF_WIDE_STAGGER
+      if (rb == EF_WIDE_STAGGER - 1 && more && wave >= 4) issue(it + 1, buf ^ 1);
 #endif
     }
     if (sl == NS - 1) {

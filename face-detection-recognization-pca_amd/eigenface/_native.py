@@ -32,6 +32,7 @@ EF_OPT_FIT_MAX_ITERS, EF_OPT_FIT_FP32_COARSE, EF_OPT_COV_SLAB_BYTES, EF_OPT_TM_I
 EF_OPT_JPEG_CHUNK_BITS = 6
 EF_OPT_SEARCH_SPLIT_BF16 = 7
 EF_OPT_JPEG_PART_FILES = 8
+EF_OPT_FIT_CHEBYSHEV = 9
 EF_E_NUMERIC = -5
 
 

@@ -37,7 +37,8 @@ def _dev(x, torch_dtype):
 _OPTIONS = {"fit_max_iters": N.EF_OPT_FIT_MAX_ITERS, "fit_fp32_coarse": N.EF_OPT_FIT_FP32_COARSE,
             "cov_slab_bytes": N.EF_OPT_COV_SLAB_BYTES, "tm_int64_sums": N.EF_OPT_TM_INT64_SUMS,
             "haar_ordered": N.EF_OPT_HAAR_ORDERED, "jpeg_chunk_bits": N.EF_OPT_JPEG_CHUNK_BITS,
-            "search_split_bf16": N.EF_OPT_SEARCH_SPLIT_BF16, "jpeg_part_files": N.EF_OPT_JPEG_PART_FILES}
+            "search_split_bf16": N.EF_OPT_SEARCH_SPLIT_BF16, "jpeg_part_files": N.EF_OPT_JPEG_PART_FILES,
+            "fit_chebyshev": N.EF_OPT_FIT_CHEBYSHEV}
 
 
 def _option(o):
@@ -150,7 +151,7 @@ class Engine:
     def set_option(self, option, value):
         """Context tunable (include/eigenface.h EF_OPT_*): "fit_max_iters",
         "fit_fp32_coarse", "cov_slab_bytes", "tm_int64_sums", "haar_ordered", "jpeg_chunk_bits",
-        "search_split_bf16", "jpeg_part_files" or the code."""
+        "search_split_bf16", "jpeg_part_files", "fit_chebyshev" or the code."""
         self._chk(self._lib.ef_set_option(self._h, _option(option), int(value)))
 
     def get_option(self, option):

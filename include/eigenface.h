@@ -213,6 +213,9 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
                                       with the 32x32x16 kernel at k in (64, 128] (comparison) */
 #define EF_OPT_JPEG_PART_FILES 8   /* ef_jpeg_ingest decodes in parts of this many files, staging
                                       part i + 1 on a host thread while part i decodes [8192] */
+#define EF_OPT_FIT_CHEBYSHEV 9     /* 1 [default]: the subspace iteration advances a Chebyshev
+                                      three-term recurrence on [0, theta_m] between Rayleigh-Ritz
+                                      steps; 0: one shifted power step per iteration */
 int ef_set_option(ef_ctx* ctx, int32_t option, int64_t value);
 int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 
