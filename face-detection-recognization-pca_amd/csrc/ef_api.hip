@@ -262,6 +262,7 @@ void ef_destroy(ef_ctx* c) {
     if (c->jpeg_pinned[i]) (void)hipHostFree(c->jpeg_pinned[i]);
     if (c->jpeg_up_done[i]) (void)hipEventDestroy(c->jpeg_up_done[i]);
   }
+  if (c->jpeg_flags_read) (void)hipEventDestroy(c->jpeg_flags_read);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);
@@ -553,7 +554,8 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
       c->opt_fit_max_iters = value;
       return EF_OK;
     case EF_OPT_FIT_FP32_COARSE:
-      c->opt_fit_fp32_coarse = value != 0;
+      if (value < 0 || value > 2) return set_err(c, EF_E_INVALID, "EF_OPT_FIT_FP32_COARSE must be 0, 1 or 2");
+      c->opt_fit_fp32_coarse = value;
       return EF_OK;
     case EF_OPT_COV_SLAB_BYTES:
       if (value < 1) return set_err(c, EF_E_INVALID, "EF_OPT_COV_SLAB_BYTES must be >= 1");

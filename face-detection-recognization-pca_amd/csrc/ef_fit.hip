@@ -234,13 +234,20 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   // steps, Y = C.Q runs as an fp32 sgemm on an fp32 copy of C (twice the fp64 matrix
   // rate); the iteration is self-correcting, and convergence is only declared between two
   // Rayleigh-Ritz steps that both follow fp64 products, so the result is the fp64 one.
+  // Its products run on the split-bf16 matrix cores (ef_gemm_s3.hip: hi.hi' + hi.lo' +
+  // lo.hi', ~2^-17 relative per product, 16/3 x the fp32 rate) when the block is 256 wide
+  // (option value 1, the default), else — or with option value 2 — as fp32 MFMA GEMMs.
   float *C32 = nullptr, *Q32 = nullptr, *Y32 = nullptr;
   bool coarse = dim >= 4096 && c->opt_fit_fp32_coarse != 0 && tall_gemm_supported(dim, C, 8);
+  const bool coarse_s3 = coarse && c->opt_fit_fp32_coarse == 1 && gemm_s3_supported(dim, dim, m);
   if (coarse) {
-    EF_TRY(B.get(c, (size_t)dim * dim, &C32));
-    EF_TRY(B.get(c, (size_t)dim * m, &Q32));  // Q^T in fp32 (the GEMM's transposed B)
-    EF_TRY(B.get(c, (size_t)dim * m, &Y32));
-    cvt64to32(s, C, dim * dim, C32);
+    EF_TRY(B.get(c, (size_t)dim * dim, &C32));  // fp32 C, or its split-bf16 copy (same bytes)
+    EF_TRY(B.get(c, (size_t)dim * m, &Q32));    // Q^T in fp32 / split-bf16 (the GEMM's transposed B)
+    EF_TRY(B.get(c, coarse_s3 ? gemm_s3_part_elems(dim) : (size_t)dim * m, &Y32));
+    if (coarse_s3)
+      EF_HIP(c, launch_split_f64(s, C, dim * dim, C32), "C (split-bf16)");
+    else
+      cvt64to32(s, C, dim * dim, C32);
   }
   std::vector<double> th(m), prev(m, 0.0);
   bool have_prev = false, prev_fine = false;
@@ -279,7 +286,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     const bool fine = !coarse;  // this iteration's product is fp64
     const double sig_it = sigma;  // the shift this iteration's product carries
     bool restarted = false;
-    if (coarse) {
+    if (coarse && coarse_s3) {
+      EF_HIP(c, launch_transpose_split(s, Q, dim, Q32), "Q^T (split-bf16)");
+      EF_HIP(c, gemm_s3(s, C32, dim, Q32, dim, dim, dim, Y32, Q, sigma, Y), "Y = C.Q (split-bf16)");
+    } else if (coarse) {
       EF_HIP(c, launch_transpose_f64_to_f32(s, Q, m, dim, m, Q32, dim), "Q^T (fp32)");
       EF_HIP(c, tall_gemm_f32(s, C32, dim, false, Q32, dim, Y32, m, dim, m, dim, 1.f, reinterpret_cast<float*>(work),
                               kWorkElems * 2),

@@ -126,6 +126,7 @@ struct ef_ctx {
   size_t jpeg_pinned_bytes[2] = {0, 0};
   hipEvent_t jpeg_up_done[2] = {nullptr, nullptr};
   int jpeg_rounds = 0;  // synchronisation rounds of the last decode (diagnostics)
+  hipEvent_t jpeg_flags_read = nullptr;  // the queued rounds' change flags reached the host
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade

@@ -764,6 +764,7 @@ __host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const uns
 }
 
 constexpr int kChunkThreads = 256;
+constexpr int kDeviceRounds = 8;  // synchronisation rounds queued without a host round trip
 constexpr int kGlobalLutStride = (int)(sizeof(HuffTab) / 2);
 
 // The batch's lookahead tables in LDS when there are at most kLdsTables of them (the usual
@@ -784,11 +785,16 @@ __device__ __forceinline__ const unsigned short* stage_luts(const ChunkCtx& X, i
   return slut;
 }
 
+// prev_changed (rounds >= 2 of the device-side sequence): the previous round's change flag;
+// when it stayed 0 the fixed point is reached and this round — and, its own flag staying
+// 0, every later one — exits at once, so rounds can be queued without a host round trip.
 __global__ __launch_bounds__(kChunkThreads) void jpeg_sync_kernel(ChunkCtx X, int lds_tables, int round,
                                                                   long long* __restrict__ S,
                                                                   const long long* __restrict__ Ein,
                                                                   long long* __restrict__ Eout, int* __restrict__ cnt,
-                                                                  int* __restrict__ changed) {
+                                                                  int* __restrict__ changed,
+                                                                  const int* __restrict__ prev_changed) {
+  if (prev_changed && *prev_changed == 0) return;  // uniform: converged before this round
   extern __shared__ unsigned short slut[];
   int lstride;
   const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);
@@ -1410,7 +1416,7 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
   const size_t o_cnt = off; off += al((size_t)nchunks * 16);
   const size_t o_G = off; off += al((size_t)nchunks * 4);
   const size_t o_P = off; off += al((size_t)nchunks * 12);
-  const size_t o_flag = off; off += al(16);
+  const size_t o_flag = off; off += al(4 * (kDeviceRounds + 2));
   const size_t o_cps = off; off += al((size_t)nchunks * kCheckpoints * sizeof(Checkpoint));
   const size_t o_coef = off; off += al((size_t)B.coef_blocks * 64 * 2);
   const size_t o_planes = off; off += al((size_t)B.plane_bytes + 16);
@@ -1456,33 +1462,73 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
   const int lds_tables = B.T.huff.size() <= (size_t)kLdsTables ? (int)B.T.huff.size() : 0;
   const size_t lds_bytes = (size_t)lds_tables * kLookSize * 2;
   int rounds = 0;
+  // flag[r]: round r changed an exit state (r = 1 .. kDeviceRounds)
+  if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4 * (kDeviceRounds + 2), s);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, 0, S_, E[1],
-                       E[0], cnt, flag);
+                       E[0], cnt, flag, nullptr);
     e = hipGetLastError();
   }
-  // synchronisation rounds until no start state changes; at most one per chunk of the
-  // longest segment (each round makes at least the next chunk in every segment exact)
+  // Synchronisation rounds until no start state changes (at most one per chunk of the
+  // longest segment: each round makes at least the next chunk in every segment exact).
+  // The first kDeviceRounds are queued back to back — a round after the fixed point exits
+  // at once (jpeg_sync_kernel prev_changed) — and the decode kernels behind them, so no
+  // host round trip separates the rounds; the host reads the flags once, while those
+  // kernels run, and only a batch that needs more rounds (rare) continues round by round
+  // and decodes again.
   int cur = 0;
-  for (int r = 1; e == hipSuccess && r <= max_chunks; ++r) {
-    e = hipMemsetAsync(flag, 0, 4, s);
-    if (e != hipSuccess) break;
+  const int qrounds = std::min(max_chunks, kDeviceRounds);
+  for (int r = 1; e == hipSuccess && r <= qrounds; ++r) {
     hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S_, E[cur],
-                       E[cur ^ 1], cnt, flag);
+                       E[cur ^ 1], cnt, flag + r, r >= 2 ? flag + r - 1 : nullptr);
     e = hipGetLastError();
     cur ^= 1;
-    rounds = r;
-    if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess || *hflag == 0) break;
   }
-  c->jpeg_rounds = rounds;
-  tm.mark("sync-rounds");
-  if (e == hipSuccess) {
+  if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4 * (qrounds + 1), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && !c->jpeg_flags_read) e = hipEventCreateWithFlags(&c->jpeg_flags_read, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(c->jpeg_flags_read, s);
+  auto decode_kernels = [&]() {
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
                        (int)B.segs.size(), cnt, G, P);
     hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S_, G,
                        P, reinterpret_cast<short*>(base + o_coef));
+  };
+  if (e == hipSuccess) {
+    decode_kernels();
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipEventSynchronize(c->jpeg_flags_read);
+  if (e == hipSuccess) {
+    rounds = qrounds;
+    for (int r = 1; r <= qrounds; ++r)
+      if (hflag[r] == 0) {
+        rounds = r;
+        break;
+      }
+    if (rounds == qrounds && hflag[qrounds] != 0 && qrounds < max_chunks) {
+      // not converged within the queued rounds: continue round by round, then decode again
+      for (int r = qrounds + 1; e == hipSuccess && r <= max_chunks; ++r) {
+        e = hipMemsetAsync(flag, 0, 4, s);
+        if (e != hipSuccess) break;
+        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S_,
+                           E[cur], E[cur ^ 1], cnt, flag, nullptr);
+        e = hipGetLastError();
+        cur ^= 1;
+        rounds = r;
+        if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess || *hflag == 0) break;
+      }
+      if (e == hipSuccess) e = hipMemsetAsync(base + o_coef, 0, (size_t)B.coef_blocks * 64 * 2, s);
+      if (e == hipSuccess) {
+        decode_kernels();
+        e = hipGetLastError();
+      }
+    }
+  }
+  c->jpeg_rounds = rounds;
+  tm.mark("sync-rounds");
+  if (e == hipSuccess) {
     const JImage* d_imgs = X.imgs;
     short* d_coef = reinterpret_cast<short*>(base + o_coef);
     uint8_t* d_planes = reinterpret_cast<uint8_t*>(base + o_planes);

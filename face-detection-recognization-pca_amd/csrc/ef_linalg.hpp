@@ -96,6 +96,15 @@ hipError_t tall_gemm_f64(hipStream_t s, const double* A, int64_t lda, bool a_tra
 hipError_t tall_gemm_f32(hipStream_t s, const float* A, int64_t lda, bool a_trans, const float* Bt, int64_t ldbt,
                          float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha, float* work,
                          size_t work_elems);
+// Split-bf16 tall GEMM of the fit's coarse phase (ef_gemm_s3.hip): Y (M x 256, fp64) =
+// A3 . Bt3^T - sigma Q with A3 (M x K, lda) and Bt3 (256 x K, ldb) in the split layout
+// (launch_split_f64 / launch_transpose_split); part: gemm_s3_part_elems(M) floats.
+bool gemm_s3_supported(int64_t M, int64_t K, int64_t N);
+size_t gemm_s3_part_elems(int64_t M);
+hipError_t launch_split_f64(hipStream_t s, const double* x, int64_t n, void* out);
+hipError_t launch_transpose_split(hipStream_t s, const double* Q, int64_t dim, void* Bt3);
+hipError_t gemm_s3(hipStream_t s, const float* A3, int64_t lda, const float* Bt3, int64_t ldb, int64_t M, int64_t K,
+                   float* part, const double* Q, double sigma, double* Y);
 // out (cols x rows, ldout) = in (rows x cols, ldin)^T; the second also converts to fp32
 hipError_t launch_transpose_f64(hipStream_t s, const double* in, int64_t ldin, int64_t rows, int64_t cols, double* out,
                                 int64_t ldout);

@@ -200,8 +200,10 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
 /* ------------------------------------------------------------------ options
  * Per-context tunables (defaults in brackets). */
 #define EF_OPT_FIT_MAX_ITERS 1   /* subspace-iteration cap [500]; reaching it unconverged -> EF_E_NUMERIC */
-#define EF_OPT_FIT_FP32_COARSE 2 /* 1 [default]: fp32 C.Q products while the Ritz values still move by
-                                    > 1e-4 (self-correcting); 0: fp64 products throughout */
+#define EF_OPT_FIT_FP32_COARSE 2 /* 1 [default]: a coarse phase of reduced-precision C.Q products while
+                                    the Ritz values still move (self-correcting; split-bf16 matrix-core
+                                    products for a 256-wide block, fp32 otherwise); 2: the same with
+                                    fp32 products; 0: fp64 products throughout */
 #define EF_OPT_COV_SLAB_BYTES 3  /* device budget of the int32 covariance partial sums [8 GiB];
                                     smaller budgets run the multi-pass int64 schedule */
 #define EF_OPT_TM_INT64_SUMS 4   /* 1: int64 integral images in the template localiser [0: auto] */

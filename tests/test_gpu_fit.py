@@ -205,22 +205,26 @@ def _c3_fixture():
     return g, x
 
 
-@pytest.mark.parametrize("coarse_fp32", [1, 0])
-def test_fit_c3_shape_vs_oracle(coarse_fp32):
+@pytest.mark.parametrize("cheb", [1, 0])
+@pytest.mark.parametrize("coarse_fp32", [1, 2, 0])
+def test_fit_c3_shape_vs_oracle(coarse_fp32, cheb):
     """The C3 fit shape (d = 128 x 128 = 16384, k = 128, n = 20000 >= d, StandardScaler):
-    covariance branch at order 16384, the order >= 12288 Rayleigh-Ritz schedule and (for
-    coarse_fp32 = 1, the default) the fp32 coarse phase, against the oracle's
-    covariance-branch fit (tests/golden/make_fit_c3.py; exact-integer generator, so the
-    box regenerates the same pixels).  Eigenvalues rtol 1e-9, components 1e-4 relative
-    (north star), fp32 coarse phase == fp64 throughout to 1e-9."""
+    covariance branch at order 16384, the Rayleigh-Ritz schedule, the coarse phase
+    (coarse_fp32 = 1, the default: split-bf16 matrix-core products; 2: fp32 products; 0:
+    fp64 throughout) and the Chebyshev recurrence (cheb = 1, the default) or plain shifted
+    steps, against the oracle's covariance-branch fit (tests/golden/make_fit_c3.py;
+    exact-integer generator, so the box regenerates the same pixels).  Eigenvalues rtol
+    1e-9, components 1e-4 relative (north star)."""
     from eigenface import get_engine
     g, x = _c3_fixture()
     e = get_engine(0)
     e.set_option("fit_fp32_coarse", coarse_fp32)
+    e.set_option("fit_chebyshev", cheb)
     try:
         r = e.fit(x, int(g["k"]), standardize=True)
     finally:
         e.set_option("fit_fp32_coarse", 1)
+        e.set_option("fit_chebyshev", 1)
     assert r.k == 128 and r.iters > 0  # subspace iteration, not the direct Jacobi
     np.testing.assert_allclose(r.mean, g["scaler_mean"], rtol=1e-14)
     np.testing.assert_allclose(r.scale, g["scaler_scale"], rtol=1e-12)
@@ -245,7 +249,7 @@ def test_fit_c3_shape_vs_oracle(coarse_fp32):
         assert margin <= err + 1e-15, f"component {c}: sign flipped with a clear max entry (margin {margin:.3e})"
         assert int(np.argmax(np.abs(r.components[c]))) == int(ti[c, 1]), f"component {c}"
         assert r.components[c, ti[c, 1]] > 0
-    print(f"C3 fit (coarse_fp32={coarse_fp32}): {len(flips)} svd_flip sign(s) differ from the oracle's, "
+    print(f"C3 fit (coarse={coarse_fp32}, chebyshev={cheb}, {r.iters} iterations): {len(flips)} svd_flip sign(s) differ from the oracle's, "
           f"all at near-tied max entries (component, margin, fit difference): {flips}")
     cr *= s[:, None]
     # unit rows against +-1 columns: |c.R| ~ 1, so atol 1e-4 is the 1e-4 relative bar

@@ -33,16 +33,18 @@ def main():
     torch.cuda.synchronize()
     eng = Engine(0)
     res = {}
-    for cheb in (1, 0, 1, 0):
+    modes = [(1, 1), (1, 2), (0, 1), (1, 1), (1, 2), (0, 1)]  # (chebyshev, coarse phase)
+    for cheb, coarse in modes:
         eng.set_option("fit_chebyshev", cheb)
+        eng.set_option("fit_fp32_coarse", coarse)
         eng.fit(X[:4096], 16, standardize=True, projection=False)
         torch.cuda.synchronize()
         t = time.perf_counter()
         r1 = eng.fit(X, k, standardize=True, projection=False)
         dt = time.perf_counter() - t
-        print(f"chebyshev={cheb}: fit {dt:.4f} s, iterations {r1.iters}", flush=True)
-        res[cheb] = r1
-    a, b = res[1], res[0]
+        print(f"chebyshev={cheb} coarse={coarse}: fit {dt:.4f} s, iterations {r1.iters}", flush=True)
+        res[(cheb, coarse)] = r1
+    a, b = res[(1, 1)], res[(0, 1)]
     ev_a, ev_b = a.eigenvalues.cpu().numpy(), b.eigenvalues.cpu().numpy()
     ca, cb = a.components.cpu().numpy(), b.components.cpu().numpy()
     s = np.sign((ca * cb).sum(1))
