@@ -19,8 +19,17 @@
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef long i64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i64x2 as_i64x2(const bf16x8& v) {
+  i64x2 r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
 
-// SHAPE 0: 32x32x16 (32 cyc), 1: 16x16x32 (16 cyc).  NACC accumulators of 512 (32x32) or
+// SHAPE 0: 32x32x16 (32 cyc), 1: 16x16x32 (16 cyc); 2: i8 32x32x32, 3: i8 16x16x64 (the
+// covariance SYRK's instruction and its 16x16 form; int32 accumulators).  NACC accumulators of 512 (32x32) or
 // 4x 16x16 = the same 1024 outputs per accumulator group.  LDS: operands re-read from LDS.
 template <int SHAPE, bool LDS>
 __global__ __launch_bounds__(512) void bf16_loop(const unsigned* __restrict__ in, float* __restrict__ out,
@@ -38,8 +47,12 @@ __global__ __launch_bounds__(512) void bf16_loop(const unsigned* __restrict__ in
   }
   f32x16 acc[8];
   f32x4 acc4[32];
+  i32x16 iacc[8];
+  i32x4 iacc4[16];
   for (int c = 0; c < 8; ++c) acc[c] = f32x16{};
   for (int c = 0; c < 32; ++c) acc4[c] = f32x4{};
+  for (int c = 0; c < 8; ++c) iacc[c] = i32x16{};
+  for (int c = 0; c < 16; ++c) iacc4[c] = i32x4{};
   unsigned long long t0 = 0, r0 = 0;
   if (tid == 0) {
     t0 = __builtin_amdgcn_s_memtime();
@@ -60,10 +73,18 @@ __global__ __launch_bounds__(512) void bf16_loop(const unsigned* __restrict__ in
     if constexpr (SHAPE == 0) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c & 3], b[(c >> 1) & 3], acc[c], 0, 0, 0);
-    } else {
+    } else if constexpr (SHAPE == 1) {
 #pragma unroll
       for (int c = 0; c < 16; ++c)
         acc4[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c & 3], b[(c >> 2) & 3], acc4[c], 0, 0, 0);
+    } else if constexpr (SHAPE == 2) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        iacc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i64x2(a[c & 3]), as_i64x2(b[(c >> 1) & 3]), iacc[c], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        iacc4[c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(as_i64x2(a[c & 3]), as_i64x2(b[(c >> 2) & 3]), iacc4[c], 0, 0, 0);
     }
   }
   float r = 0.f;
@@ -71,6 +92,10 @@ __global__ __launch_bounds__(512) void bf16_loop(const unsigned* __restrict__ in
     for (int q = 0; q < 16; ++q) r += acc[c][q];
   for (int c = 0; c < 32; ++c)
     for (int q = 0; q < 4; ++q) r += acc4[c][q];
+  for (int c = 0; c < 8; ++c)
+    for (int q = 0; q < 16; ++q) r += (float)iacc[c][q];
+  for (int c = 0; c < 16; ++c)
+    for (int q = 0; q < 4; ++q) r += (float)iacc4[c][q];
   if (tid == 0) {
     stamps[blockIdx.x * 2] = __builtin_amdgcn_s_memtime() - t0;
     stamps[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime() - r0;
@@ -81,7 +106,7 @@ __global__ __launch_bounds__(512) void bf16_loop(const unsigned* __restrict__ in
 template <int SHAPE, bool LDS>
 static void run(const char* name, int threads, const unsigned* in, float* out, unsigned long long* stamps, int cus) {
   // flops per loop iteration per wave: 8 x 32x32x16 = 8 x 32768, or 16 x 16x16x32 = 16 x 16384
-  const double flop_it_wave = SHAPE == 0 ? 8.0 * 32768 : 16.0 * 16384;
+  const double flop_it_wave = SHAPE == 0 ? 8.0 * 32768 : SHAPE == 1 ? 16.0 * 16384 : SHAPE == 2 ? 8.0 * 65536 : 16.0 * 32768;
   const int iters = 20000;
   const int waves = threads / 64;
   hipEvent_t e0, e1;
@@ -110,13 +135,13 @@ static void run(const char* name, int threads, const unsigned* in, float* out, u
     if (st[2 * i + 1]) ghz.push_back((double)st[2 * i] / (double)st[2 * i + 1] * 0.1);  // memrealtime: 100 MHz
   std::sort(ghz.begin(), ghz.end());
   const double tf = flop_it_wave * iters * waves * cus / (ms * 1e-3) / 1e12;
-  const double cyc = SHAPE == 0 ? 32.0 : 16.0;  // cycles per MFMA per SIMD at full issue
-  const double mfma_per_simd = (SHAPE == 0 ? 8.0 : 16.0) * iters * waves / 4.0;
+  const double cyc = (SHAPE % 2) == 0 ? 32.0 : 16.0;  // cycles per MFMA per SIMD at full issue
+  const double mfma_per_simd = ((SHAPE % 2) == 0 ? 8.0 : 16.0) * iters * waves / 4.0;
   const double busy = mfma_per_simd * cyc / (ghz.empty() ? 1.0 : ghz[ghz.size() / 2] * 1e9) / (ms * 1e-3);
   printf("{\"loop\": \"%s\", \"threads_per_cu\": %d, \"ms\": %.3f, \"tflops\": %.1f, \"frac_of_2500\": %.4f, "
          "\"clock_ghz_median\": %.3f, \"clock_ghz_min\": %.3f, \"clock_ghz_max\": %.3f, \"mfma_busy_at_clock\": %.3f, "
          "\"launches_before\": %d}\n",
-         name, threads, ms, tf, tf / 2500.0, ghz.empty() ? 0.0 : ghz[ghz.size() / 2], ghz.empty() ? 0.0 : ghz[0],
+         name, threads, ms, tf, tf / (SHAPE >= 2 ? 5000.0 : 2500.0), ghz.empty() ? 0.0 : ghz[ghz.size() / 2], ghz.empty() ? 0.0 : ghz[0],
          ghz.empty() ? 0.0 : ghz.back(), busy, n);
   fflush(stdout);
 }
@@ -141,6 +166,14 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&stamps, (size_t)cus * 16);
   (void)hipMemcpy(in, h.data(), h.size() * 4, hipMemcpyHostToDevice);
   const bool lds_only = argc > 1 && argv[1][0] == 'l';
+  const bool i8_only = argc > 1 && argv[1][0] == 'i';
+  if (i8_only || argc == 1) {  // int8 (the covariance SYRK): TOPS, fraction of the 5 POPS dense peak
+    run<2, false>("i8 32x32x32 regs", 512, in, out, stamps, cus);
+    run<3, false>("i8 16x16x64 regs", 512, in, out, stamps, cus);
+    run<2, true>("i8 32x32x32 lds", 512, in, out, stamps, cus);
+    run<3, true>("i8 16x16x64 lds", 512, in, out, stamps, cus);
+    if (i8_only) return 0;
+  }
   if (!lds_only) {
     run<0, false>("32x32x16 regs", 512, in, out, stamps, cus);
     run<1, false>("16x16x32 regs", 512, in, out, stamps, cus);
