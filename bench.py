@@ -170,12 +170,13 @@ def pmc_traffic(config):
     return None, None
 
 
-def bf16_ceiling(loop):
+def bf16_ceiling(loop, name="bf16_clock.json"):
     """TFLOP/s a bare bf16 MFMA loop of this shape (operands re-read from LDS, 2 waves per
     SIMD, every CU busy, random data) holds under the chip's power-limited clock: the
-    newest committed tools/micro/bf16_clock.cpp capture (profiles/r*/bf16_clock.json)."""
+    newest committed tools/micro/bf16_clock.cpp capture (profiles/r*/bf16_clock.json; the
+    int8 loops, `bf16_clock i`, in profiles/r*/i8_clock.json)."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bf16_clock.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
         for line in open(f):
             if line.startswith("{"):
                 rec = json.loads(line)
@@ -214,9 +215,13 @@ def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu
     t = time.perf_counter()
     eng.fit(X, k, standardize=True, projection=True)
     t_cold = time.perf_counter() - t
+    eng.timing(True)
+    eng.timing_reset()
     t = time.perf_counter()
     r1 = eng.fit(X, k, standardize=True, projection=False)
     t_fit = time.perf_counter() - t
+    syrk_ms, syrk_n = eng.timing_get("syrk")
+    eng.timing(False)
     t = time.perf_counter()
     r2 = eng.fit(X, k, standardize=True, projection=True)
     t_fit_tr = time.perf_counter() - t
@@ -231,6 +236,24 @@ def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu
         "explained_variance_top3": [float(v) for v in ev[:3]],
         "repeat_identical": bool(torch.equal(r1.components, r2.components)),
     }
+    # fit roofline: the int8 SYRK (syrk_i8_kernel) is the fit's dominant kernel.  Algorithmic
+    # ops = the upper triangle with its diagonal, 2 ops per multiply-add: n d (d + 1); the
+    # launches' time from hipEvents on the fit's stream (EF_KERNEL_SYRK, one fit).
+    if syrk_n > 0 and syrk_ms > 0:
+        ops = float(n) * d * (d + 1)
+        tops = ops / (syrk_ms * 1e-3) / 1e12
+        roof = {"kernel": "syrk_i8_kernel<384,4>", "bound": "mfma", "achieved": round(tops, 1),
+                "peak": 5000.0, "unit": "TOP/s (int8)", "frac": round(tops / 5000.0, 4),
+                "syrk_ms": round(syrk_ms, 3), "syrk_share_of_fit": round(syrk_ms * 1e-3 / t_fit, 3),
+                "ops_per_fit": ops,
+                "note": "ops = n d (d+1) (upper triangle of X'^T X', 2 per MAC); peak = 2 x the 2.5 PF bf16 "
+                        "dense figure (MI355X_MICROARCH.md: I8 at 2x the BF16 rate per clock)"}
+        ceil = bf16_ceiling("i8 32x32x32 lds", "i8_clock.json")
+        if ceil:
+            roof["power_limited_ceiling_TOPs"] = ceil[0]
+            roof["frac_of_power_limited_ceiling"] = round(tops / ceil[0], 4)
+            roof["ceiling_source"] = ceil[1]
+        out["roofline"] = roof
     del r1, r2
     if with_cpu:
         xs = X[:n_cpu].cpu().numpy()

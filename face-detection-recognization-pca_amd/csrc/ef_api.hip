@@ -49,6 +49,18 @@ void timer_begin(ef_ctx* c, int kernel, TimerEvt* t) {
   (void)hipEventRecord(t->a, c->stream);
 }
 
+void timer_arm(ef_ctx* c, int kernel, TimerEvt* t) {
+  t->kernel = -1;
+  if (!c->timing) return;
+  if (hipEventCreate(&t->a) != hipSuccess) return;
+  if (hipEventCreate(&t->b) != hipSuccess) { (void)hipEventDestroy(t->a); return; }
+  t->kernel = kernel;
+}
+
+void timer_commit(ef_ctx* c, TimerEvt* t) {
+  if (t->kernel >= 0) c->pending.push_back(*t);
+}
+
 void timer_end(ef_ctx* c, TimerEvt* t) {
   if (t->kernel < 0) return;
   (void)hipEventRecord(t->b, c->stream);

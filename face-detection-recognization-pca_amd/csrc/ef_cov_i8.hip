@@ -488,7 +488,7 @@ bool cov_i8_fused_stats(const uint8_t* X, int64_t d) { return d % 4 == 0 && ((si
 hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, bool gram,
                          const unsigned long long* S1, const double* w, const uint8_t* At, int* slabs,
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
-                         double* C) {
+                         double* C, hipEvent_t syrk_begin, hipEvent_t syrk_end) {
   const int64_t dim = gram ? n : d;
   const std::vector<int2> order = syrk_tiles(dim, p.tj);  // one H2D of the list
   if ((int)order.size() != p.ntiles) return hipErrorInvalidValue;
@@ -502,6 +502,7 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
     e = hipMemsetAsync(S64, 0, (size_t)dim * dim * sizeof(long long), s);
     if (e != hipSuccess) return e;
   }
+  if (syrk_begin) (void)hipEventRecord(syrk_begin, s);  // EF_KERNEL_SYRK: every pass of the SYRK
   for (int pass = 0; pass < p.passes; ++pass) {
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
@@ -515,6 +516,7 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
       hipLaunchKernelGGL(slab_accumulate_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s, slabs,
                          p.splits, dim, S64);
   }
+  if (syrk_end) (void)hipEventRecord(syrk_end, s);
   e = hipStreamSynchronize(s);  // the host list must outlive the copy
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(shifted_sums_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, n, d, cvec);

@@ -615,8 +615,13 @@ extern "C" int ef_fit_ex(ef_ctx* c, const void* Xv, int32_t x_dtype, int64_t n, 
     EF_TRY(B.get(c, 2, &Q2));
     uint8_t* order;
     EF_TRY(B.get(c, (size_t)cov_i8_order_bytes(dim), &order));
-    EF_HIP(c, launch_cov_i8(s, plan, n, d, gram, S1, stdz ? w : nullptr, At, slabs, S64, cvec, R, Q2, order, C),
-           "covariance (int8)");
+    TimerEvt tev;
+    timer_arm(c, EF_KERNEL_SYRK, &tev);
+    const hipError_t ecov = launch_cov_i8(s, plan, n, d, gram, S1, stdz ? w : nullptr, At, slabs, S64, cvec, R, Q2,
+                                          order, C, tev.kernel >= 0 ? tev.a : nullptr,
+                                          tev.kernel >= 0 ? tev.b : nullptr);
+    timer_commit(c, &tev);  // (the drain skips a pair whose end was never recorded)
+    EF_HIP(c, ecov, "covariance (int8)");
     B.drop(s, At);
     B.drop(s, slabs);
     if (S64) B.drop(s, S64);

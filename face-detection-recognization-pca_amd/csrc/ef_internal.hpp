@@ -154,6 +154,10 @@ int ensure(ef_ctx* c, DevBuf& b, size_t bytes);
 void release(DevBuf& b);
 void timer_begin(ef_ctx* c, int kernel, TimerEvt* t);
 void timer_end(ef_ctx* c, TimerEvt* t);
+// events created but not recorded: the launcher records them itself around the kernels
+// (t->kernel < 0 when timing is off); timer_commit queues them for ef_timing_get
+void timer_arm(ef_ctx* c, int kernel, TimerEvt* t);
+void timer_commit(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
 SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3);

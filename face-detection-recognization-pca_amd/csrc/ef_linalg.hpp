@@ -154,7 +154,7 @@ hipError_t launch_cov_i8_prep(hipStream_t s, const uint8_t* X, int64_t n, int64_
 hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, bool gram,
                          const unsigned long long* S1, const double* w, const uint8_t* At, int* slabs,
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
-                         double* C);
+                         double* C, hipEvent_t syrk_begin = nullptr, hipEvent_t syrk_end = nullptr);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
 // Li = L^-1 (row-major, zeros above the diagonal) for G = L L^T in one register-resident
 // workgroup (m <= 256, m even: chol_inv_supported); G is not modified; *info as

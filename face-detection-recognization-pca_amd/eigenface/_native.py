@@ -21,8 +21,8 @@ EF_FIT_STANDARDIZE = 0x1
 EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
-EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR, EF_KERNEL_JPEG = \
-    0, 1, 2, 3, 4, 5
+EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR, EF_KERNEL_JPEG, \
+    EF_KERNEL_SYRK = 0, 1, 2, 3, 4, 5, 6
 EF_JPEG_GRAY, EF_JPEG_BGR = 0, 1
 EF_JPEG_E_UNSUPPORTED, EF_JPEG_E_CORRUPT = -10, -11
 EF_KEY_NONE = (1 << 63) - 1

@@ -656,7 +656,8 @@ class Engine:
 
     def timing_get(self, kernel="search"):
         kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT, "tmatch": N.EF_KERNEL_TMATCH,
-               "ingest": N.EF_KERNEL_INGEST, "haar": N.EF_KERNEL_HAAR, "jpeg": N.EF_KERNEL_JPEG}[kernel]
+               "ingest": N.EF_KERNEL_INGEST, "haar": N.EF_KERNEL_HAAR, "jpeg": N.EF_KERNEL_JPEG,
+               "syrk": N.EF_KERNEL_SYRK}[kernel]
         ms = C.c_double(0)
         n = C.c_int64(0)
         self._chk(self._lib.ef_timing_get(self._h, kid, C.byref(ms), C.byref(n)))

@@ -61,6 +61,7 @@ extern "C" {
 #define EF_KERNEL_INGEST 3  /* grey + resize of one image batch */
 #define EF_KERNEL_HAAR 4    /* Haar cascade detection, one frame (GPU part) */
 #define EF_KERNEL_JPEG 5    /* JPEG entropy decode + IDCT + colour, one batch */
+#define EF_KERNEL_SYRK 6    /* the fit's int8 covariance/Gram SYRK, all passes of one fit */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX

@@ -175,6 +175,25 @@ def test_pooled_workspaces_refit_and_trim():
     np.testing.assert_array_equal(ra1.projection, ra3.projection)
 
 
+def test_syrk_timing_hook():
+    """EF_KERNEL_SYRK: one hipEvent pair per fit around the int8 SYRK launches (the fit
+    roofline's duration in bench.py); nothing recorded while timing is off."""
+    from eigenface import Engine
+    x, _ = orc.synth_faces(900, 16, r=32, seed=23)
+    with Engine(0) as e:
+        e.fit(x, 10)
+        assert e.timing_get("syrk") == (0.0, 0)
+        e.timing(True)
+        r1 = e.fit(x, 10)
+        e.fit(x, 10)
+        ms, n = e.timing_get("syrk")
+        assert n == 2 and ms > 0
+        e.timing_reset()
+        assert e.timing_get("syrk") == (0.0, 0)
+        r2 = e.fit(x, 10)
+    np.testing.assert_array_equal(r1.components, r2.components)
+
+
 def test_eigensolver_non_convergence_is_reported():
     """The subspace iteration's cap (EF_OPT_FIT_MAX_ITERS) ends an unconverged solve with
     EF_E_NUMERIC instead of returning partial eigenpairs; FaceTrainer.train_pca_model
