@@ -336,10 +336,11 @@ def _face_jpegs(n, sides, seed=11):
     return out
 
 
-def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=5):
-    """JPEG files -> grey 64x64 rows (ef_jpeg_ingest: host marker parse + destuff of part i+1
-    overlapped with the upload / GPU Huffman / IDCT / upsample+YCC / resize of part i)
-    against per-file libjpeg-turbo decoding."""
+def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
+    """JPEG files -> grey 64x64 rows (ef_jpeg_ingest into a device tensor): a stream of
+    `reps` batches, each call returning once queued, so batch i+1's host marker parse +
+    destuff overlaps batch i's upload / GPU Huffman / IDCT / upsample+YCC / resize; the
+    clock stops after a device synchronise.  Against per-file libjpeg-turbo decoding."""
     import torch
     blobs = _face_jpegs(n, sides)
     nbytes = sum(len(b) for b in blobs)

@@ -262,19 +262,23 @@ void ef_destroy(ef_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  (void)jpeg_quiesce(c);
   for (auto& t : c->pending) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
-  DevBuf* bufs[] = {&c->mean,  &c->W,    &c->W16,       &c->mean_r,  &c->mean_u8,   &c->corr,      &c->G,
-                    &c->G3, &c->q3, &c->gnorm2, &c->ginv, &c->gmax2,     &c->q_pad,   &c->keys,      &c->search_ws,
-                    &c->p_stage, &c->proj_part, &c->feats_dev, &c->jpeg_ws, &c->jpeg_out, &c->jpeg_rows};
+  DevBuf* bufs[] = {&c->mean,      &c->W,         &c->W16,       &c->mean_r,    &c->mean_u8, &c->corr,
+                    &c->G,         &c->G3,        &c->q3,        &c->gnorm2,    &c->ginv,    &c->gmax2,
+                    &c->q_pad,     &c->keys,      &c->search_ws, &c->p_stage,   &c->proj_part,
+                    &c->feats_dev, &c->jpeg_ws,   &c->jpeg_out,  &c->jpeg_rows, &c->jpeg_up[0], &c->jpeg_up[1]};
   for (DevBuf* b : bufs) release(*b);
   for (int i = 0; i < 2; ++i) {
     if (c->jpeg_pinned[i]) (void)hipHostFree(c->jpeg_pinned[i]);
     if (c->jpeg_up_done[i]) (void)hipEventDestroy(c->jpeg_up_done[i]);
+    if (c->jpeg_ws_free[i]) (void)hipEventDestroy(c->jpeg_ws_free[i]);
   }
-  if (c->jpeg_flags_read) (void)hipEventDestroy(c->jpeg_flags_read);
+  if (c->jpeg_done) (void)hipEventDestroy(c->jpeg_done);
+  if (c->jpeg_copy) (void)hipStreamDestroy(c->jpeg_copy);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);
@@ -307,11 +311,14 @@ int ef_trim(ef_ctx* c) {
   if (!c) return EF_E_INVALID;
   EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
   EF_HIP(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  EF_HIP(c, jpeg_quiesce(c), "jpeg quiesce");
   for (auto& b : c->fit_pool) release(b);
   c->fit_pool.clear();
   release(c->jpeg_ws);
   release(c->jpeg_out);
   release(c->jpeg_rows);
+  release(c->jpeg_up[0]);
+  release(c->jpeg_up[1]);
   for (int i = 0; i < 2; ++i) {
     if (c->jpeg_pinned[i]) (void)hipHostFree(c->jpeg_pinned[i]);
     c->jpeg_pinned[i] = nullptr;

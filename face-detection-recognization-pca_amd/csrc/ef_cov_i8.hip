@@ -159,6 +159,95 @@ __global__ __launch_bounds__(256) void transpose_stats_kernel(const uint8_t* __r
   }
 }
 
+// The same pass with every HBM access a contiguous 1-KiB wave piece (d % 256 == 0):
+// a step is 64 samples x 256 pixels (16 KiB in, 16 KiB out — At's block for those pixels
+// is one contiguous run).  Thread t loads 16 B of sample row 16i + t/16 (dwordx4) into an
+// LDS image [sample][256 px] whose 16-B column chunks are XORed by the row's quarter
+// (r >> 4), then assembles At's 16-B piece t + 256i — pixel t/4 + 64i, samples
+// 16(t%4) .. +15 — from 16 byte reads (the XOR puts a wave's four sample quarters on four
+// distinct bank groups) and stores it at byte 16t + 4096i of the block.  The stats come
+// from the assembled pieces (v_dot4_u32_u8: Σx against 1s, Σx² against itself), one pixel
+// per thread slot; samples past n read as x = 0 for the sums and x' = 0 in At.
+__global__ __launch_bounds__(256) void transpose_stats_lds_kernel(const uint8_t* __restrict__ X, int64_t n,
+                                                                  int64_t d, int64_t nkb, uint8_t* __restrict__ At,
+                                                                  unsigned long long* __restrict__ S1,
+                                                                  unsigned long long* __restrict__ S2) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) uint8_t img[64 * 256];
+  const int t = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.y * 256;
+  const int lc = t & 15, lr = t >> 4;  // load: 16-B column chunk, row within a 16-row group
+  const int q = t & 3;                 // assemble: sample quarter
+  unsigned s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  // the next step's four loads are issued before this step's assembly (registers v)
+  u32x4 v[4];
+  auto load = [&](int64_t kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t smp = kb * 64 + 16 * i + lr;
+      const int64_t sc = smp < n ? smp : n - 1;  // unconditional (all four in flight), zeroed below
+      v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + sc * d + c0) + lc);
+    }
+  };
+  if ((int64_t)blockIdx.x < nkb) load(blockIdx.x);
+  for (int64_t kb = blockIdx.x; kb < nkb; kb += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * i + lr;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(img + r * 256 + 16 * (lc ^ i)) = kb * 64 + r < n ? v[i] : z;
+    }
+    if (kb + gridDim.x < nkb) load(kb + gridDim.x);
+    __syncthreads();
+    const int64_t valid = n - (kb * 64 + 16 * q);  // samples of this quarter inside the data
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = (t >> 2) + 64 * i;
+      const uint8_t* col = img + 16 * q * 256 + (p ^ (16 * q));
+      unsigned w[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const unsigned b0 = col[(4 * g) * 256], b1 = col[(4 * g + 1) * 256], b2 = col[(4 * g + 2) * 256],
+                       b3 = col[(4 * g + 3) * 256];
+        w[g] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        s1[i] = __builtin_amdgcn_udot4(w[g], 0x01010101u, s1[i], false);
+        s2[i] = __builtin_amdgcn_udot4(w[g], w[g], s2[i], false);
+      }
+      u32x4 o = {w[0] ^ 0x80808080u, w[1] ^ 0x80808080u, w[2] ^ 0x80808080u, w[3] ^ 0x80808080u};
+      if (valid < 16) {  // the last block's pad samples: x' = 0
+        unsigned m[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int64_t k = valid - 4 * g;  // valid bytes of dword g
+          m[g] = k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : (0xffffffffu >> (8 * (4 - k))));
+        }
+        o.x &= m[0];
+        o.y &= m[1];
+        o.z &= m[2];
+        o.w &= m[3];
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(At + (kb * d + c0) * 64) + t + 256 * i);
+    }
+    __syncthreads();
+  }
+  // the four quarters of a pixel sit in lanes 4j .. 4j+3
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s1[i] += __shfl_xor(s1[i], 1);
+    s1[i] += __shfl_xor(s1[i], 2);
+    s2[i] += __shfl_xor(s2[i], 1);
+    s2[i] += __shfl_xor(s2[i], 2);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t col = c0 + (t >> 2) + 64 * i;
+      atomicAdd(&S1[col], (unsigned long long)s1[i]);
+      atomicAdd(&S2[col], (unsigned long long)s2[i]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- SYRK on int8 MFMA
 // Slab[ks][i][j] = sum over split ks's samples of At[.][i][k] At[.][j][k] over the tiles
 // (256 rows x TJ columns) that touch the upper triangle.  Item = (split, tile), split-major.
@@ -474,8 +563,16 @@ hipError_t launch_cov_i8_prep(hipStream_t s, const uint8_t* X, int64_t n, int64_
     // <= 4096 blocks of 64 rows per workgroup keeps the uint32 partials exact
     int64_t gx = std::min<int64_t>(nkb, 128);
     gx = std::max<int64_t>(gx, (nkb + 4095) / 4096);
-    hipLaunchKernelGGL(transpose_stats_kernel, dim3((unsigned)gx, (unsigned)((d + 255) / 256)), dim3(256), 0, s, X,
-                       n, d, nkb, At, S1, S2);
+    bool lds = d % 256 == 0;
+#ifdef EF_DIAGNOSTICS
+    if (const char* v = std::getenv("EF_TRANSPOSE_LDS")) lds = lds && std::atoi(v) != 0;
+#endif
+    if (lds)
+      hipLaunchKernelGGL(transpose_stats_lds_kernel, dim3((unsigned)gx, (unsigned)(d / 256)), dim3(256), 0, s, X, n,
+                         d, nkb, At, S1, S2);
+    else
+      hipLaunchKernelGGL(transpose_stats_kernel, dim3((unsigned)gx, (unsigned)((d + 255) / 256)), dim3(256), 0, s, X,
+                         n, d, nkb, At, S1, S2);
   } else {
     hipLaunchKernelGGL(shift_transpose_kernel, dim3((unsigned)nkb, (unsigned)((d + 63) / 64)), dim3(256), 0, s, X,
                        n, d, nkb, At);

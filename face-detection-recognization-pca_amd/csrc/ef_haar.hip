@@ -534,12 +534,6 @@ static std::vector<RectI> group_rectangles(const std::vector<RectI>& rects, int 
   return out;
 }
 
-// The ImgDesc / resize launcher of ef_image.hip (same translation-unit-free interface).
-hipError_t launch_resize_gray(hipStream_t s, const uint8_t* src, const void* desc_dev, int count, int64_t max_out,
-                              uint8_t* dst);
-size_t img_desc_size();
-void img_desc_fill(void* d, int64_t src_off, int64_t dst_off, int h, int w, int c, int oh, int ow);
-
 }  // namespace ef
 
 using namespace ef;

@@ -118,15 +118,21 @@ struct ef_ctx {
 
   std::vector<ef::DevBuf> fit_pool;  // ef_fit workspaces, reused across calls (ef_trim frees)
 
-  // JPEG decode (ef_jpeg.hip): device workspace, host-output staging, pinned upload buffer
+  // JPEG decode (ef_jpeg.hip): device workspace, host-output staging, and two upload slots
+  // (a pinned host buffer + its device copy each): the host stages batch i + 1 into one slot
+  // — the next part of a call, or the next call — while the device decodes batch i from
+  // the other.  up_done[s]: the upload that last read pinned slot s (copy stream);
+  // ws_free[s]: the last kernel that read device slot s (compute stream); done: the last
+  // decode's kernels (a call on another stream, or a reallocation, waits for it).
   ef::DevBuf jpeg_ws, jpeg_out, jpeg_rows;
-  // two pinned upload slots: the ingest stages part i + 1 on a host thread while part i
-  // decodes; each slot's event marks the end of the upload that last read it
+  ef::DevBuf jpeg_up[2];
   void* jpeg_pinned[2] = {nullptr, nullptr};
   size_t jpeg_pinned_bytes[2] = {0, 0};
   hipEvent_t jpeg_up_done[2] = {nullptr, nullptr};
-  int jpeg_rounds = 0;  // synchronisation rounds of the last decode (diagnostics)
-  hipEvent_t jpeg_flags_read = nullptr;  // the queued rounds' change flags reached the host
+  hipEvent_t jpeg_ws_free[2] = {nullptr, nullptr};
+  hipEvent_t jpeg_done = nullptr;
+  hipStream_t jpeg_copy = nullptr;  // upload stream (created on first use)
+  int jpeg_slot = 0;                // slot of the next staged batch
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
   void* haar = nullptr;  // Haar cascade state (ef_haar.hip HaarState), ef_haar_set_cascade
@@ -172,6 +178,14 @@ hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b, ef_match*
 hipError_t launch_matches_merge(hipStream_t s, const ef_match* parts, int nparts, int64_t b, long long* keys,
                                 ef_match* merged);
 void comm_release(ef_ctx* c);
+// ragged resize (ef_image.hip) from device descriptors written by img_desc_fill: the Haar
+// pyramid and the JPEG ingest (BGR order for 3-channel sources)
+hipError_t launch_resize_gray(hipStream_t s, const uint8_t* src, const void* desc_dev, int count, int64_t max_out,
+                              uint8_t* dst);
+size_t img_desc_size();
+void img_desc_fill(void* d, int64_t src_off, int64_t dst_off, int h, int w, int c, int oh, int ow);
+// wait for every queued JPEG upload and decode of the context (ef_jpeg.hip)
+hipError_t jpeg_quiesce(ef_ctx* c);
 // all-gather over the attached communicator on ctx->stream (bytes per rank)
 int comm_allgather(ef_ctx* c, const void* send, void* recv, size_t bytes_per_rank);
 hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,

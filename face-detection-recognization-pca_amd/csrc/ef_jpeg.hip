@@ -802,6 +802,44 @@ __global__ __launch_bounds__(kChunkThreads) void jpeg_sync_kernel(ChunkCtx X, in
   if (i < X.nchunks) sync_chunk(X, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
 }
 
+// Completion of one segment after r synchronisation rounds, sequentially along its chunks.
+// After round r chunks 0..r start exactly (induction from the segment start), and after
+// every round E[i] is the exit of a decode from S[i] (cnt[i] its counts).  So walking
+// j = r+1, r+2, …: E[i-1] is exact; when it equals S[i] chunk i is already exact, else
+// chunk i re-decodes from it (merging into its old trajectory at the first shared
+// checkpoint, as a round does).  Replaces further rounds for the rare batch whose rounds
+// have not reached the fixed point after the queued ones — without a host round trip.
+__host__ __device__ __forceinline__ void finish_segment(const ChunkCtx& X, const unsigned short* luts, int lstride,
+                                                        const JSeg& sg, int r, long long* S, long long* E, int* cnt) {
+  if (sg.nchunk <= r + 1) return;
+  McuInfo M;
+  M.load(X.imgs[sg.img]);
+  const int cp_bits = X.chunk_bits / (kCheckpoints + 1);
+  for (int j = r + 1; j < sg.nchunk; ++j) {
+    const int i = sg.chunk0 + j;
+    const long long s = E[i - 1];
+    if (s == S[i]) continue;
+    S[i] = s;
+    if (j == sg.nchunk - 1) {
+      E[i] = kStateNone;
+      break;
+    }
+    BitStream bs;
+    chunk_stream(X, sg, st_pos(s), bs);
+    E[i] = chunk_sync(M, X.pool, luts, lstride, bs, st_b(s), st_k(s), (j + 1) * X.chunk_bits, cnt + 4 * i,
+                      j * X.chunk_bits, cp_bits, X.cps + (int64_t)i * kCheckpoints, true, E[i]);
+  }
+}
+
+// One thread per segment; returns at once when the last queued round changed nothing.
+__global__ __launch_bounds__(64) void jpeg_finish_kernel(ChunkCtx X, int nseg, int r, long long* __restrict__ S,
+                                                         long long* __restrict__ E, int* __restrict__ cnt,
+                                                         const int* __restrict__ last_changed) {
+  if (*last_changed == 0) return;
+  const int si = blockIdx.x * blockDim.x + threadIdx.x;
+  if (si < nseg) finish_segment(X, X.pool[0].look, kGlobalLutStride, X.segs[si], r, S, E, cnt);
+}
+
 // Exclusive scan of the chunk counts inside each segment: first block index and DC
 // predictors at every chunk's start.
 __host__ __device__ __forceinline__ void scan_segment(const ChunkCtx& X, const JSeg& sg, const int* cnt, int* G, int* P) {
@@ -1175,6 +1213,8 @@ struct Batch {
   std::vector<int> ic;                // (image << 2) | component of each run
   std::vector<int64_t> row_start;     // first output row of each image (rows of all images in order)
   std::vector<int> chunk_seg;         // segment of each chunk
+  std::vector<char> rdesc;            // ingest: resize descriptors of the batch's files (ef_image.hip ImgDesc)
+  int rcount = 0;
   int64_t words = 0;                  // 32-bit words reserved for the destuffed segments
   int chunk_bits = 0, warm_bits = 0;
   int64_t coef_blocks = 0, plane_bytes = 0, blocks = 0, rows = 0, dense_out = 0;
@@ -1335,13 +1375,14 @@ void make_chunks(Batch& B, int64_t opt_bits) {
 }
 
 // A built batch staged for upload: one pinned slot holds [destuffed words | images |
-// Huffman tables | quant tables | segments | IDCT runs | pixel starts]; the chunk table
-// (known only after destuffing) is uploaded from B.chunk_seg.
+// Huffman tables | quant tables | segments | IDCT runs | pixel starts | resize descriptors |
+// chunk table]; the chunk table is cut after destuffing, into room reserved for its bound.
+// The slot uploads as one copy of up_bytes into the device slot of the same index.
 struct Staged {
   int slot = 0;
   char* h = nullptr;
-  size_t o_words = 0, o_imgs = 0, o_pool = 0, o_q = 0, o_seg = 0, o_bs = 0, o_ic = 0, o_ps = 0, o_cseg = 0;
-  size_t pin_need = 0;
+  size_t o_words = 0, o_imgs = 0, o_pool = 0, o_q = 0, o_seg = 0, o_bs = 0, o_ic = 0, o_ps = 0, o_desc = 0, o_cseg = 0;
+  size_t pin_need = 0, up_bytes = 0;
 };
 
 // Host half of a decode: size / allocate pinned slot `slot` (waiting for the upload that last
@@ -1362,7 +1403,12 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   S.o_bs = off; off += al(B.block_start.size() * 8);
   S.o_ic = off; off += al(B.ic.size() * 4);
   S.o_ps = off; off += al(B.row_start.size() * 8);
+  S.o_desc = off; off += al(B.rdesc.size());
   S.o_cseg = off;  // chunk table last: its size is known only after destuffing
+  {  // make_chunks' bound: every segment has <= nbits / chunk_bits + 1 chunks
+    const int64_t cb_min = (c->opt_jpeg_chunk_bits > 0 || chunk_bits > 0) ? 64 : 2048;
+    off += al(((size_t)(B.words * 32 / cb_min) + B.segs.size() + 1) * 4);
+  }
   S.pin_need = off;
   if (c->jpeg_up_done[slot]) {  // the upload that last read this slot
     const hipError_t e = hipEventSynchronize(c->jpeg_up_done[slot]);
@@ -1394,23 +1440,44 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   std::memcpy(h + S.o_bs, B.block_start.data(), B.block_start.size() * 8);
   std::memcpy(h + S.o_ic, B.ic.data(), B.ic.size() * 4);
   std::memcpy(h + S.o_ps, B.row_start.data(), B.row_start.size() * 8);
+  if (!B.rdesc.empty()) std::memcpy(h + S.o_desc, B.rdesc.data(), B.rdesc.size());
+  std::memcpy(h + S.o_cseg, B.chunk_seg.data(), B.chunk_seg.size() * 4);
+  S.up_bytes = S.o_cseg + B.chunk_seg.size() * 4;
   tm.mark("tables");
   return EF_OK;
 }
 
-// Device half: upload a staged batch, entropy-decode, IDCT and colour-convert it into dout
-// (device), each image at its out_off.  Stream-ordered on ctx's stream.
-int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
+// ensure() for the buffers a queued decode may still use: a reallocation first waits for
+// the context's queued uploads and decodes (growth only; steady-state calls never wait).
+int jpeg_ensure(ef_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.p && b.bytes >= bytes) return EF_OK;
+  const hipError_t e = jpeg_quiesce(c);
+  if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
+  return ensure(c, b, bytes);
+}
+
+hipError_t jpeg_event(hipEvent_t* ev, hipStream_t record_on) {
+  if (*ev) return hipSuccess;
+  hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+  if (e == hipSuccess && record_on) e = hipEventRecord(*ev, record_on);  // waits on it pass until re-recorded
+  return e;
+}
+
+// Device half: upload a staged batch (copy stream), entropy-decode, IDCT and colour-convert
+// it into dout (device), each image at its out_off, then — for the ingest — resize the
+// batch's files into rz_dst (rz_row bytes each) from the descriptors staged with it.
+// Stream-ordered on ctx's stream and never waits on the host: the synchronisation rounds
+// are queued back to back (a round after the fixed point exits at once) and a batch that
+// has not converged after them is completed on the device (jpeg_finish_kernel).
+int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* rz_dst = nullptr,
+                 int64_t rz_row = 0) {
   hipStream_t s = c->stream;
   StageTimer tm;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  char* h = S.h;
+  const int slot = S.slot;
   const int nchunks = (int)B.chunk_seg.size();
-  const size_t up_bytes = S.o_cseg;
-  size_t off = S.o_cseg;
-  const size_t o_S = off + al((size_t)nchunks * 4);
-  off = o_S;
-  off += al((size_t)nchunks * 8);
+  size_t off = 0;
+  const size_t o_S = off; off += al((size_t)nchunks * 8);
   const size_t o_E0 = off; off += al((size_t)nchunks * 8);
   const size_t o_E1 = off; off += al((size_t)nchunks * 8);
   const size_t o_cnt = off; off += al((size_t)nchunks * 16);
@@ -1420,29 +1487,37 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
   const size_t o_cps = off; off += al((size_t)nchunks * kCheckpoints * sizeof(Checkpoint));
   const size_t o_coef = off; off += al((size_t)B.coef_blocks * 64 * 2);
   const size_t o_planes = off; off += al((size_t)B.plane_bytes + 16);
+  hipError_t e = hipSuccess;
+  if (!c->jpeg_copy) e = hipStreamCreateWithFlags(&c->jpeg_copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = jpeg_event(&c->jpeg_up_done[slot], nullptr);
+  if (e == hipSuccess) e = jpeg_event(&c->jpeg_ws_free[slot], s);
+  if (e == hipSuccess) e = jpeg_event(&c->jpeg_done, s);
+  if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   {
-    const int rc = ensure(c, c->jpeg_ws, off);
+    int rc = jpeg_ensure(c, c->jpeg_ws, off);
+    if (rc == EF_OK) rc = jpeg_ensure(c, c->jpeg_up[slot], S.up_bytes + 16);
     if (rc != EF_OK) return rc;
   }
-  if (!c->jpeg_up_done[S.slot]) {
-    const hipError_t e = hipEventCreateWithFlags(&c->jpeg_up_done[S.slot], hipEventDisableTiming);
-    if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
-  }
+  char* up = static_cast<char*>(c->jpeg_up[slot].p);
   char* base = static_cast<char*>(c->jpeg_ws.p);
-  const size_t o_seg = S.o_seg, o_imgs = S.o_imgs, o_pool = S.o_pool, o_words = S.o_words, o_cseg = S.o_cseg;
-  const size_t o_bs = S.o_bs, o_ic = S.o_ic, o_q = S.o_q, o_ps = S.o_ps;
-  hipError_t e = hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipEventRecord(c->jpeg_up_done[S.slot], s);
-  tm.mark("upload", s, true);
-  if (e == hipSuccess)  // pageable; complete before the first round's flag read below
-    e = hipMemcpyAsync(base + o_cseg, B.chunk_seg.data(), (size_t)nchunks * 4, hipMemcpyHostToDevice, s);
+  // upload on the copy stream once the kernels that last read this device slot are done;
+  // the compute stream waits for it and for the previous decode (shared workspace)
+  hipStream_t cs = c->jpeg_copy;
+  e = hipStreamWaitEvent(cs, c->jpeg_ws_free[slot], 0);
+  if (e == hipSuccess) e = hipMemcpyAsync(up, S.h, S.up_bytes, hipMemcpyHostToDevice, cs);
+  if (e == hipSuccess) e = hipEventRecord(c->jpeg_up_done[slot], cs);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, c->jpeg_up_done[slot], 0);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, c->jpeg_done, 0);
+  tm.mark("upload", cs, true);
+  TimerEvt tev;
+  timer_begin(c, EF_KERNEL_JPEG, &tev);
   if (e == hipSuccess) e = hipMemsetAsync(base + o_coef, 0, (size_t)B.coef_blocks * 64 * 2, s);
   ChunkCtx X;
-  X.chunk_seg = reinterpret_cast<const int*>(base + o_cseg);
-  X.segs = reinterpret_cast<const JSeg*>(base + o_seg);
-  X.imgs = reinterpret_cast<const JImage*>(base + o_imgs);
-  X.pool = reinterpret_cast<const HuffTab*>(base + o_pool);
-  X.words = reinterpret_cast<const unsigned*>(base + o_words);
+  X.chunk_seg = reinterpret_cast<const int*>(up + S.o_cseg);
+  X.segs = reinterpret_cast<const JSeg*>(up + S.o_seg);
+  X.imgs = reinterpret_cast<const JImage*>(up + S.o_imgs);
+  X.pool = reinterpret_cast<const HuffTab*>(up + S.o_pool);
+  X.words = reinterpret_cast<const unsigned*>(up + S.o_words);
   X.nchunks = nchunks;
   X.chunk_bits = B.chunk_bits;
   X.warm_bits = B.warm_bits;
@@ -1453,15 +1528,12 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
   int* G = reinterpret_cast<int*>(base + o_G);
   int* P = reinterpret_cast<int*>(base + o_P);
   int* flag = reinterpret_cast<int*>(base + o_flag);
-  int* hflag = reinterpret_cast<int*>(h + S.pin_need);  // in the pinned slot's slack
   int max_chunks = 1;
   for (const JSeg& sg : B.segs) max_chunks = std::max(max_chunks, sg.nchunk);
-  TimerEvt tev;
-  timer_begin(c, EF_KERNEL_JPEG, &tev);
   const unsigned cgrid = (unsigned)((nchunks + kChunkThreads - 1) / kChunkThreads);
   const int lds_tables = B.T.huff.size() <= (size_t)kLdsTables ? (int)B.T.huff.size() : 0;
   const size_t lds_bytes = (size_t)lds_tables * kLookSize * 2;
-  int rounds = 0;
+  const int nseg = (int)B.segs.size();
   // flag[r]: round r changed an exit state (r = 1 .. kDeviceRounds)
   if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4 * (kDeviceRounds + 2), s);
   if (e == hipSuccess) {
@@ -1469,13 +1541,10 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
                        E[0], cnt, flag, nullptr);
     e = hipGetLastError();
   }
-  // Synchronisation rounds until no start state changes (at most one per chunk of the
-  // longest segment: each round makes at least the next chunk in every segment exact).
-  // The first kDeviceRounds are queued back to back — a round after the fixed point exits
-  // at once (jpeg_sync_kernel prev_changed) — and the decode kernels behind them, so no
-  // host round trip separates the rounds; the host reads the flags once, while those
-  // kernels run, and only a batch that needs more rounds (rare) continues round by round
-  // and decodes again.
+  // Synchronisation rounds until no start state changes.  Round r makes chunk r of every
+  // segment exact, so a segment of m chunks needs at most m - 1; the first kDeviceRounds
+  // are queued back to back, and jpeg_finish_kernel completes whatever has not converged
+  // after them (nothing, in the test corpora and the bench set: 3-4 rounds).
   int cur = 0;
   const int qrounds = std::min(max_chunks, kDeviceRounds);
   for (int r = 1; e == hipSuccess && r <= qrounds; ++r) {
@@ -1484,81 +1553,69 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout) {
     e = hipGetLastError();
     cur ^= 1;
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4 * (qrounds + 1), hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && !c->jpeg_flags_read) e = hipEventCreateWithFlags(&c->jpeg_flags_read, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventRecord(c->jpeg_flags_read, s);
-  auto decode_kernels = [&]() {
-    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((B.segs.size() + 63) / 64)), dim3(64), 0, s, X,
-                       (int)B.segs.size(), cnt, G, P);
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S_, G,
-                       P, reinterpret_cast<short*>(base + o_coef));
-  };
-  if (e == hipSuccess) {
-    decode_kernels();
+  if (e == hipSuccess && max_chunks > qrounds) {
+    hipLaunchKernelGGL(jpeg_finish_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, X, nseg, qrounds, S_,
+                       E[cur], cnt, flag + qrounds);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipEventSynchronize(c->jpeg_flags_read);
+  tm.mark("sync-rounds", s, true);
   if (e == hipSuccess) {
-    rounds = qrounds;
-    for (int r = 1; r <= qrounds; ++r)
-      if (hflag[r] == 0) {
-        rounds = r;
-        break;
-      }
-    if (rounds == qrounds && hflag[qrounds] != 0 && qrounds < max_chunks) {
-      // not converged within the queued rounds: continue round by round, then decode again
-      for (int r = qrounds + 1; e == hipSuccess && r <= max_chunks; ++r) {
-        e = hipMemsetAsync(flag, 0, 4, s);
-        if (e != hipSuccess) break;
-        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes, s, X, lds_tables, r, S_,
-                           E[cur], E[cur ^ 1], cnt, flag, nullptr);
-        e = hipGetLastError();
-        cur ^= 1;
-        rounds = r;
-        if (e == hipSuccess) e = hipMemcpyAsync(hflag, flag, 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess || *hflag == 0) break;
-      }
-      if (e == hipSuccess) e = hipMemsetAsync(base + o_coef, 0, (size_t)B.coef_blocks * 64 * 2, s);
-      if (e == hipSuccess) {
-        decode_kernels();
-        e = hipGetLastError();
-      }
-    }
+    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((unsigned)((nseg + 63) / 64)), dim3(64), 0, s, X, nseg, cnt, G, P);
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(cgrid), dim3(kChunkThreads), lds_bytes + 128, s, X, lds_tables, S_, G,
+                       P, reinterpret_cast<short*>(base + o_coef));
+    e = hipGetLastError();
   }
-  c->jpeg_rounds = rounds;
-  tm.mark("sync-rounds");
   if (e == hipSuccess) {
     const JImage* d_imgs = X.imgs;
     short* d_coef = reinterpret_cast<short*>(base + o_coef);
     uint8_t* d_planes = reinterpret_cast<uint8_t*>(base + o_planes);
     if (B.blocks > 0)
       hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((B.blocks + kIdctBlocks - 1) / kIdctBlocks)), dim3(256), 0,
-                         s, d_coef, d_imgs, reinterpret_cast<const int64_t*>(base + o_bs), (int)B.block_start.size(),
-                         reinterpret_cast<const int*>(base + o_ic), reinterpret_cast<const unsigned short*>(base + o_q),
+                         s, d_coef, d_imgs, reinterpret_cast<const int64_t*>(up + S.o_bs), (int)B.block_start.size(),
+                         reinterpret_cast<const int*>(up + S.o_ic), reinterpret_cast<const unsigned short*>(up + S.o_q),
                          B.blocks, d_planes);
     if (B.rows > 0)
       hipLaunchKernelGGL(jpeg_out_kernel, dim3((unsigned)((B.rows + 3) / 4)), dim3(256), 0, s, d_imgs,
-                         reinterpret_cast<const int64_t*>(base + o_ps), (int)B.imgs.size(), B.rows, d_planes, dout);
+                         reinterpret_cast<const int64_t*>(up + S.o_ps), (int)B.imgs.size(), B.rows, d_planes, dout);
     e = hipGetLastError();
   }
   timer_end(c, &tev);
+  if (e == hipSuccess && rz_dst && B.rcount > 0) {
+    // files the decoder did not take resize from 16 zero bytes past the batch's pixels
+    e = hipMemsetAsync(dout + B.dense_out, 0, 16, s);
+    TimerEvt tr;
+    timer_begin(c, EF_KERNEL_INGEST, &tr);
+    if (e == hipSuccess) e = launch_resize_gray(s, dout, up + S.o_desc, B.rcount, rz_row, rz_dst);
+    timer_end(c, &tr);
+  }
+  if (e == hipSuccess) e = hipEventRecord(c->jpeg_ws_free[slot], s);
+  if (e == hipSuccess) e = hipEventRecord(c->jpeg_done, s);
   tm.mark("kernels", s, true);
   if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   return EF_OK;
 }
 
 
-// Host and device halves in sequence (one slot).
+// Host and device halves in sequence (the context's next slot).
 int decode_batch(ef_ctx* c, Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* dout) {
   Staged S;
   std::string err;
-  const int rc = stage_batch(c, 0, B, data, offsets, S, &err);
+  const int slot = c->jpeg_slot;
+  c->jpeg_slot ^= 1;
+  const int rc = stage_batch(c, slot, B, data, offsets, S, &err);
   if (rc != EF_OK) return set_err(c, rc, "jpeg decode: " + err);
   return launch_batch(c, B, S, dout);
 }
 
 }  // namespace
+
+hipError_t jpeg_quiesce(ef_ctx* c) {
+  hipError_t e = hipSuccess;
+  if (c->jpeg_done) e = hipEventSynchronize(c->jpeg_done);
+  if (e == hipSuccess && c->jpeg_copy) e = hipStreamSynchronize(c->jpeg_copy);
+  return e;
+}
+
 }  // namespace ef
 
 using namespace ef;
@@ -1622,18 +1679,18 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
   (void)hipSetDevice(c->device);
   const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   const int64_t row = (int64_t)out_h * out_w;
-  // Parts of ~kIngestPart files: while part i uploads, synchronises and decodes on the
-  // device (its rounds block this thread on the stream), a host thread parses and destuffs
-  // part i + 1 into the other pinned slot.
+  // Parts of ~kIngestPart files, each staged (parse, destuff, tables, chunks, resize
+  // descriptors) into one of the context's two upload slots, the next part on a host thread
+  // while this one is queued.  Nothing in a part's device work waits on the host (see
+  // launch_batch), so with device output the call returns once every part is queued, and
+  // the next call's host staging overlaps this call's decode.
   // Parts keep the whole call's entropy-chunk size (a part sized on its own would cut
   // twice as many, shorter chunks, whose warm-up and synchronisation cost more than the
-  // overlap wins).  Measured at 4096 face crops (profiles/r02/jpeg): one part 10.2 ms,
-  // two parts 10.7 ms, four 14.7 ms — each part pays its synchronisation rounds' host
-  // round trips and decodes fewer chunks at once — so calls up to EF_OPT_JPEG_PART_FILES
-  // (8192) files run as one part.
+  // overlap wins).  Calls up to EF_OPT_JPEG_PART_FILES (8192) files run as one part.
   const int32_t kIngestPart = (int32_t)std::max<int64_t>(1, c->opt_jpeg_part_files);
   struct Part {
     int32_t a = 0, m = 0;
+    int slot = 0;
     Batch B;
     Staged S;
     std::vector<int32_t> st;
@@ -1641,17 +1698,30 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     std::string err;
   };
   int64_t call_chunk_bits = 0;
-  auto prepare = [&](Part& P, int slot) {
+  const size_t dsz = img_desc_size();
+  auto prepare = [&](Part& P) {
     (void)hipSetDevice(c->device);  // a fresh host thread starts on device 0
     P.st.assign(P.m, 0);
     build_batch(data, offsets + P.a, sizes + P.a, P.m, mode, nullptr, P.st.data(), P.B);
-    if (!P.B.imgs.empty()) P.rc = stage_batch(c, slot, P.B, data, offsets + P.a, P.S, &P.err, call_chunk_bits);
+    if (P.B.imgs.empty()) return;
+    // resize descriptors: file j of the part -> row j; a file the GPU decoder does not take
+    // reads as a 1x1 zero image placed after the batch's pixels
+    Batch& B = P.B;
+    B.rcount = P.m;
+    B.rdesc.assign((size_t)P.m * dsz, 0);
+    for (int32_t j = 0; j < P.m; ++j) img_desc_fill(B.rdesc.data() + j * dsz, B.dense_out, j * row, 1, 1, 1, out_h, out_w);
+    for (size_t q = 0; q < B.imgs.size(); ++q) {
+      const JImage& im = B.imgs[q];
+      img_desc_fill(B.rdesc.data() + (size_t)B.img_of[q] * dsz, im.out_off, (int64_t)B.img_of[q] * row, im.h, im.w, ch,
+                    out_h, out_w);
+    }
+    P.rc = stage_batch(c, P.slot, B, data, offsets + P.a, P.S, &P.err, call_chunk_bits);
   };
-  for (int32_t a0 = 0; a0 < count; a0 += 65535) {  // ef_preprocess's per-call image limit
+  for (int32_t a0 = 0; a0 < count; a0 += 65535) {  // the resize launch's per-launch image limit
     const int32_t m0 = std::min<int32_t>(65535, count - a0);
     uint8_t* rows_all = out + (int64_t)a0 * row;
     if (!(flags & EF_MEM_DEVICE)) {  // host rows: resize into device staging, then copy out
-      const int rc = ensure(c, c->jpeg_rows, (size_t)m0 * row);
+      const int rc = jpeg_ensure(c, c->jpeg_rows, (size_t)m0 * row);
       if (rc != EF_OK) return rc;
       rows_all = static_cast<uint8_t*>(c->jpeg_rows.p);
     }
@@ -1664,38 +1734,25 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     for (int32_t i = 0; i < nparts; ++i) {
       parts[i].a = a0 + (int32_t)((int64_t)m0 * i / nparts);
       parts[i].m = a0 + (int32_t)((int64_t)m0 * (i + 1) / nparts) - parts[i].a;
+      parts[i].slot = c->jpeg_slot;
+      c->jpeg_slot ^= 1;
     }
-    prepare(parts[0], 0);
+    // one pixel buffer for the whole call, sized for its largest part (growing it waits for
+    // the queued decodes that use it)
+    prepare(parts[0]);
     for (int32_t i = 0; i < nparts; ++i) {
       Part& P = parts[i];
       std::thread next;
-      if (i + 1 < nparts) next = std::thread(prepare, std::ref(parts[i + 1]), (i + 1) & 1);
+      if (i + 1 < nparts) next = std::thread(prepare, std::ref(parts[i + 1]));
       int rc = P.rc != EF_OK ? set_err(c, P.rc, "ef_jpeg_ingest: " + P.err) : EF_OK;
-      uint8_t* pix = nullptr;
-      if (rc == EF_OK) rc = ensure(c, c->jpeg_out, (size_t)P.B.dense_out + 256);
-      if (rc == EF_OK) {
-        pix = static_cast<uint8_t*>(c->jpeg_out.p);
-        if (!P.B.imgs.empty()) rc = launch_batch(c, P.B, P.S, pix);
+      uint8_t* dst = rows_all + (int64_t)(P.a - a0) * row;
+      if (rc == EF_OK && P.B.imgs.empty()) {  // no file of the part decodes here: zero rows
+        const hipError_t e = hipMemsetAsync(dst, 0, (size_t)P.m * row, c->stream);
+        if (e != hipSuccess) rc = hip_err(c, e, "jpeg ingest");
+      } else if (rc == EF_OK) {
+        rc = jpeg_ensure(c, c->jpeg_out, (size_t)P.B.dense_out + 256);
+        if (rc == EF_OK) rc = launch_batch(c, P.B, P.S, static_cast<uint8_t*>(c->jpeg_out.p), dst, row);
       }
-      std::vector<int32_t> hh(P.m, 1), ww(P.m, 1), cc(P.m, 1);
-      std::vector<int64_t> doff(P.m, P.B.dense_out);
-      if (rc == EF_OK) {
-        // a file the GPU decoder does not take becomes a 1x1 zero image: its row is zero
-        for (size_t j = 0; j < P.B.imgs.size(); ++j) {
-          const int k = P.B.img_of[j];
-          doff[k] = P.B.imgs[j].out_off;
-          hh[k] = P.B.imgs[j].h;
-          ww[k] = P.B.imgs[j].w;
-          cc[k] = ch;
-        }
-        if ((int32_t)P.B.imgs.size() < P.m) {
-          const hipError_t e = hipMemsetAsync(pix + P.B.dense_out, 0, 16, c->stream);
-          if (e != hipSuccess) rc = hip_err(c, e, "jpeg ingest");
-        }
-      }
-      if (rc == EF_OK)
-        rc = ef_preprocess(c, pix, doff.data(), hh.data(), ww.data(), cc.data(), P.m, out_h, out_w,
-                           rows_all + (int64_t)(P.a - a0) * row, EF_MEM_DEVICE);
       if (next.joinable()) next.join();  // before any return: the thread uses parts[i + 1]
       if (rc != EF_OK) return rc;
       if (status) std::memcpy(status + P.a, P.st.data(), (size_t)P.m * 4);
@@ -1740,7 +1797,11 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   long long* Ein = E0.data();
   long long* Eout = E1.data();
   int rounds = 0;
-  for (int r = 1; r <= nch + 1; ++r) {
+  // EF_JPEG_QROUNDS=q: stop after q rounds and complete with finish_segment, as the device
+  // does after its queued rounds
+  const char* qenv = std::getenv("EF_JPEG_QROUNDS");
+  const int qmax = qenv ? std::max(1, std::atoi(qenv)) : nch + 1;
+  for (int r = 1; r <= std::min(qmax, nch + 1); ++r) {
     changed = 0;
     const std::vector<long long> S0 = S;
     for (int i = 0; i < nch; ++i) sync_chunk(X, luts, ls, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
@@ -1750,6 +1811,10 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
     std::swap(Ein, Eout);
     rounds = r;
     if (!changed) break;
+  }
+  if (changed) {
+    for (const JSeg& sg : B.segs) finish_segment(X, luts, ls, sg, rounds, S.data(), Ein, cnt.data());
+    std::fprintf(stderr, "finished after %d rounds\n", rounds);
   }
   if (rounds_out) *rounds_out = rounds;
   if (std::getenv("EF_JPEG_CHECK")) {  // recompute every non-last chunk's counts and exit from its start

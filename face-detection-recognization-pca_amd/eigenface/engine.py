@@ -574,7 +574,11 @@ class Engine:
     def ingest_jpegs(self, blobs, size=(64, 64), mode="bgr", out=None):
         """Fused GPU decode + grey + INTER_LINEAR resize of JPEG files
         (ef_jpeg_ingest): (rows uint8 (n, h*w) — or device tensor ``out`` filled —,
-        status int32 (n,)).  Rows of files with status != 0 are zero."""
+        status int32 (n,)).  Rows of files with status != 0 are zero.  With ``out`` the
+        call returns once the decode is queued on the engine's stream (status is final):
+        synchronise (``synchronize()``, or run the engine on torch's stream) before
+        reading ``out``; back-to-back calls overlap one batch's host staging with the
+        previous batch's decode."""
         m = _jpeg_mode(mode)
         ow, oh = int(size[0]), int(size[1])
         n = len(blobs)

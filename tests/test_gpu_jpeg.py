@@ -136,3 +136,44 @@ def test_ingest_parts_host_output_status(eng):
     np.testing.assert_array_equal(out.cpu().numpy(), rows)
     for i in [0, 1022, 1025, 1699, 1701, 2498]:
         np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(blobs[i], "gray"), (64, 64)))
+
+
+@pytest.mark.parametrize("chunk_bits", [64, 512])
+def test_unconverged_rounds_finish_on_device(eng, corpus, chunk_bits):
+    """Chunks far shorter than the self-synchronisation distance: the queued rounds do not
+    reach the fixed point (64-bit chunks need one round per chunk, ~1100 on this corpus), so
+    jpeg_finish_kernel completes every segment sequentially on the device — still bit-exact."""
+    blobs = [b for _, b in corpus]
+    eng.set_option("jpeg_chunk_bits", chunk_bits)
+    try:
+        got = eng.decode_jpegs(blobs, "bgr")
+        rows, st = eng.ingest_jpegs(blobs, (64, 64), "gray")
+    finally:
+        eng.set_option("jpeg_chunk_bits", 0)
+    assert (st == 0).all()
+    for (name, b), g, r in zip(corpus, got, rows):
+        np.testing.assert_array_equal(g, J.decode_ref(b, "bgr"), err_msg=f"{chunk_bits} {name}")
+        np.testing.assert_array_equal(r, io_oracle.preprocess(J.decode_ref(b, "gray"), (64, 64)),
+                                      err_msg=f"{chunk_bits} {name}")
+
+
+def test_back_to_back_device_ingests(eng):
+    """Device-output ingests return once queued: consecutive calls alternate the two upload
+    slots, the next call's staging overlapping this call's decode.  Four calls of different
+    batches (and sizes, so buffers grow in between) into separate tensors, one sync at the
+    end: every row equals a synchronous host-output ingest of the same batch."""
+    import torch
+    batches = []
+    for c, n in enumerate([700, 1300, 400, 1300]):
+        batches.append([J.encode(J.smooth_image(40 + (k * 7 + c) % 90, 50 + (k * 3 + c) % 70, 3, 1000 * c + k),
+                                 quality=55 + (k + c) % 45, subsampling=(k + c) % 3) for k in range(n)])
+    outs = [torch.empty((len(b), 32 * 32), dtype=torch.uint8, device="cuda") for b in batches]
+    sts = [eng.ingest_jpegs(b, (32, 32), "bgr", out=o)[1] for b, o in zip(batches, outs)]
+    torch.cuda.synchronize()
+    for b, o, st in zip(batches, outs, sts):
+        ref, ref_st = eng.ingest_jpegs(b, (32, 32), "bgr")
+        np.testing.assert_array_equal(st, ref_st)
+        np.testing.assert_array_equal(o.cpu().numpy(), ref)
+    for i in range(0, len(batches[1]), 101):
+        np.testing.assert_array_equal(outs[1][i].cpu().numpy(),
+                                      io_oracle.preprocess(J.decode_ref(batches[1][i], "bgr"), (32, 32)))
