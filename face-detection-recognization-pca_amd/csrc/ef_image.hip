@@ -42,6 +42,7 @@
 
 #include "ef_dma.hpp"
 #include "ef_internal.hpp"
+#include "ef_resize.hpp"
 
 namespace ef {
 
@@ -66,25 +67,6 @@ struct ImgDesc {
   int h, w, c, oh, ow, pad;
 };
 
-// One axis of OpenCV's INTER_LINEAR setup (resizeGeneric_): source pair and 11-bit
-// weights.  Horizontal: borders clamp the index AND zero the fraction; vertical: only
-// the source rows clamp.  Separate roundings as in the reference (no FMA contraction).
-__device__ __forceinline__ void lin_axis(int dpos, int n_in, int n_out, bool zero_borders, int& i0, int& i1,
-                                         int& c0, int& c1) {
-  const double scale = __ddiv_rn(1.0, __ddiv_rn((double)n_out, (double)n_in));  // 1 / inv_scale
-  float f = __double2float_rn(__dadd_rn(__dmul_rn(__dadd_rn((double)dpos, 0.5), scale), -0.5));
-  int s = (int)floorf(f);
-  f = __fsub_rn(f, (float)s);
-  if (zero_borders) {
-    if (s < 0) { f = 0.f; s = 0; }
-    if (s >= n_in - 1) { f = 0.f; s = n_in - 1; }
-  }
-  c0 = __float2int_rn(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
-  c1 = __float2int_rn(__fmul_rn(f, 2048.f));
-  i0 = s < 0 ? 0 : (s > n_in - 1 ? n_in - 1 : s);
-  i1 = s + 1 < 0 ? 0 : (s + 1 > n_in - 1 ? n_in - 1 : s + 1);
-}
-
 template <bool RGB>
 __device__ __forceinline__ int gray_at(const uint8_t* __restrict__ src, int w, int c, int y, int x) {
   const uint8_t* p = src + ((int64_t)y * w + x) * c;
@@ -102,22 +84,8 @@ __global__ __launch_bounds__(256) void resize_kernel(const uint8_t* __restrict__
   if (o >= dd.oh * dd.ow) return;
   const int dy = o / dd.ow, dx = o - (o / dd.ow) * dd.ow;
   const uint8_t* s = src + dd.src_off;
-  int v;
-  if (dd.oh == dd.h && dd.ow == dd.w) {  // dsize == ssize: copy
-    v = gray_at<RGB>(s, dd.w, dd.c, dy, dx);
-  } else if (dd.h == 2 * dd.oh && dd.w == 2 * dd.ow) {  // INTER_AREA fast path (exact 2x)
-    const int y = 2 * dy, x = 2 * dx;
-    v = (gray_at<RGB>(s, dd.w, dd.c, y, x) + gray_at<RGB>(s, dd.w, dd.c, y, x + 1) +
-         gray_at<RGB>(s, dd.w, dd.c, y + 1, x) + gray_at<RGB>(s, dd.w, dd.c, y + 1, x + 1) + 2) >> 2;
-  } else {
-    int x0, x1, a0, a1, y0, y1, b0, b1;
-    lin_axis(dx, dd.w, dd.ow, true, x0, x1, a0, a1);
-    lin_axis(dy, dd.h, dd.oh, false, y0, y1, b0, b1);
-    const int d0 = gray_at<RGB>(s, dd.w, dd.c, y0, x0) * a0 + gray_at<RGB>(s, dd.w, dd.c, y0, x1) * a1;
-    const int d1 = gray_at<RGB>(s, dd.w, dd.c, y1, x0) * a0 + gray_at<RGB>(s, dd.w, dd.c, y1, x1) * a1;
-    v = (((b0 * (d0 >> 4)) >> 16) + ((b1 * (d1 >> 4)) >> 16) + 2) >> 2;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-  }
+  const auto gray = [&](int y, int x) { return gray_at<RGB>(s, dd.w, dd.c, y, x); };
+  const int v = resize_px(gray, dd.h, dd.w, dd.oh, dd.ow, dy, dx);
   dst[dd.dst_off + o] = (uint8_t)v;
 }
 

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "ef_internal.hpp"
+#include "ef_resize.hpp"
 
 namespace ef {
 namespace {
@@ -1182,6 +1183,40 @@ __global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict_
   for (int x0 = 4 * (threadIdx.x & 63); x0 < im.w; x0 += 256) out_quad(im, y, x0, planes, out);
 }
 
+// Ingest: the grey value cvtColor(BGR2GRAY) gives at pixel (y, x) of the decoded image —
+// the luma plane for grey output or a one-component file (B = G = R = Y makes BT.601's
+// weighted sum exactly Y), else out_pixel's upsample + YCC->BGR followed by
+// (1868 B + 9617 G + 4899 R + 2^13) >> 14.
+__device__ __forceinline__ int grey_px(const JImage& im, int y, int x, const uint8_t* planes) {
+  const int Y = planes[im.c[0].plane_off + (int64_t)y * im.c[0].bw * 8 + x];
+  if (im.mode == EF_JPEG_GRAY || im.nc == 1) return Y;
+  const int cb = upsample(planes + im.c[1].plane_off, im.c[1], im.hmax, im.vmax, y, x);
+  const int cr = upsample(planes + im.c[2].plane_off, im.c[2], im.hmax, im.vmax, y, x);
+  const int b = clamp255(Y + cb_b(cb)), g = clamp255(Y + cbcr_g(cb, cr)), r = clamp255(Y + cr_r(cr));
+  return (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14;
+}
+
+// Ingest: row f of the output (oh x ow grey, ef_preprocess's arithmetic) straight from the
+// decoded planes, without writing the full-size BGR image and reading it back: grid
+// (ceil(oh*ow / 256), files), thread = output pixel; file_img[f] < 0 (a file the decoder
+// does not take) gives a zero row, as the resize of a 1x1 zero image does.
+__global__ __launch_bounds__(256) void jpeg_resize_kernel(const JImage* __restrict__ imgs, const int* __restrict__ file_img,
+                                                         const uint8_t* __restrict__ planes, int oh, int ow,
+                                                         uint8_t* __restrict__ dst) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= oh * ow) return;
+  uint8_t* row = dst + (int64_t)blockIdx.y * oh * ow;
+  const int ii = file_img[blockIdx.y];
+  if (ii < 0) {
+    row[o] = 0;
+    return;
+  }
+  const JImage& im = imgs[ii];
+  const int dy = o / ow, dx = o - dy * ow;
+  const auto gray = [&](int y, int x) { return grey_px(im, y, x, planes); };
+  row[o] = (uint8_t)resize_px(gray, im.h, im.w, oh, ow, dy, dx);
+}
+
 // Diagnostic build: wall time of the host stages of a decode (EF_JPEG_TIMES=1 prints them).
 #ifdef EF_DIAGNOSTICS
 struct StageTimer {
@@ -1213,8 +1248,7 @@ struct Batch {
   std::vector<int> ic;                // (image << 2) | component of each run
   std::vector<int64_t> row_start;     // first output row of each image (rows of all images in order)
   std::vector<int> chunk_seg;         // segment of each chunk
-  std::vector<char> rdesc;            // ingest: resize descriptors of the batch's files (ef_image.hip ImgDesc)
-  int rcount = 0;
+  std::vector<int> file_img;          // ingest: image of each input file of the batch (-1: not decoded here)
   int64_t words = 0;                  // 32-bit words reserved for the destuffed segments
   int chunk_bits = 0, warm_bits = 0;
   int64_t coef_blocks = 0, plane_bytes = 0, blocks = 0, rows = 0, dense_out = 0;
@@ -1375,7 +1409,7 @@ void make_chunks(Batch& B, int64_t opt_bits) {
 }
 
 // A built batch staged for upload: one pinned slot holds [destuffed words | images |
-// Huffman tables | quant tables | segments | IDCT runs | pixel starts | resize descriptors |
+// Huffman tables | quant tables | segments | IDCT runs | pixel starts | file -> image map |
 // chunk table]; the chunk table is cut after destuffing, into room reserved for its bound.
 // The slot uploads as one copy of up_bytes into the device slot of the same index.
 struct Staged {
@@ -1403,7 +1437,7 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   S.o_bs = off; off += al(B.block_start.size() * 8);
   S.o_ic = off; off += al(B.ic.size() * 4);
   S.o_ps = off; off += al(B.row_start.size() * 8);
-  S.o_desc = off; off += al(B.rdesc.size());
+  S.o_desc = off; off += al(B.file_img.size() * 4);
   S.o_cseg = off;  // chunk table last: its size is known only after destuffing
   {  // make_chunks' bound: every segment has <= nbits / chunk_bits + 1 chunks
     const int64_t cb_min = (c->opt_jpeg_chunk_bits > 0 || chunk_bits > 0) ? 64 : 2048;
@@ -1440,7 +1474,7 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   std::memcpy(h + S.o_bs, B.block_start.data(), B.block_start.size() * 8);
   std::memcpy(h + S.o_ic, B.ic.data(), B.ic.size() * 4);
   std::memcpy(h + S.o_ps, B.row_start.data(), B.row_start.size() * 8);
-  if (!B.rdesc.empty()) std::memcpy(h + S.o_desc, B.rdesc.data(), B.rdesc.size());
+  if (!B.file_img.empty()) std::memcpy(h + S.o_desc, B.file_img.data(), B.file_img.size() * 4);
   std::memcpy(h + S.o_cseg, B.chunk_seg.data(), B.chunk_seg.size() * 4);
   S.up_bytes = S.o_cseg + B.chunk_seg.size() * 4;
   tm.mark("tables");
@@ -1463,14 +1497,15 @@ hipError_t jpeg_event(hipEvent_t* ev, hipStream_t record_on) {
   return e;
 }
 
-// Device half: upload a staged batch (copy stream), entropy-decode, IDCT and colour-convert
-// it into dout (device), each image at its out_off, then — for the ingest — resize the
-// batch's files into rz_dst (rz_row bytes each) from the descriptors staged with it.
+// Device half: upload a staged batch (copy stream), entropy-decode and IDCT it, then either
+// colour-convert it into dout (device), each image at its out_off, or — for the ingest
+// (rz_dst) — resize every file of the batch to an (oh x ow) grey row of rz_dst straight from
+// the planes (jpeg_resize_kernel, file -> image map staged with the batch).
 // Stream-ordered on ctx's stream and never waits on the host: the synchronisation rounds
 // are queued back to back (a round after the fixed point exits at once) and a batch that
 // has not converged after them is completed on the device (jpeg_finish_kernel).
-int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* rz_dst = nullptr,
-                 int64_t rz_row = 0) {
+int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* rz_dst = nullptr, int oh = 0,
+                 int ow = 0) {
   hipStream_t s = c->stream;
   StageTimer tm;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -1574,18 +1609,19 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
                          s, d_coef, d_imgs, reinterpret_cast<const int64_t*>(up + S.o_bs), (int)B.block_start.size(),
                          reinterpret_cast<const int*>(up + S.o_ic), reinterpret_cast<const unsigned short*>(up + S.o_q),
                          B.blocks, d_planes);
-    if (B.rows > 0)
+    if (B.rows > 0 && !rz_dst)
       hipLaunchKernelGGL(jpeg_out_kernel, dim3((unsigned)((B.rows + 3) / 4)), dim3(256), 0, s, d_imgs,
                          reinterpret_cast<const int64_t*>(up + S.o_ps), (int)B.imgs.size(), B.rows, d_planes, dout);
     e = hipGetLastError();
   }
   timer_end(c, &tev);
-  if (e == hipSuccess && rz_dst && B.rcount > 0) {
-    // files the decoder did not take resize from 16 zero bytes past the batch's pixels
-    e = hipMemsetAsync(dout + B.dense_out, 0, 16, s);
+  if (e == hipSuccess && rz_dst && !B.file_img.empty()) {
     TimerEvt tr;
     timer_begin(c, EF_KERNEL_INGEST, &tr);
-    if (e == hipSuccess) e = launch_resize_gray(s, dout, up + S.o_desc, B.rcount, rz_row, rz_dst);
+    hipLaunchKernelGGL(jpeg_resize_kernel, dim3((unsigned)(((int64_t)oh * ow + 255) / 256), (unsigned)B.file_img.size()),
+                       dim3(256), 0, s, X.imgs, reinterpret_cast<const int*>(up + S.o_desc),
+                       reinterpret_cast<const uint8_t*>(base + o_planes), oh, ow, rz_dst);
+    e = hipGetLastError();
     timer_end(c, &tr);
   }
   if (e == hipSuccess) e = hipEventRecord(c->jpeg_ws_free[slot], s);
@@ -1677,10 +1713,9 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     return set_err(c, EF_E_INVALID, "ef_jpeg_ingest: bad arguments");
   if (count == 0) return EF_OK;
   (void)hipSetDevice(c->device);
-  const int ch = mode == EF_JPEG_GRAY ? 1 : 3;
   const int64_t row = (int64_t)out_h * out_w;
-  // Parts of ~kIngestPart files, each staged (parse, destuff, tables, chunks, resize
-  // descriptors) into one of the context's two upload slots, the next part on a host thread
+  // Parts of ~kIngestPart files, each staged (parse, destuff, tables, chunks, file -> image
+  // map) into one of the context's two upload slots, the next part on a host thread
   // while this one is queued.  Nothing in a part's device work waits on the host (see
   // launch_batch), so with device output the call returns once every part is queued, and
   // the next call's host staging overlaps this call's decode.
@@ -1698,23 +1733,14 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     std::string err;
   };
   int64_t call_chunk_bits = 0;
-  const size_t dsz = img_desc_size();
   auto prepare = [&](Part& P) {
     (void)hipSetDevice(c->device);  // a fresh host thread starts on device 0
     P.st.assign(P.m, 0);
     build_batch(data, offsets + P.a, sizes + P.a, P.m, mode, nullptr, P.st.data(), P.B);
     if (P.B.imgs.empty()) return;
-    // resize descriptors: file j of the part -> row j; a file the GPU decoder does not take
-    // reads as a 1x1 zero image placed after the batch's pixels
     Batch& B = P.B;
-    B.rcount = P.m;
-    B.rdesc.assign((size_t)P.m * dsz, 0);
-    for (int32_t j = 0; j < P.m; ++j) img_desc_fill(B.rdesc.data() + j * dsz, B.dense_out, j * row, 1, 1, 1, out_h, out_w);
-    for (size_t q = 0; q < B.imgs.size(); ++q) {
-      const JImage& im = B.imgs[q];
-      img_desc_fill(B.rdesc.data() + (size_t)B.img_of[q] * dsz, im.out_off, (int64_t)B.img_of[q] * row, im.h, im.w, ch,
-                    out_h, out_w);
-    }
+    B.file_img.assign((size_t)P.m, -1);  // file j of the part -> row j
+    for (size_t q = 0; q < B.imgs.size(); ++q) B.file_img[(size_t)B.img_of[q]] = (int)q;
     P.rc = stage_batch(c, P.slot, B, data, offsets + P.a, P.S, &P.err, call_chunk_bits);
   };
   for (int32_t a0 = 0; a0 < count; a0 += 65535) {  // the resize launch's per-launch image limit
@@ -1737,8 +1763,6 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       parts[i].slot = c->jpeg_slot;
       c->jpeg_slot ^= 1;
     }
-    // one pixel buffer for the whole call, sized for its largest part (growing it waits for
-    // the queued decodes that use it)
     prepare(parts[0]);
     for (int32_t i = 0; i < nparts; ++i) {
       Part& P = parts[i];
@@ -1750,8 +1774,7 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
         const hipError_t e = hipMemsetAsync(dst, 0, (size_t)P.m * row, c->stream);
         if (e != hipSuccess) rc = hip_err(c, e, "jpeg ingest");
       } else if (rc == EF_OK) {
-        rc = jpeg_ensure(c, c->jpeg_out, (size_t)P.B.dense_out + 256);
-        if (rc == EF_OK) rc = launch_batch(c, P.B, P.S, static_cast<uint8_t*>(c->jpeg_out.p), dst, row);
+        rc = launch_batch(c, P.B, P.S, nullptr, dst, out_h, out_w);
       }
       if (next.joinable()) next.join();  // before any return: the thread uses parts[i + 1]
       if (rc != EF_OK) return rc;

@@ -72,21 +72,24 @@ def test_detect_faces_and_save_data_layout(tmp_path):
                              "center_y", "area", "image_path", "image_filename"}
 
 
-@pytest.mark.parametrize("tiny_leaf", [False, True])
-def test_long_cascade_split_and_ordered_paths(tiny_leaf):
-    """A 12-stage cascade reaches the late stage groups (split kernel when the stage sums
-    are order-free; a 1e-12 leaf value makes them order-dependent and forces the
-    sequential thread-per-window form) — both must equal the oracle's candidates."""
+@pytest.mark.parametrize("tiny_leaf,nst,shape,seed", [(False, 12, (120, 160), 7), (True, 12, (120, 160), 7),
+                                                      (False, 20, (150, 200), 8)])
+def test_long_cascade_split_and_ordered_paths(tiny_leaf, nst, shape, seed):
+    """A 12- or 20-stage cascade reaches the late stage groups (stages 1-3 in the split
+    kernel, 4 on in the LDS-patch kernel when the stage sums are order-free; a 1e-12 leaf
+    value makes them order-dependent and forces the sequential thread-per-window form) —
+    every form must equal the oracle's candidates."""
     from eigenface.haar import CascadeClassifier
-    c = synth_cascade(7, n_feat=60, stages=(3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25), loose=2.0)
+    c = synth_cascade(seed, n_feat=60, stages=tuple(range(3, 3 + 2 * nst, 2)), loose=2.0 if nst <= 12 else 2.7)
     if tiny_leaf:
         thr, stumps = c["stages"][7]
         f, t, left, right = stumps[0]
         stumps[0] = (f, t, float(np.float32(1e-12)), right)
-    f = synth_frame(3, (120, 160))
+    f = synth_frame(3, shape)
     clf = CascadeClassifier(cascade=c)
     rects, cand = clf.detect(f, 1.1, 2, (0, 0), return_candidates=True)
     ref_cand = ho.candidates(f, c, 1.1, (0, 0))
     assert len(ref_cand) > 0  # windows survive every stage, so the late groups ran
     assert [tuple(r) for r in cand] == ref_cand
-    assert [tuple(r) for r in rects] == ho.group_rectangles(ref_cand, 2)
+    if len(ref_cand) <= 2000:  # the oracle's grouping is quadratic in pure Python
+        assert [tuple(r) for r in rects] == ho.group_rectangles(ref_cand, 2)
