@@ -451,9 +451,9 @@ __global__ __launch_bounds__(NQ * 64) void haar_cascade_split_kernel(const HaarL
 // half h takes stumps 2q+h, 2q+h+16, … of each stage from LDS records; the 16 partial sums
 // of a window are added in LDS (order-free cascades only, as the split form).  The patch
 // stride is odd, so the 32 windows' copies of one corner fall on 32 distinct banks.
-constexpr int kHaarPatchWin = 32;
 constexpr int kHaarPatchMax = 1025;  // ints per patch (a window up to 31 x 31)
 constexpr int kHaarPatchRecs = 128;
+template <int kHaarPatchWin>
 __global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer* __restrict__ L,
                                                                  const int* __restrict__ ii1,
                                                                  const HaarStage* __restrict__ stages, int s0, int s1,
@@ -468,10 +468,11 @@ __global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer
   const int pw = ww + 1, ps = ((wh + 1) * pw) | 1;  // patch row length, odd stride
   int* patch = hsm;                                           // [kHaarPatchWin][ps]
   HaarRec* srec = reinterpret_cast<HaarRec*>(hsm + kHaarPatchWin * ps + (kHaarPatchWin * ps & 1));
-  double* part = reinterpret_cast<double*>(srec + kHaarPatchRecs);  // [16][kHaarPatchWin]
-  int* alive_s = reinterpret_cast<int*>(part + 16 * kHaarPatchWin);  // [kHaarPatchWin]
+  constexpr int SPW = 64 / kHaarPatchWin, NS = 8 * SPW;  // stump streams per wave / in all
+  double* part = reinterpret_cast<double*>(srec + kHaarPatchRecs);  // [NS][kHaarPatchWin]
+  int* alive_s = reinterpret_cast<int*>(part + NS * kHaarPatchWin);  // [kHaarPatchWin]
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
-  const int slot = lane & 31, sq = 2 * q + (lane >> 5);
+  const int slot = lane % kHaarPatchWin, sq = q * SPW + lane / kHaarPatchWin;
   const int nw = min(kHaarPatchWin, n - w0);
   // patches: row r of window k's patch is (ww + 1) consecutive ints of its layer's ii row y + r
   const int prow = (wh + 1) * kHaarPatchWin;  // (window, row) pairs
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer
       __syncthreads();
       if (alive) {
 #pragma unroll 4
-        for (int t = sq; t < cn; t += 16) {
+        for (int t = sq; t < cn; t += NS) {
           const HaarRec& f = srec[t];
           float val = haar_feature_shared(pp, pw, 0, 0, f);
           val = __fmul_rn(val, vnf);
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer
     if (tid < kHaarPatchWin && alive_s[tid]) {
       double tot = part[tid];
 #pragma unroll
-      for (int r = 1; r < 16; ++r) tot = __dadd_rn(tot, part[r * kHaarPatchWin + tid]);
+      for (int r = 1; r < NS; ++r) tot = __dadd_rn(tot, part[r * kHaarPatchWin + tid]);
       alive_s[tid] = !(tot < (double)sg.thr);
     }
     if (!__syncthreads_or(tid < kHaarPatchWin && alive_s[tid])) return;  // the workgroup's windows all rejected
@@ -528,10 +529,10 @@ __global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer
   }
 }
 
-size_t haar_patch_lds(int ww, int wh) {
+size_t haar_patch_lds(int kHaarPatchWin, int ww, int wh) {
   const size_t ps = (size_t)(((wh + 1) * (ww + 1)) | 1);
   const size_t ints = kHaarPatchWin * ps + ((kHaarPatchWin * ps) & 1);
-  return ints * 4 + kHaarPatchRecs * sizeof(HaarRec) + 16 * kHaarPatchWin * sizeof(double) + kHaarPatchWin * 4;
+  return ints * 4 + kHaarPatchRecs * sizeof(HaarRec) + 512 * sizeof(double) + kHaarPatchWin * 4;
 }
 
 // ------------------------------------------------------------------ host side
@@ -889,11 +890,14 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
 #else
   constexpr int kHaarSplitFrom = 1, split_waves = 8;
 #endif
-  // groups from kHaarPatchFrom on read box sums from LDS patches (measured: see DESIGN K12)
+  // The LDS-patch form (haar_cascade_patch_kernel) is an experiment of the diagnostic build
+  // (EF_HAAR_PATCH_FROM = first stage, EF_HAAR_PATCH_WIN = 16 | 32 windows per workgroup):
+  // from stage 4 on it measured 2.4x slower than the split form (DESIGN K12).
 #ifdef EF_DIAGNOSTICS
-  static const int kHaarPatchFrom = [] { const char* e = getenv("EF_HAAR_PATCH_FROM"); return e ? atoi(e) : 4; }();
+  static const int kHaarPatchFrom = [] { const char* e = getenv("EF_HAAR_PATCH_FROM"); return e ? atoi(e) : 1 << 30; }();
+  static const int patch_win = [] { const char* e = getenv("EF_HAAR_PATCH_WIN"); return e && atoi(e) == 16 ? 16 : 32; }();
 #else
-  constexpr int kHaarPatchFrom = 4;
+  constexpr int kHaarPatchFrom = 1 << 30, patch_win = 32;
 #endif
   const bool patch_ok = (h->ww + 1) * (h->wh + 1) <= kHaarPatchMax;
   int gi = 0;
@@ -905,15 +909,21 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
     if (live > 0 && h->order_free && patch_ok && s0 >= kHaarPatchFrom) {
       static bool attr_set = false;  // > 64 KiB of dynamic LDS
       if (!attr_set) {
-        EF_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(haar_cascade_patch_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)haar_patch_lds(kHaarPatchMax - 1, 0)),
-               "haar patch kernel attribute");
+        for (const void* k : {reinterpret_cast<const void*>(haar_cascade_patch_kernel<16>),
+                              reinterpret_cast<const void*>(haar_cascade_patch_kernel<32>)})
+          EF_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)haar_patch_lds(32, kHaarPatchMax - 1, 0)),
+                 "haar patch kernel attribute");
         attr_set = true;
       }
-      hipLaunchKernelGGL(haar_cascade_patch_kernel, dim3((unsigned)((live + kHaarPatchWin - 1) / kHaarPatchWin)),
-                         dim3(512), haar_patch_lds(h->ww, h->wh), s, dl, ii1, dst, s0, s1, drc, h->ww, h->wh, bin,
-                         cnt + gi, cap, bout, cnt + gi + 1);
+      const size_t lds = haar_patch_lds(patch_win, h->ww, h->wh);
+      const dim3 g((unsigned)((live + patch_win - 1) / patch_win));
+      if (patch_win == 16)
+        hipLaunchKernelGGL(haar_cascade_patch_kernel<16>, g, dim3(512), lds, s, dl, ii1, dst, s0, s1, drc, h->ww, h->wh,
+                           bin, cnt + gi, cap, bout, cnt + gi + 1);
+      else
+        hipLaunchKernelGGL(haar_cascade_patch_kernel<32>, g, dim3(512), lds, s, dl, ii1, dst, s0, s1, drc, h->ww, h->wh,
+                           bin, cnt + gi, cap, bout, cnt + gi + 1);
     } else if (live > 0 && h->order_free && s0 >= kHaarSplitFrom) {
       const dim3 g((unsigned)((live + 63) / 64));
       if (split_waves == 16)

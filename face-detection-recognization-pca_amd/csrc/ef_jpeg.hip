@@ -1183,38 +1183,104 @@ __global__ __launch_bounds__(256) void jpeg_out_kernel(const JImage* __restrict_
   for (int x0 = 4 * (threadIdx.x & 63); x0 < im.w; x0 += 256) out_quad(im, y, x0, planes, out);
 }
 
-// Ingest: the grey value cvtColor(BGR2GRAY) gives at pixel (y, x) of the decoded image —
-// the luma plane for grey output or a one-component file (B = G = R = Y makes BT.601's
-// weighted sum exactly Y), else out_pixel's upsample + YCC->BGR followed by
-// (1868 B + 9617 G + 4899 R + 2^13) >> 14.
-__device__ __forceinline__ int grey_px(const JImage& im, int y, int x, const uint8_t* planes) {
-  const int Y = planes[im.c[0].plane_off + (int64_t)y * im.c[0].bw * 8 + x];
-  if (im.mode == EF_JPEG_GRAY || im.nc == 1) return Y;
-  const int cb = upsample(planes + im.c[1].plane_off, im.c[1], im.hmax, im.vmax, y, x);
-  const int cr = upsample(planes + im.c[2].plane_off, im.c[2], im.hmax, im.vmax, y, x);
-  const int b = clamp255(Y + cb_b(cb)), g = clamp255(Y + cbcr_g(cb, cr)), r = clamp255(Y + cr_r(cr));
-  return (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14;
+// Source rows output row dy of an (oh x ow) resize of an (h x w) image reads (resize_px's
+// three cases): first and last.
+__device__ __forceinline__ void resize_rows(int h, int w, int oh, int ow, int dy, int& r0, int& r1) {
+  if (oh == h && ow == w) {
+    r0 = r1 = dy;
+  } else if (h == 2 * oh && w == 2 * ow) {
+    r0 = 2 * dy;
+    r1 = 2 * dy + 1;
+  } else {
+    int a, b;
+    lin_axis(dy, h, oh, false, r0, r1, a, b);
+  }
 }
 
-// Ingest: row f of the output (oh x ow grey, ef_preprocess's arithmetic) straight from the
-// decoded planes, without writing the full-size BGR image and reading it back: grid
-// (ceil(oh*ow / 256), files), thread = output pixel; file_img[f] < 0 (a file the decoder
-// does not take) gives a zero row, as the resize of a 1x1 zero image does.
+// Chroma rows of component cp that luma rows [ya, yb] read through upsample().
+__device__ __forceinline__ void chroma_rows(const JComp& cp, int vmax, int ya, int yb, int& ca, int& cb) {
+  if (vmax == 2 * cp.v) {
+    ca = max((ya >> 1) - 1, 0);
+    cb = min((yb >> 1) + 1, cp.dh - 1);
+  } else {
+    ca = ya;
+    cb = yb;
+  }
+}
+
+// Ingest: rows [kResizeBand * blockIdx.x, +kResizeBand) of file blockIdx.y's (oh x ow) grey
+// output (ef_preprocess's arithmetic) straight from the decoded planes, without writing the
+// full-size BGR image and reading it back.  The band's luma rows and the chroma rows their
+// upsampling reads are first copied into LDS with coalesced dword loads (each output pixel
+// otherwise gathers ~36 single bytes: 4 samples x (Y + 2 x 4 chroma)); the samples are then
+// formed from LDS by the same functions (pointers into LDS offset by the first staged row).
+// A band whose rows exceed the LDS budget (very wide sources) reads the planes directly.
+// file_img[f] < 0 (a file the decoder does not take) gives a zero row, as the resize of a
+// 1x1 zero image does.
+constexpr int kResizeBand = 8;
+constexpr int kResizeLds = 40 * 1024;
 __global__ __launch_bounds__(256) void jpeg_resize_kernel(const JImage* __restrict__ imgs, const int* __restrict__ file_img,
                                                          const uint8_t* __restrict__ planes, int oh, int ow,
                                                          uint8_t* __restrict__ dst) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
-  if (o >= oh * ow) return;
-  uint8_t* row = dst + (int64_t)blockIdx.y * oh * ow;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kResizeLds / 4];
+  const int dy0 = blockIdx.x * kResizeBand, dy1 = min(dy0 + kResizeBand, oh);
+  uint8_t* rows = dst + (int64_t)blockIdx.y * oh * ow;
   const int ii = file_img[blockIdx.y];
+  const int nout = (dy1 - dy0) * ow;
   if (ii < 0) {
-    row[o] = 0;
+    for (int o = threadIdx.x; o < nout; o += 256) rows[dy0 * ow + o] = 0;
     return;
   }
   const JImage& im = imgs[ii];
-  const int dy = o / ow, dx = o - dy * ow;
-  const auto gray = [&](int y, int x) { return grey_px(im, y, x, planes); };
-  row[o] = (uint8_t)resize_px(gray, im.h, im.w, oh, ow, dy, dx);
+  const bool colour = !(im.mode == EF_JPEG_GRAY || im.nc == 1);
+  int ya, yb, t;
+  resize_rows(im.h, im.w, oh, ow, dy0, ya, t);
+  resize_rows(im.h, im.w, oh, ow, dy1 - 1, t, yb);
+  const int64_t py = (int64_t)im.c[0].bw * 8;
+  int c1a = 0, c1b = -1, c2a = 0, c2b = -1;
+  int64_t p1 = 0, p2 = 0;
+  if (colour) {
+    chroma_rows(im.c[1], im.vmax, ya, yb, c1a, c1b);
+    chroma_rows(im.c[2], im.vmax, ya, yb, c2a, c2b);
+    p1 = (int64_t)im.c[1].bw * 8;
+    p2 = (int64_t)im.c[2].bw * 8;
+  }
+  const int64_t ny = (yb - ya + 1) * py, n1 = (c1b - c1a + 1) * p1, n2 = (c2b - c2a + 1) * p2;
+  const uint8_t* Yp = planes + im.c[0].plane_off;
+  const uint8_t* Cb = planes + im.c[1].plane_off;
+  const uint8_t* Cr = planes + im.c[2].plane_off;
+  const auto run = [&](const uint8_t* Yq, const uint8_t* Cbq, const uint8_t* Crq) {
+    const auto gray = [&](int y, int x) {
+      const int Y = Yq[(int64_t)y * py + x];
+      if (!colour) return Y;
+      const int cb = upsample(Cbq, im.c[1], im.hmax, im.vmax, y, x);
+      const int cr = upsample(Crq, im.c[2], im.hmax, im.vmax, y, x);
+      const int b = clamp255(Y + cb_b(cb)), g = clamp255(Y + cbcr_g(cb, cr)), r = clamp255(Y + cr_r(cr));
+      return (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14;
+    };
+    for (int o = threadIdx.x; o < nout; o += 256) {
+      const int dy = dy0 + o / ow, dx = o - (o / ow) * ow;
+      rows[dy * ow + dx] = (uint8_t)resize_px(gray, im.h, im.w, oh, ow, dy, dx);
+    }
+  };
+  if (ny + n1 + n2 > kResizeLds) {  // uniform: a band too wide for LDS reads the planes directly
+    run(Yp, Cb, Cr);
+    return;
+  }
+  // stage the band's rows (pitches are multiples of 8, planes 64-byte aligned)
+  const auto stage = [&](const uint8_t* src, int64_t bytes, int64_t at) {
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+    for (int64_t e = threadIdx.x; e < bytes / 4; e += 256) lds[at / 4 + e] = s4[e];
+  };
+  stage(Yp + ya * py, ny, 0);
+  if (colour) {
+    stage(Cb + c1a * p1, n1, ny);
+    stage(Cr + c2a * p2, n2, ny + n1);
+  }
+  __syncthreads();
+  // row r of a plane at (r - its first staged row) * pitch in LDS
+  const uint8_t* l8 = reinterpret_cast<const uint8_t*>(lds);
+  run(l8 - ya * py, l8 + ny - c1a * p1, l8 + ny + n1 - c2a * p2);
 }
 
 // Diagnostic build: wall time of the host stages of a decode (EF_JPEG_TIMES=1 prints them).
@@ -1618,7 +1684,7 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
   if (e == hipSuccess && rz_dst && !B.file_img.empty()) {
     TimerEvt tr;
     timer_begin(c, EF_KERNEL_INGEST, &tr);
-    hipLaunchKernelGGL(jpeg_resize_kernel, dim3((unsigned)(((int64_t)oh * ow + 255) / 256), (unsigned)B.file_img.size()),
+    hipLaunchKernelGGL(jpeg_resize_kernel, dim3((unsigned)((oh + kResizeBand - 1) / kResizeBand), (unsigned)B.file_img.size()),
                        dim3(256), 0, s, X.imgs, reinterpret_cast<const int*>(up + S.o_desc),
                        reinterpret_cast<const uint8_t*>(base + o_planes), oh, ow, rz_dst);
     e = hipGetLastError();

@@ -141,6 +141,7 @@ struct CovPlan {
   int64_t slab_elems = 0;       // splits * dim * dim
   int ntiles = 0, splits = 1, passes = 1;
   int tj = 256;                 // SYRK tile columns (tiles are 256 x tj)
+  int njb = 0;                  // > 0: the 16x16x64 kernel (syrk16_i8_kernel, tj = 64 njb)
 };
 int64_t cov_i8_kpad(int64_t K);
 constexpr int64_t kSyrkPadBytes = 384 * 64;  // readable slack the At allocation carries past its end

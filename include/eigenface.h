@@ -259,10 +259,14 @@ int ef_jpeg_info(const uint8_t* data, const int64_t* offsets, const int64_t* siz
                  int32_t* widths, int32_t* components, int32_t* status);
 int ef_jpeg_decode(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count,
                    int32_t mode, uint8_t* out, const int64_t* out_offsets, int32_t* status, uint32_t flags);
-/* Fused ingest (train-v4.py:59-68 for a batch of files): ef_jpeg_decode into device
- * scratch, then ef_preprocess (grey + INTER_LINEAR resize to out_h x out_w) without a host
- * round trip.  out: count x out_h x out_w uint8 rows (host, or device with EF_MEM_DEVICE);
- * the row of a file with status[i] != 0 is zero and the caller decodes that file itself. */
+/* Fused ingest (train-v4.py:59-68 for a batch of files): decode, then ef_preprocess's
+ * grey + INTER_LINEAR resize to out_h x out_w computed straight from the decoded planes
+ * (the same pixels as ef_jpeg_decode followed by ef_preprocess).  out: count x out_h x out_w
+ * uint8 rows (host, or device with EF_MEM_DEVICE); the row of a file with status[i] != 0 is
+ * zero and the caller decodes that file itself.  status is final on return.  With
+ * EF_MEM_DEVICE the rows are stream-ordered on ctx's stream and the call returns once the
+ * decode is queued (no host wait), so the next call's host-side parse overlaps this
+ * decode; ef_jpeg_decode with EF_MEM_DEVICE behaves the same.  Host outputs return complete. */
 int ef_jpeg_ingest(ef_ctx* ctx, const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int32_t count,
                    int32_t mode, int32_t out_h, int32_t out_w, uint8_t* out, int32_t* status, uint32_t flags);
 

@@ -177,3 +177,20 @@ def test_back_to_back_device_ingests(eng):
     for i in range(0, len(batches[1]), 101):
         np.testing.assert_array_equal(outs[1][i].cpu().numpy(),
                                       io_oracle.preprocess(J.decode_ref(batches[1][i], "bgr"), (32, 32)))
+
+
+def test_ingest_wide_sources_read_planes_directly(eng):
+    """Sources whose band of rows exceeds the fused resize's LDS budget (large frames) take its
+    direct-read path; small ones in the same call the LDS-staged path — both equal libjpeg's
+    pixels through the resize oracle, for 4:2:0, 4:2:2, 4:4:4 and grey files."""
+    blobs = [J.encode(J.smooth_image(1200, 1500, 3, 31), quality=85, subsampling=0),
+             J.encode(J.smooth_image(900, 1700, 3, 32), quality=75, subsampling=1),
+             J.encode(J.smooth_image(1100, 640, 3, 33), quality=90, subsampling=2),
+             J.encode(J.smooth_image(700, 1300, 1, 34), quality=80),
+             J.encode(J.smooth_image(130, 170, 3, 35), quality=95, subsampling=2)]
+    for mode in ("bgr", "gray"):
+        rows, st = eng.ingest_jpegs(blobs, (64, 64), mode)
+        assert (st == 0).all()
+        for i, b in enumerate(blobs):
+            np.testing.assert_array_equal(rows[i], io_oracle.preprocess(J.decode_ref(b, mode), (64, 64)),
+                                          err_msg=f"{mode} file {i}")
