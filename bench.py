@@ -346,7 +346,8 @@ def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
     nbytes = sum(len(b) for b in blobs)
     dev = torch.device("cuda", torch.cuda.current_device())
     out = torch.empty((n, 4096), dtype=torch.uint8, device=dev)
-    eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
+    for _ in range(2):  # both upload slots allocated before the clock starts
+        eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
     torch.cuda.synchronize(dev)
     eng.timing_reset()
     t = time.perf_counter()

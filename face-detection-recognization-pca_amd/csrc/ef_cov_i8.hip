@@ -389,17 +389,22 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
     }
 }
 
+#ifdef EF_DIAGNOSTICS
+// Diagnostic-build experiment (EF_SYRK16 = 5 | 6), not used by the product library: the int8
+// 16x16x64 MFMA holds a higher clock than 32x32x32 under load (tools/micro/bf16_clock i:
+// 2.06 vs 1.78 GHz with LDS-fed operands, profiles/r03/i8_clock.json), but this kernel
+// measured no faster in the C3 fit (NJB = 6: 0.165 vs 0.163-0.168 s; NJB = 5: 0.176 s;
+// identical results) — the SYRK stays on the L2 -> LDS stream's limit.
 // The same item on v_mfma_i32_16x16x64_i8 (one 64-sample k-step per stage): wave (wm, wn)
 // owns 128 rows x 16 NJB columns as 8 x NJB 16 x 16 blocks (4 accumulator VGPRs each).
 // Lane l supplies row l & 15 of a block and samples 16 (l >> 4) .. +15 (the K order inside a
 // fragment is the same for A and B — both are At rows — so it cancels in the dot product).
 // The stage's 64-B rows hold their 16-B chunks at chunk ^ f((row >> 2) & 3), f = {0, 2, 3, 1}:
 // each ds_read_b128 lane group ({0-3,12-15,20-27}, … MI355X_MICROARCH §LDS) then covers all 16
-// bank quads.  Order per stage: column block by column block over the 8 row blocks; every
-// fragment of stage st is in registers before its first MFMA, the barrier (stage st+1
-// visible, slot st retired) sits after column 0, and each fragment is refilled with stage
-// st+1's as soon as its last MFMA of stage st is issued (b[j] after column j, a[i] during the
-// last column).
+// bank quads.  Order per stage: column block by column block over the 8 row blocks, the
+// next column's B fragment read while a column's MFMAs run; the barrier (stage st+1
+// visible, slot st retired) sits before the last column, during which the A fragments are
+// refilled with stage st+1's.
 __device__ __forceinline__ int syrk16_swz(int b) { return (0x78 >> (2 * b)) & 3; }
 
 template <int NJB, int NB>
@@ -459,34 +464,38 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
     for (int j = 0; j < NB; ++j) issue(sb + (j < nst ? j : 0), j);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 1)) : "memory");  // stage 0 landed
     __syncthreads();
-    i32x4 a[8], b[NJB];
+    // registers: the stage's 8 A fragments, and a two-entry ring of B fragments (the column
+    // being multiplied and the next one) — 40 VGPRs next to the 32 NJB accumulators
+    i32x4 a[8], bq, bn;
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = fa(smem, i);
-#pragma unroll
-    for (int j = 0; j < NJB; ++j) b[j] = fb(smem, j);
+    bq = fb(smem, 0);
     for (int64_t st = 0; st < nst; ++st) {
+      const uint8_t* cur = smem + (st % NB) * STG;
       const uint8_t* nxt = smem + ((st + 1) % NB) * STG;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[0], acc[i][0], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 2)) : "memory");  // stage st+1 landed
-      __syncthreads();  // every wave's stage-st fragments are in registers; stage st+1 visible
+      for (int j = 0; j < NJB - 1; ++j) {
+        bn = fb(cur, j + 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][j], 0, 0, 0);
+        bq = bn;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // every read of stage st is issued (the barrier waits for them); stage st+1 landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 2)) : "memory");
+      __syncthreads();
       {
         const int64_t nx = st + NB;
         issue(sb + (nx < nst ? nx : 0), (int)(nx % NB));  // into stage st's slot
       }
-      b[0] = fb(nxt, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      bn = fb(nxt, 0);
 #pragma unroll
-      for (int j = 1; j < NJB; ++j) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-          if (j == NJB - 1) a[i] = fa(nxt, i);
-        }
-        b[j] = fb(nxt, j);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 8; ++i) {
+        acc[i][NJB - 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][NJB - 1], 0, 0, 0);
+        a[i] = fa(nxt, i);
       }
+      bq = bn;
+      __builtin_amdgcn_sched_barrier(0);
     }
     dma_wait_all();
   }
@@ -503,6 +512,7 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
       }
     }
 }
+#endif  // EF_DIAGNOSTICS
 
 // ---------------------------------------------------------------- exact finishing
 // R[r] = sum_k At[.][r][k] * c[k]   (Gram path; exact in int64)
@@ -724,13 +734,16 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
   for (int pass = 0; pass < p.passes; ++pass) {
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
+#ifdef EF_DIAGNOSTICS
     if (p.njb == 6)
       hipLaunchKernelGGL((syrk16_i8_kernel<6, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
     else if (p.njb == 5)
       hipLaunchKernelGGL((syrk16_i8_kernel<5, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
-    else if (p.tj == 384)
+    else
+#endif
+    if (p.tj == 384)
       hipLaunchKernelGGL((syrk_i8_kernel<384, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
     else

@@ -441,100 +441,6 @@ __global__ __launch_bounds__(NQ * 64) void haar_cascade_split_kernel(const HaarL
   }
 }
 
-// Pass 3, patch form (the late stage groups): the windows reaching them are sparse, so the
-// split form's gathers — lane = window, each stump's corners a separate cache line per
-// lane — keep the texture path busy (TA ~60 %) while the MFMA-free ALUs idle.  Here a
-// workgroup copies the integral-image patch of each of its kHaarPatchWin windows
-// ((wh+1) x (ww+1) ints, ~2.5 KiB for a 24 x 24 window) into LDS once, with coalesced
-// row loads, and every stump's box sums are read from there.  Layout as the split form:
-// lane = window (lanes 32..63 repeat the windows with the other half of the stumps), wave q
-// half h takes stumps 2q+h, 2q+h+16, … of each stage from LDS records; the 16 partial sums
-// of a window are added in LDS (order-free cascades only, as the split form).  The patch
-// stride is odd, so the 32 windows' copies of one corner fall on 32 distinct banks.
-constexpr int kHaarPatchMax = 1025;  // ints per patch (a window up to 31 x 31)
-constexpr int kHaarPatchRecs = 128;
-template <int kHaarPatchWin>
-__global__ __launch_bounds__(512) void haar_cascade_patch_kernel(const HaarLayer* __restrict__ L,
-                                                                 const int* __restrict__ ii1,
-                                                                 const HaarStage* __restrict__ stages, int s0, int s1,
-                                                                 const HaarRec* __restrict__ recs, int ww, int wh,
-                                                                 const HaarCand* __restrict__ in,
-                                                                 const int* __restrict__ nin, int cap,
-                                                                 HaarCand* __restrict__ out, int* __restrict__ nout) {
-  extern __shared__ __attribute__((aligned(16))) int hsm[];
-  const int n = min(*nin, cap);
-  const int w0 = blockIdx.x * kHaarPatchWin;
-  if (w0 >= n) return;  // uniform over the workgroup
-  const int pw = ww + 1, ps = ((wh + 1) * pw) | 1;  // patch row length, odd stride
-  int* patch = hsm;                                           // [kHaarPatchWin][ps]
-  HaarRec* srec = reinterpret_cast<HaarRec*>(hsm + kHaarPatchWin * ps + (kHaarPatchWin * ps & 1));
-  constexpr int SPW = 64 / kHaarPatchWin, NS = 8 * SPW;  // stump streams per wave / in all
-  double* part = reinterpret_cast<double*>(srec + kHaarPatchRecs);  // [NS][kHaarPatchWin]
-  int* alive_s = reinterpret_cast<int*>(part + NS * kHaarPatchWin);  // [kHaarPatchWin]
-  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
-  const int slot = lane % kHaarPatchWin, sq = q * SPW + lane / kHaarPatchWin;
-  const int nw = min(kHaarPatchWin, n - w0);
-  // patches: row r of window k's patch is (ww + 1) consecutive ints of its layer's ii row y + r
-  const int prow = (wh + 1) * kHaarPatchWin;  // (window, row) pairs
-  for (int e = tid >> 5; e < prow; e += 16) {  // 32 lanes per row piece
-    const int k = e / (wh + 1), r = e - k * (wh + 1);
-    if (k >= nw) continue;
-    const HaarCand wc = in[w0 + k];
-    const HaarLayer ly = L[wc.layer];
-    const int* src = ii1 + ly.ii_off + (int64_t)(wc.y + r) * (ly.w + 1) + wc.x;
-    for (int c = tid & 31; c < pw; c += 32) patch[k * ps + r * pw + c] = src[c];
-  }
-  const bool valid = slot < nw;
-  const HaarCand w = in[w0 + (valid ? slot : 0)];
-  const float vnf = w.vnf;
-  if (tid < kHaarPatchWin) alive_s[tid] = tid < nw;
-  const int* pp = patch + slot * ps;
-  __syncthreads();
-  for (int st = s0; st < s1; ++st) {
-    const HaarStage sg = stages[st];
-    const bool alive = alive_s[slot] != 0;
-    double tmp = 0.0;
-    for (int c0 = 0; c0 < sg.count; c0 += kHaarPatchRecs) {
-      const int cn = min(kHaarPatchRecs, sg.count - c0);
-      {
-        const int* src = reinterpret_cast<const int*>(recs + sg.first + c0);
-        int* dst = reinterpret_cast<int*>(srec);
-        for (int e = tid; e < cn * (int)(sizeof(HaarRec) / 4); e += 512) dst[e] = src[e];
-      }
-      __syncthreads();
-      if (alive) {
-#pragma unroll 4
-        for (int t = sq; t < cn; t += NS) {
-          const HaarRec& f = srec[t];
-          float val = haar_feature_shared(pp, pw, 0, 0, f);
-          val = __fmul_rn(val, vnf);
-          tmp = __dadd_rn(tmp, (double)(val < f.thr ? f.left : f.right));
-        }
-      }
-      __syncthreads();
-    }
-    part[sq * kHaarPatchWin + slot] = tmp;
-    __syncthreads();
-    if (tid < kHaarPatchWin && alive_s[tid]) {
-      double tot = part[tid];
-#pragma unroll
-      for (int r = 1; r < NS; ++r) tot = __dadd_rn(tot, part[r * kHaarPatchWin + tid]);
-      alive_s[tid] = !(tot < (double)sg.thr);
-    }
-    if (!__syncthreads_or(tid < kHaarPatchWin && alive_s[tid])) return;  // the workgroup's windows all rejected
-  }
-  if (tid < kHaarPatchWin && alive_s[tid]) {
-    const int k = atomicAdd(nout, 1);
-    if (k < cap) out[k] = in[w0 + tid];
-  }
-}
-
-size_t haar_patch_lds(int kHaarPatchWin, int ww, int wh) {
-  const size_t ps = (size_t)(((wh + 1) * (ww + 1)) | 1);
-  const size_t ints = kHaarPatchWin * ps + ((kHaarPatchWin * ps) & 1);
-  return ints * 4 + kHaarPatchRecs * sizeof(HaarRec) + 512 * sizeof(double) + kHaarPatchWin * 4;
-}
-
 // ------------------------------------------------------------------ host side
 struct HaarState {
   int ww = 0, wh = 0, nstages = 0;
@@ -890,41 +796,13 @@ int ef_haar_detect(ef_ctx* c, const uint8_t* gray, int32_t H, int32_t W, int64_t
 #else
   constexpr int kHaarSplitFrom = 1, split_waves = 8;
 #endif
-  // The LDS-patch form (haar_cascade_patch_kernel) is an experiment of the diagnostic build
-  // (EF_HAAR_PATCH_FROM = first stage, EF_HAAR_PATCH_WIN = 16 | 32 windows per workgroup):
-  // from stage 4 on it measured 2.4x slower than the split form (DESIGN K12).
-#ifdef EF_DIAGNOSTICS
-  static const int kHaarPatchFrom = [] { const char* e = getenv("EF_HAAR_PATCH_FROM"); return e ? atoi(e) : 1 << 30; }();
-  static const int patch_win = [] { const char* e = getenv("EF_HAAR_PATCH_WIN"); return e && atoi(e) == 16 ? 16 : 32; }();
-#else
-  constexpr int kHaarPatchFrom = 1 << 30, patch_win = 32;
-#endif
-  const bool patch_ok = (h->ww + 1) * (h->wh + 1) <= kHaarPatchMax;
   int gi = 0;
   const int live = hc[0];  // upper bound of every group's input
   HaarCand* bin = work;
   HaarCand* bout = cand;
   for (; groups[gi] < h->nstages; ++gi) {
     const int s0 = groups[gi], s1 = std::min(groups[gi + 1], h->nstages);
-    if (live > 0 && h->order_free && patch_ok && s0 >= kHaarPatchFrom) {
-      static bool attr_set = false;  // > 64 KiB of dynamic LDS
-      if (!attr_set) {
-        for (const void* k : {reinterpret_cast<const void*>(haar_cascade_patch_kernel<16>),
-                              reinterpret_cast<const void*>(haar_cascade_patch_kernel<32>)})
-          EF_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)haar_patch_lds(32, kHaarPatchMax - 1, 0)),
-                 "haar patch kernel attribute");
-        attr_set = true;
-      }
-      const size_t lds = haar_patch_lds(patch_win, h->ww, h->wh);
-      const dim3 g((unsigned)((live + patch_win - 1) / patch_win));
-      if (patch_win == 16)
-        hipLaunchKernelGGL(haar_cascade_patch_kernel<16>, g, dim3(512), lds, s, dl, ii1, dst, s0, s1, drc, h->ww, h->wh,
-                           bin, cnt + gi, cap, bout, cnt + gi + 1);
-      else
-        hipLaunchKernelGGL(haar_cascade_patch_kernel<32>, g, dim3(512), lds, s, dl, ii1, dst, s0, s1, drc, h->ww, h->wh,
-                           bin, cnt + gi, cap, bout, cnt + gi + 1);
-    } else if (live > 0 && h->order_free && s0 >= kHaarSplitFrom) {
+    if (live > 0 && h->order_free && s0 >= kHaarSplitFrom) {
       const dim3 g((unsigned)((live + 63) / 64));
       if (split_waves == 16)
         hipLaunchKernelGGL(haar_cascade_split_kernel<16>, g, dim3(1024), 0, s, dl, ii1, ii2, dst, s0, s1, drc, h->ww,
