@@ -400,32 +400,66 @@ __constant__ unsigned char kNatural[80] = EF_NATURAL_ORDER;
 const unsigned char kNaturalHost[80] = EF_NATURAL_ORDER;
 #endif
 
-// Destuffed big-endian bit string of one segment, read through aligned 32-bit words into a
-// 64-bit window; past the end it yields zeros, as libjpeg feeds zeros after a marker.
+// Destuffed big-endian bit string of one segment, read through 32-bit words into a 64-bit
+// window; past the end it yields zeros, as libjpeg feeds zeros after a marker.  The words
+// come from a queue refilled by one aligned 16-byte load per four words, issued a whole
+// block ahead: the chunk loops are latency-bound (one dependent table lookup per symbol),
+// and a word loaded only one refill ahead arrived too late (each lane streams its own chunk,
+// so the loads do not coalesce).  The words array is 16-byte aligned and carries at least
+// 32 bytes of readable slack past its last word (the block reads never fault; words past a
+// segment's end read as zero).
 struct BitStream {
   const unsigned* w;
   int nw;
-  int widx;   // index of the word after nextw
   int pos;    // bit offset of the next unread bit
   int bits;   // valid bits in buf
-  unsigned nextw;  // the word the next refill appends, loaded one refill ahead
   unsigned long long buf;
+  unsigned q0, q1, q2, q3;  // the next words to append, q0 first (`left` of them valid)
+  unsigned n0, n1, n2, n3;  // the aligned block after them (loaded ahead)
+  int left;
+  int wi;                   // segment word index of q0
+  const unsigned* nb;       // the next aligned block to load
   __host__ __device__ unsigned word(int i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+  __host__ __device__ __forceinline__ void fetch() {
+    n0 = nb[0];
+    n1 = nb[1];
+    n2 = nb[2];
+    n3 = nb[3];
+    nb += 4;
+  }
   __host__ __device__ __forceinline__ void init(const unsigned* words, int nwords, int p) {
     w = words;
     nw = nwords;
     const int i = p >> 5, s = p & 31;
     buf = (unsigned long long)(word(i) << s) << 32;
     bits = 32 - s;
-    nextw = word(i + 1);
-    widx = i + 2;
     pos = p;
+    // queue from word i + 1: its aligned block, the words before it shifted out
+    const unsigned* a = w + i + 1;
+    const int off = (int)(((size_t)a >> 2) & 3);
+    nb = a - off;
+    fetch();
+    q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+    for (int t = 0; t < off; ++t) q0 = q1, q1 = q2, q2 = q3;
+    left = 4 - off;
+    wi = i + 1;
+    fetch();
+  }
+  __host__ __device__ __forceinline__ unsigned take() {
+    const unsigned v = wi < nw ? __builtin_bswap32(q0) : 0u;
+    ++wi;
+    q0 = q1, q1 = q2, q2 = q3;
+    if (--left == 0) {
+      q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+      left = 4;
+      fetch();
+    }
+    return v;
   }
   __host__ __device__ void refill() {  // afterwards at least 32 bits are buffered
     if (bits <= 32) {
-      buf |= (unsigned long long)nextw << (32 - bits);
+      buf |= (unsigned long long)take() << (32 - bits);
       bits += 32;
-      nextw = word(widx++);
     }
   }
   __host__ __device__ unsigned peek(int n) const { return (unsigned)(buf >> (64 - n)); }
@@ -1498,7 +1532,7 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t off = 0;
   S.slot = slot;
-  S.o_words = off; off += al((size_t)B.words * 4 + 16);
+  S.o_words = off; off += al((size_t)B.words * 4 + 32);  // BitStream reads up to 8 words past a segment
   S.o_imgs = off; off += al(B.imgs.size() * sizeof(JImage));
   S.o_pool = off; off += al(std::max<size_t>(B.T.huff.size(), 1) * sizeof(HuffTab));
   S.o_q = off; off += al(std::max<size_t>(B.T.quant.size(), 1) * 2);
@@ -1873,7 +1907,7 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
                                         int32_t* status, int32_t chunk_bits, int32_t* rounds_out) {
   Batch B;
   build_batch(data, offsets, sizes, count, mode, out_offsets, status, B);
-  std::vector<unsigned> words((size_t)B.words + 4, 0);
+  std::vector<unsigned> words((size_t)B.words + 16, 0);  // BitStream's block reads run ahead
   destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(words.data()));
   make_chunks(B, chunk_bits);
   const int nch = (int)B.chunk_seg.size();
