@@ -624,23 +624,24 @@ __host__ __device__ __forceinline__ long long chunk_sync(const McuInfo& M, const
       next_cp = ++m <= kCheckpoints ? start + m * cp_bits : 0x7FFFFFFF;
     }
     bs.refill();
-    if (k == 0) {
-      const int s = bs.decode(*T.tdc, T.ldc);
-      const int diff = s ? huff_extend(bs.get(s), s) : 0;
+    // one symbol decode for DC and AC alike (the table is selected, not the code path): the
+    // lanes of a wave sit at DC and AC symbols at once, and two decode paths would serialise
+    // two table lookups per step
+    const bool dc = k == 0;
+    const int sym = bs.decode(dc ? *T.tdc : *T.tac, dc ? T.ldc : T.lac);
+    const int s = dc ? sym : (sym & 15), r = dc ? 0 : (sym >> 4);
+    const int bitsv = s ? bs.get(s) : 0;
+    if (dc) {
+      const int diff = s ? huff_extend(bitsv, s) : 0;
       dc0 += T.comp == 0 ? diff : 0;
       dc1 += T.comp == 1 ? diff : 0;
       dc2 += T.comp == 2 ? diff : 0;
       ++nblk;
       k = 1;
+    } else if (s) {
+      k += r + 1;
     } else {
-      const int rs = bs.decode(*T.tac, T.lac);
-      const int s = rs & 15, r = rs >> 4;
-      if (s) {
-        bs.skip(s);
-        k += r + 1;
-      } else {
-        k = r == 15 ? k + 16 : 64;
-      }
+      k = r == 15 ? k + 16 : 64;
     }
     if (k >= 64) {
       k = 0;
@@ -685,28 +686,29 @@ __host__ __device__ __forceinline__ void chunk_write(const McuInfo& M, int mcu0,
   while (bs.pos < end_bit) {
     if (k == 0 && g >= total) break;
     bs.refill();
-    if (k == 0) {
+    // one symbol decode and one store path for DC and AC alike (see chunk_sync)
+    const bool dc = k == 0;
+    if (dc) {
       blk = M.block(bi, my, mx, coef);
       ++g;
-      const int s = bs.decode(*T.tdc, T.ldc);
-      const int diff = s ? huff_extend(bs.get(s), s) : 0;
-      int p;
-      if (T.comp == 0) p = pred[0] += diff;
-      else if (T.comp == 1) p = pred[1] += diff;
-      else p = pred[2] += diff;
-      blk[0] = (short)p;
-      k = 1;
-    } else {
-      const int rs = bs.decode(*T.tac, T.lac);
-      const int s = rs & 15, r = rs >> 4;
-      if (s) {
-        k += r;
-        blk[nat[k]] = (short)huff_extend(bs.get(s), s);
-        ++k;
-      } else {
-        k = r == 15 ? k + 16 : 64;
-      }
     }
+    const int sym = bs.decode(dc ? *T.tdc : *T.tac, dc ? T.ldc : T.lac);
+    const int s = dc ? sym : (sym & 15), r = dc ? 0 : (sym >> 4);
+    const int val = s ? huff_extend(bs.get(s), s) : 0;
+    int v = val, pos = 0;
+    if (dc) {
+      if (T.comp == 0) v = pred[0] += val;
+      else if (T.comp == 1) v = pred[1] += val;
+      else v = pred[2] += val;
+      k = 1;
+    } else if (s) {
+      k += r;
+      pos = nat[k];
+      ++k;
+    } else {
+      k = r == 15 ? k + 16 : 64;
+    }
+    if (dc || s) blk[pos] = (short)v;
     if (k >= 64) {
       k = 0;
       if (++b == M.bpm) {
@@ -803,12 +805,16 @@ constexpr int kDeviceRounds = 8;  // synchronisation rounds queued without a hos
 constexpr int kGlobalLutStride = (int)(sizeof(HuffTab) / 2);
 
 // The batch's lookahead tables in LDS when there are at most kLdsTables of them (the usual
-// case: one encoder's 4 tables), else read from the global pool.
-__device__ __forceinline__ const unsigned short* stage_luts(const ChunkCtx& X, int lds_tables, unsigned short* slut,
-                                                            int* lstride) {
+// case: one encoder's 4 tables), else read from the global pool.  The chunk loops are
+// instantiated once per case (`with_luts`), so the LDS case's table pointer is known to
+// point into LDS and every lookup is a ds_read: a pointer that may point to either memory is
+// a flat access, whose wait also drains every outstanding global load and store — the bit
+// stream's prefetch and the coefficient stores — at each symbol.
+template <class F>
+__device__ __forceinline__ void with_luts(const ChunkCtx& X, int lds_tables, unsigned short* slut, const F& f) {
   if (lds_tables == 0) {
-    *lstride = kGlobalLutStride;
-    return X.pool[0].look;
+    f(X.pool[0].look, kGlobalLutStride);
+    return;
   }
   constexpr int kVec = kLookSize * 2 / 16;  // 16-byte pieces per table
   for (int t = threadIdx.x; t < lds_tables * kVec; t += blockDim.x) {
@@ -816,8 +822,7 @@ __device__ __forceinline__ const unsigned short* stage_luts(const ChunkCtx& X, i
     reinterpret_cast<uint4*>(slut + tb * kLookSize)[v] = reinterpret_cast<const uint4*>(X.pool[tb].look)[v];
   }
   __syncthreads();
-  *lstride = kLookSize;
-  return slut;
+  f(static_cast<const unsigned short*>(slut), kLookSize);
 }
 
 // prev_changed (rounds >= 2 of the device-side sequence): the previous round's change flag;
@@ -831,10 +836,10 @@ __global__ __launch_bounds__(kChunkThreads) void jpeg_sync_kernel(ChunkCtx X, in
                                                                   const int* __restrict__ prev_changed) {
   if (prev_changed && *prev_changed == 0) return;  // uniform: converged before this round
   extern __shared__ unsigned short slut[];
-  int lstride;
-  const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < X.nchunks) sync_chunk(X, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
+  with_luts(X, lds_tables, slut, [&](const unsigned short* luts, int lstride) {
+    if (i < X.nchunks) sync_chunk(X, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
+  });
 }
 
 // Completion of one segment after r synchronisation rounds, sequentially along its chunks.
@@ -923,10 +928,11 @@ __global__ __launch_bounds__(kChunkThreads) void jpeg_write_kernel(ChunkCtx X, i
   extern __shared__ unsigned short slut[];
   unsigned char* snat = reinterpret_cast<unsigned char*>(slut + lds_tables * kLookSize);
   if (threadIdx.x < 80) snat[threadIdx.x] = kNatural[threadIdx.x];
-  int lstride;
-  const unsigned short* luts = stage_luts(X, lds_tables, slut, &lstride);  // ends with a barrier
+  if (lds_tables == 0) __syncthreads();  // (with_luts' staging ends with one otherwise)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat);
+  with_luts(X, lds_tables, slut, [&](const unsigned short* luts, int lstride) {
+    if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat);
+  });
 }
 
 // jidctint.c jpeg_idct_islow arithmetic
