@@ -785,7 +785,9 @@ __host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const uns
       // codeword boundary is often already exact
       chunk_stream(X, sg, start - X.warm_bits, bs);
       int dummy[4];
-      s = chunk_sync(M, X.pool, luts, lstride, bs, 0, 0, start, dummy);
+      // (cps passed although no checkpoint is taken here: a null pointer merged with the
+      // global one would make the checkpoint stores flat)
+      s = chunk_sync(M, X.pool, luts, lstride, bs, 0, 0, start, dummy, 0, 0, cps);
       S[i] = s;
     } else {
       chunk_stream(X, sg, st_pos(s), bs);
