@@ -748,7 +748,8 @@ __host__ __device__ __forceinline__ void chunk_stream(const ChunkCtx& X, const J
 // from the one it started from, re-decodes and raises *changed.  At the fixed point every
 // start state is exact by induction from the segment start.  Last chunks of a segment only
 // record their start state (nothing follows them).
-__host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const unsigned short* luts, int lstride, int i, int round,
+__host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const HuffTab* pool, const unsigned short* luts,
+                                                    int lstride, int i, int round,
                                     long long* S, const long long* Ein, long long* Eout, int* cnt, int* changed) {
   const JSeg& sg = X.segs[X.chunk_seg[i]];
   const int j = i - sg.chunk0;
@@ -787,16 +788,16 @@ __host__ __device__ __forceinline__ void sync_chunk(const ChunkCtx& X, const uns
       int dummy[4];
       // (cps passed although no checkpoint is taken here: a null pointer merged with the
       // global one would make the checkpoint stores flat)
-      s = chunk_sync(M, X.pool, luts, lstride, bs, 0, 0, start, dummy, 0, 0, cps);
+      s = chunk_sync(M, pool, luts, lstride, bs, 0, 0, start, dummy, 0, 0, cps);
       S[i] = s;
     } else {
       chunk_stream(X, sg, st_pos(s), bs);
     }
-    Eout[i] = chunk_sync(M, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits, cps);
+    Eout[i] = chunk_sync(M, pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits, cps);
     return;
   }
   chunk_stream(X, sg, st_pos(s), bs);
-  const long long e = chunk_sync(M, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits,
+  const long long e = chunk_sync(M, pool, luts, lstride, bs, st_b(s), st_k(s), end, cnt + 4 * i, start, cp_bits,
                                  cps, true, Ein[i]);
   Eout[i] = e;
   if (e != Ein[i]) *changed = 1;  // only a changed exit can change the next chunk
@@ -806,25 +807,28 @@ constexpr int kChunkThreads = 256;
 constexpr int kDeviceRounds = 8;  // synchronisation rounds queued without a host round trip
 constexpr int kGlobalLutStride = (int)(sizeof(HuffTab) / 2);
 
-// The batch's lookahead tables in LDS when there are at most kLdsTables of them (the usual
-// case: one encoder's 4 tables), else read from the global pool.  The chunk loops are
-// instantiated once per case (`with_luts`), so the LDS case's table pointer is known to
-// point into LDS and every lookup is a ds_read: a pointer that may point to either memory is
-// a flat access, whose wait also drains every outstanding global load and store — the bit
-// stream's prefetch and the coefficient stores — at each symbol.
+// The batch's Huffman tables (lookahead table, maxcode / valoffset / huffval for codes longer
+// than the lookahead) copied whole into LDS when there are at most kLdsTables of them (the
+// usual case: one encoder's 4 tables), else read from the global pool.  The chunk loops are
+// instantiated once per case, so the LDS case's table pointer is known to point into LDS
+// and every lookup is a ds_read: a pointer that may point to either memory is a flat access,
+// whose wait also drains every outstanding global load and store — the bit stream's prefetch
+// and the coefficient stores — at each symbol.  The long-code tables must be in LDS too:
+// codes over 12 bits are rare, but a 64-lane wave meets one in most steps, and their
+// dependent maxcode reads from global memory then stall the whole wave.
+constexpr int kTabBytes = (int)sizeof(HuffTab);
 template <class F>
-__device__ __forceinline__ void with_luts(const ChunkCtx& X, int lds_tables, unsigned short* slut, const F& f) {
+__device__ __forceinline__ void with_luts(const ChunkCtx& X, int lds_tables, unsigned short* smem, const F& f) {
   if (lds_tables == 0) {
-    f(X.pool[0].look, kGlobalLutStride);
+    f(X.pool, X.pool[0].look, kGlobalLutStride);
     return;
   }
-  constexpr int kVec = kLookSize * 2 / 16;  // 16-byte pieces per table
-  for (int t = threadIdx.x; t < lds_tables * kVec; t += blockDim.x) {
-    const int tb = t / kVec, v = t - tb * kVec;
-    reinterpret_cast<uint4*>(slut + tb * kLookSize)[v] = reinterpret_cast<const uint4*>(X.pool[tb].look)[v];
-  }
+  const int nvec = lds_tables * (kTabBytes / 16);
+  for (int t = threadIdx.x; t < nvec; t += blockDim.x)
+    reinterpret_cast<uint4*>(smem)[t] = reinterpret_cast<const uint4*>(X.pool)[t];
   __syncthreads();
-  f(static_cast<const unsigned short*>(slut), kLookSize);
+  const HuffTab* lp = reinterpret_cast<const HuffTab*>(smem);
+  f(lp, lp[0].look, kGlobalLutStride);
 }
 
 // prev_changed (rounds >= 2 of the device-side sequence): the previous round's change flag;
@@ -839,8 +843,8 @@ __global__ __launch_bounds__(kChunkThreads) void jpeg_sync_kernel(ChunkCtx X, in
   if (prev_changed && *prev_changed == 0) return;  // uniform: converged before this round
   extern __shared__ unsigned short slut[];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  with_luts(X, lds_tables, slut, [&](const unsigned short* luts, int lstride) {
-    if (i < X.nchunks) sync_chunk(X, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
+  with_luts(X, lds_tables, slut, [&](const HuffTab* pool, const unsigned short* luts, int lstride) {
+    if (i < X.nchunks) sync_chunk(X, pool, luts, lstride, i, round, S, Ein, Eout, cnt, changed);
   });
 }
 
@@ -907,7 +911,8 @@ __global__ __launch_bounds__(64) void jpeg_scan_kernel(ChunkCtx X, int nseg, con
   if (si < nseg) scan_segment(X, X.segs[si], cnt, G, P);
 }
 
-__host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const unsigned short* luts, int lstride, int i,
+__host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const HuffTab* pool, const unsigned short* luts,
+                                                     int lstride, int i,
                                                      const long long* S, const int* G, const int* P, short* coef,
                                                      const unsigned char* nat) {
   const JSeg& sg = X.segs[X.chunk_seg[i]];
@@ -919,21 +924,21 @@ __host__ __device__ __forceinline__ void write_chunk(const ChunkCtx& X, const un
   const int end = j == sg.nchunk - 1 ? 0x7FFFFFFF : (j + 1) * X.chunk_bits;
   McuInfo M;
   M.load(X.imgs[sg.img]);
-  chunk_write(M, sg.mcu0, X.pool, luts, lstride, bs, st_b(s), st_k(s), end, G[i], sg.nmcu * M.bpm, pred, coef, nat);
+  chunk_write(M, sg.mcu0, pool, luts, lstride, bs, st_b(s), st_k(s), end, G[i], sg.nmcu * M.bpm, pred, coef, nat);
 }
 
-// LDS: [lookahead tables | natural order]
+// LDS: [Huffman tables | natural order]
 __global__ __launch_bounds__(kChunkThreads) void jpeg_write_kernel(ChunkCtx X, int lds_tables,
                                                                    const long long* __restrict__ S,
                                                                    const int* __restrict__ G, const int* __restrict__ P,
                                                                    short* __restrict__ coef) {
   extern __shared__ unsigned short slut[];
-  unsigned char* snat = reinterpret_cast<unsigned char*>(slut + lds_tables * kLookSize);
+  unsigned char* snat = reinterpret_cast<unsigned char*>(slut) + lds_tables * kTabBytes;
   if (threadIdx.x < 80) snat[threadIdx.x] = kNatural[threadIdx.x];
   if (lds_tables == 0) __syncthreads();  // (with_luts' staging ends with one otherwise)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  with_luts(X, lds_tables, slut, [&](const unsigned short* luts, int lstride) {
-    if (i < X.nchunks) write_chunk(X, luts, lstride, i, S, G, P, coef, snat);
+  with_luts(X, lds_tables, slut, [&](const HuffTab* pool, const unsigned short* luts, int lstride) {
+    if (i < X.nchunks) write_chunk(X, pool, luts, lstride, i, S, G, P, coef, snat);
   });
 }
 
@@ -1678,7 +1683,17 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
   for (const JSeg& sg : B.segs) max_chunks = std::max(max_chunks, sg.nchunk);
   const unsigned cgrid = (unsigned)((nchunks + kChunkThreads - 1) / kChunkThreads);
   const int lds_tables = B.T.huff.size() <= (size_t)kLdsTables ? (int)B.T.huff.size() : 0;
-  const size_t lds_bytes = (size_t)lds_tables * kLookSize * 2;
+  const size_t lds_bytes = (size_t)lds_tables * kTabBytes;
+  static bool lds_attr = false;  // up to kLdsTables whole tables: > 64 KiB of dynamic LDS
+  if (!lds_attr && e == hipSuccess) {
+    const int most = kLdsTables * kTabBytes + 128;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_sync_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            most);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_write_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, most);
+    lds_attr = e == hipSuccess;
+  }
   const int nseg = (int)B.segs.size();
   // flag[r]: round r changed an exit state (r = 1 .. kDeviceRounds)
   if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4 * (kDeviceRounds + 2), s);
@@ -1927,7 +1942,8 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   int changed = 0;
   const unsigned short* luts = B.T.huff.empty() ? nullptr : B.T.huff[0].look;
   const int ls = kGlobalLutStride;
-  for (int i = 0; i < nch; ++i) sync_chunk(X, luts, ls, i, 0, S.data(), E1.data(), E0.data(), cnt.data(), &changed);
+  for (int i = 0; i < nch; ++i)
+    sync_chunk(X, X.pool, luts, ls, i, 0, S.data(), E1.data(), E0.data(), cnt.data(), &changed);
   long long* Ein = E0.data();
   long long* Eout = E1.data();
   int rounds = 0;
@@ -1938,7 +1954,7 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   for (int r = 1; r <= std::min(qmax, nch + 1); ++r) {
     changed = 0;
     const std::vector<long long> S0 = S;
-    for (int i = 0; i < nch; ++i) sync_chunk(X, luts, ls, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
+    for (int i = 0; i < nch; ++i) sync_chunk(X, X.pool, luts, ls, i, r, S.data(), Ein, Eout, cnt.data(), &changed);
     int nchg = 0;
     for (int i = 0; i < nch; ++i) nchg += S[i] != S0[i];
     std::fprintf(stderr, "round %d: %d of %d chunk starts changed\n", r, nchg, nch);
@@ -1974,7 +1990,8 @@ extern "C" int ef_diag_jpeg_decode_host(const uint8_t* data, const int64_t* offs
   }
   for (const JSeg& sg : B.segs) scan_segment(X, sg, cnt.data(), G.data(), P.data());
   std::vector<short> coef((size_t)B.coef_blocks * 64 + 64, 0);
-  for (int i = 0; i < nch; ++i) write_chunk(X, luts, ls, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost);
+  for (int i = 0; i < nch; ++i)
+    write_chunk(X, X.pool, luts, ls, i, S.data(), G.data(), P.data(), coef.data(), kNaturalHost);
   std::vector<uint8_t> planes((size_t)B.plane_bytes + 16);
   for (size_t r = 0; r < B.block_start.size(); ++r) {
     const JImage& im = B.imgs[B.ic[r] >> 2];
