@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -294,17 +295,23 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 // One barrier per template-row pair (half the barriers, and half the LDS fragment reads
 // per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).
 constexpr int kTmRing = 144;  // A-ring slots (>= 133; 144 * 16 = 0 mod 256 keeps banks aligned)
-constexpr int kTmMaxSA = 528;
-constexpr int kTmMaxNkb = (kTmPiece + 31 + 31) / 32;
-constexpr int kTmBStage = 2 * kTmMaxNkb * 1024;  // one row pair of band slices
+constexpr int tm_max_sa(int maxnkb) { return (32 * (maxnkb + 3) + 255) / 256 * 256 + 16; }
+constexpr int tm_lds_bytes(int maxnkb) { return kTmRing * tm_max_sa(maxnkb) + 3 * 2 * maxnkb * 1024 + 1024; }
 
-__global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restrict__ f8, int64_t pitch,
-                                                         const uint8_t* __restrict__ bands,
-                                                         const TmPiece* __restrict__ pieces,
-                                                         const TmWork* __restrict__ works,
-                                                         const TmProblem* __restrict__ probs, int* __restrict__ parts,
-                                                         int nwork) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kTmRing * kTmMaxSA + 3 * kTmBStage + 1024];
+// MAXNKB: the largest k-block count of the launch's pieces (12 for 352-column pieces; the
+// diagnostic build's EF_TM_PIECE = 96 runs MAXNKB = 5, whose 71 KiB of LDS let two
+// workgroups share a CU).
+template <int MAXNKB>
+__global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const int8_t* __restrict__ f8,
+                                                                          int64_t pitch,
+                                                                          const uint8_t* __restrict__ bands,
+                                                                          const TmPiece* __restrict__ pieces,
+                                                                          const TmWork* __restrict__ works,
+                                                                          const TmProblem* __restrict__ probs,
+                                                                          int* __restrict__ parts, int nwork) {
+  constexpr int kTmMaxSA = tm_max_sa(MAXNKB), kTmMaxNkb = MAXNKB, kTmBStage = 2 * MAXNKB * 1024;
+  static_assert(tm_lds_bytes(MAXNKB) >= 4 * 4 * 16 * 64 * 4, "the final reduction reuses the ring");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[tm_lds_bytes(MAXNKB)];
   const TmWork wk = works[blockIdx.x];
   const TmPiece pc = pieces[wk.piece];
   const TmProblem pb = probs[pc.prob];
@@ -428,9 +435,9 @@ __global__ __launch_bounds__(512, 1) void tm_corr_kernel(const int8_t* __restric
 #undef EF_STAMP
   };
   switch (nkb) {
-#define EF_TM_NKB(V) \
-  case V:            \
-    run(std::integral_constant<int, V>{}); \
+#define EF_TM_NKB(V)                                     \
+  case V:                                                \
+    if constexpr (V <= MAXNKB) run(std::integral_constant<int, V>{}); \
     break;
     EF_TM_NKB(1) EF_TM_NKB(2) EF_TM_NKB(3) EF_TM_NKB(4) EF_TM_NKB(5) EF_TM_NKB(6)
     EF_TM_NKB(7) EF_TM_NKB(8) EF_TM_NKB(9) EF_TM_NKB(10) EF_TM_NKB(11) EF_TM_NKB(12)
@@ -557,7 +564,7 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
 
 // ------------------------------------------------------------------ ctx state
 struct TmState {
-  int H = 0, W = 0, nprob = 0, nwork = 0;
+  int H = 0, W = 0, nprob = 0, nwork = 0, max_nkb = 0;
   bool ii64 = false;  // int64 integral images (some template area >= 2^18, or EF_TM_II64)
   int64_t pitch = 0, max_pos = 0, map_total = 0;
   std::vector<TmProblem> probs;
@@ -659,6 +666,10 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     const int64_t e = templ_offsets[i] + (int64_t)templ_h[i] * templ_w[i];
     raw_bytes = e > raw_bytes ? e : raw_bytes;
   }
+  int piece_w = kTmPiece;  // template columns per piece
+#ifdef EF_DIAGNOSTICS
+  if (const char* e = std::getenv("EF_TM_PIECE")) piece_w = std::max(1, std::min(kTmPiece, std::atoi(e)));
+#endif
   std::vector<ImgDesc> rd;
   std::vector<TmPiece> pieces;
   std::vector<TmWork> works;
@@ -676,7 +687,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     pb.tmpl_off = scaled_bytes;
     rd.push_back(ImgDesc{templ_offsets[ti], scaled_bytes, templ_h[ti], templ_w[ti], 1, th, tw, 0});
     scaled_bytes += rup((int64_t)th * tw, 16);
-    const int npiece = (tw + kTmPiece - 1) / kTmPiece;
+    const int npiece = (tw + piece_w - 1) / piece_w;
     const int nchunk = (th + kTmChunk - 1) / kTmChunk;
     pb.nparts = npiece * nchunk;
     pb.part_off = part_elems;
@@ -689,9 +700,10 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     for (int q = 0; q < npiece; ++q) {
       TmPiece pc{};
       pc.prob = p;
-      pc.px = q * kTmPiece;
-      pc.wp = std::min(kTmPiece, tw - pc.px);
+      pc.px = q * piece_w;
+      pc.wp = std::min(piece_w, tw - pc.px);
       pc.nkb = (pc.wp + 31 + 31) / 32;
+      t->max_nkb = std::max(t->max_nkb, pc.nkb);
       pc.band_off = band_bytes;
       band_bytes += (int64_t)th * pc.nkb * 1024;
       const int pi = (int)pieces.size();
@@ -790,11 +802,17 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
     hipLaunchKernelGGL(tm_cols_kernel<unsigned>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
   }
   if (t->nprob > 0) {
-    if (t->nwork > 0)
-      hipLaunchKernelGGL(tm_corr_kernel, dim3((unsigned)t->nwork), dim3(512), 0, s, f8, t->pitch,
+    if (t->nwork > 0) {
+      bool narrow = t->max_nkb <= 5;
+#ifdef EF_DIAGNOSTICS
+      if (std::getenv("EF_TM_WIDE")) narrow = false;  // A/B: one workgroup per CU
+#endif
+      auto corr = narrow ? tm_corr_kernel<5> : tm_corr_kernel<12>;
+      hipLaunchKernelGGL(corr, dim3((unsigned)t->nwork), dim3(512), 0, s, f8, t->pitch,
                          static_cast<const uint8_t*>(t->bands.p), static_cast<const TmPiece*>(t->d_pieces.p),
                          static_cast<const TmWork*>(t->d_works.p), static_cast<const TmProblem*>(t->d_probs.p),
                          static_cast<int*>(t->parts.p), t->nwork);
+    }
     float* maps = nullptr;
     if (maps_out) {
       if (dev) {
