@@ -4,6 +4,9 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <utility>
 #include <vector>
 
 #include "ef_internal.hpp"
@@ -222,6 +225,19 @@ static int stage_probes(ef_ctx* c, const void* P, int dtype, int64_t b, uint32_t
   EF_HIP(c, hipMemcpyAsync(c->p_stage.p, P, bytes, hipMemcpyHostToDevice, c->stream), "H2D probes");
   *Pd = c->p_stage.p;
   return EF_OK;
+}
+
+hipError_t allow_dynamic_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;  // (kernel, device)
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
 }
 
 }  // namespace ef

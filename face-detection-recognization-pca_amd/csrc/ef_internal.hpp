@@ -186,6 +186,9 @@ size_t img_desc_size();
 void img_desc_fill(void* d, int64_t src_off, int64_t dst_off, int h, int w, int c, int oh, int ow);
 // wait for every queued JPEG upload and decode of the context (ef_jpeg.hip)
 hipError_t jpeg_quiesce(ef_ctx* c);
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (kernel, device),
+// thread-safe (several contexts may launch the same kernel on different devices)
+hipError_t allow_dynamic_lds(const void* fn, int bytes);
 // all-gather over the attached communicator on ctx->stream (bytes per rank)
 int comm_allgather(ef_ctx* c, const void* send, void* recv, size_t bytes_per_rank);
 hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,

@@ -1684,15 +1684,10 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
   const unsigned cgrid = (unsigned)((nchunks + kChunkThreads - 1) / kChunkThreads);
   const int lds_tables = B.T.huff.size() <= (size_t)kLdsTables ? (int)B.T.huff.size() : 0;
   const size_t lds_bytes = (size_t)lds_tables * kTabBytes;
-  static bool lds_attr = false;  // up to kLdsTables whole tables: > 64 KiB of dynamic LDS
-  if (!lds_attr && e == hipSuccess) {
+  if (e == hipSuccess) {  // up to kLdsTables whole tables: > 64 KiB of dynamic LDS
     const int most = kLdsTables * kTabBytes + 128;
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_sync_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            most);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(jpeg_write_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, most);
-    lds_attr = e == hipSuccess;
+    e = allow_dynamic_lds(reinterpret_cast<const void*>(jpeg_sync_kernel), most);
+    if (e == hipSuccess) e = allow_dynamic_lds(reinterpret_cast<const void*>(jpeg_write_kernel), most);
   }
   const int nseg = (int)B.segs.size();
   // flag[r]: round r changed an exit state (r = 1 .. kDeviceRounds)

@@ -391,13 +391,9 @@ hipError_t launch_jacobi(hipStream_t s, const double* A, int m, int64_t lda, dou
                          int64_t ldv, int max_sweeps, int* info) {
   if (m < 1 || m > kJacobiMax) return hipErrorInvalidValue;
   const size_t lds = jacobi_lds_bytes(m);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(jacobi_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)jacobi_lds_bytes(kJacobiMax));
+  {
+    const hipError_t e = allow_dynamic_lds(reinterpret_cast<const void*>(jacobi_kernel), (int)jacobi_lds_bytes(kJacobiMax));
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(jacobi_kernel, dim3(1), dim3(1024), lds, s, A, m, lda, evals, evecs, ldv, max_sweeps,
                      info);
@@ -601,13 +597,10 @@ hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double 
     hipLaunchKernelGGL(chol_small_kernel, dim3(1), dim3(1024), 0, s, A, m, lda, tol_rel, info);
     return hipGetLastError();
   }
-  static bool attr_set = false;
-  const size_t lds = (size_t)kCholMaxM * kCholPS * sizeof(double);
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chol_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    const hipError_t e = allow_dynamic_lds(reinterpret_cast<const void*>(chol_kernel),
+                                           (int)((size_t)kCholMaxM * kCholPS * sizeof(double)));
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), (size_t)m * kCholPS * sizeof(double), s, A, m, lda, tol_rel,
                      info);
