@@ -11,15 +11,20 @@
 // combine 2^-t_c sum_j 256^j I_j (proj_combine_kernel) — the same order of error as the
 // fp64 GEMM it replaces (reference: useless/train.py:122 in float64).
 //
-// proj_i8_kernel: C[n][N] (int32) = X' . D^T with D = [N = P * kk padded to 128][d] int8
-// (K-contiguous).  Workgroup tile 256 rows x 128 digit-columns, 8 waves of 64 x 64, K
-// stages of 64 bytes staged by LDS-DMA into a 4-stage ring (same 64-B row swizzle as the
-// covariance kernel); A fragments are flipped to int8 (x ^ 0x80) in registers.  The
-// N-tiles of one row block are consecutive on one XCD, so X is read from HBM about once.
+// proj_i8_kernel<TN>: C[n][N] (int32) = X' . D^T with D = [N = P * kk padded to TN][d] int8
+// (K-contiguous).  Workgroup tile 256 rows x TN digit-columns, 8 waves (TN = 128: 4 x 2 of
+// 64 x 64; TN = 256: 2 x 4 of 128 x 64), K stages of 64 bytes staged by LDS-DMA into a
+// 4-stage ring (same 64-B row swizzle as the covariance kernel); A fragments are flipped to
+// int8 (x ^ 0x80) in registers.  The N-tiles of one row block are consecutive on one XCD,
+// so X is read from HBM about once.  A stage streams (256 + TN) x 64 B from L2 for
+// 256 x TN x 64 MACs: 48 B per MFMA-clock of a CU at TN = 128, 32 at TN = 256 — the L2 -> LDS
+// stream (~30 B/clk per CU, K3) is the limit, so 7 digits x kk = 128 run as 4 tiles of 256
+// (14 % padding) rather than 7 of 128.
 // Requires d % 64 == 0 (X rows are DMA'd 64 bytes at a time; otherwise the caller keeps
 // the fp64 GEMM).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "ef_dma.hpp"
 #include "ef_linalg.hpp"
@@ -32,12 +37,10 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int PM = 256;           // rows per tile
-constexpr int PN = 128;           // digit-columns per tile
 constexpr int PK = 64;            // K bytes per stage
 constexpr int PNB = 4;            // LDS ring stages
 constexpr int kDigits = 7;        // base-256 digits of the scaled eigenvector entries
 constexpr int kTopBit = 54;       // largest scaled entry ~ 2^54
-constexpr int PSTAGE = (PM + PN) * PK;  // 24 KiB per stage
 
 // t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^53, 2^54); zero columns get t_c = 0.
 __global__ void digit_scale_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
@@ -91,30 +94,34 @@ __global__ void cc_kernel(const double* __restrict__ E, const double* __restrict
   if (threadIdx.x == 0) cc[c] = red[0];
 }
 
+template <int TN>
 __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
                                                          const int8_t* __restrict__ D, int ntn, int nblocks,
                                                          int* __restrict__ C, int64_t ldc) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[PNB * PSTAGE];  // [stage][A 16 KiB | B 8 KiB]
+  constexpr int WN = TN / 64, WM = 8 / WN;      // wave grid; a wave owns (PM / WM) x 64
+  constexpr int IA = PM / WM / 32, JB = 2;      // 32 x 32 blocks per wave
+  constexpr int BPW = TN / 128;                 // B pieces per wave per stage (A: 2)
+  constexpr int PSTAGE = (PM + TN) * PK;        // bytes per stage: A panel, then B panel
+  __shared__ __attribute__((aligned(16))) uint8_t smem[PNB * PSTAGE];
   const int total = gridDim.x;  // multiple of 8; trailing blocks are idle padding
   // blocks b and b+8 share an XCD: XCD x runs items [x*total/8, (x+1)*total/8), row-block
   // major, so the N-tiles of a row block run together and share its X rows in L2
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
   if (lin >= nblocks) return;
   const int mt = lin / ntn, nt = lin - (lin / ntn) * ntn;
-  const int64_t m0 = (int64_t)mt * PM, n0 = (int64_t)nt * PN;
+  const int64_t m0 = (int64_t)mt * PM, n0 = (int64_t)nt * TN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c32 = lane & 31;
-  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 x 64
+  const int wm = wave / WN, wn = wave % WN;
 
-  // DMA: a stage = 16 A pieces + 8 B pieces of 1 KiB (16 rows x 64 B); wave w issues A
-  // pieces 2w, 2w+1 and B piece w.  Lane l -> row 16j + (l >> 2), physical chunk l & 3
-  // holding logical chunk (l & 3) ^ ((l >> 4) & 3).
+  // DMA: a stage = 16 A pieces + TN / 16 B pieces of 1 KiB (16 rows x 64 B); wave w issues
+  // A pieces 2w, 2w+1 and B pieces BPW w .. BPW w + BPW - 1.  Lane l -> row 16j + (l >> 2),
+  // physical chunk l & 3 holding logical chunk (l & 3) ^ ((l >> 4) & 3).
   const unsigned lds_base = lds_addr(smem);
   const int lrow = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lane >> 4) & 3);
-  unsigned voffB;
   // A rows are d bytes apart (X row-major): 64-bit per-lane row base, stage offset added
   const uint8_t* arow[2];
 #pragma unroll
@@ -123,60 +130,90 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
     ra = ra < n ? ra : n - 1;
     arow[jj] = X + ra * d + lchunk * 16;
   }
-  voffB = (unsigned)((n0 + wave * 16 + lrow) * d + lchunk * 16);  // D is N x d (< 4 GiB)
+  const unsigned voffB = (unsigned)((n0 + wave * BPW * 16 + lrow) * d + lchunk * 16);  // D is N x d (< 4 GiB)
   const int64_t nst = d / PK;
   auto issue = [&](int64_t st, int buf) {
     const unsigned sbuf = lds_base + (unsigned)(buf * PSTAGE);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) glds16(arow[jj] + st * PK, sbuf + (unsigned)((wave * 2 + jj) * 1024));
-    glds16s(voffB + (unsigned)(st * PK), (unsigned long long)(size_t)D, sbuf + (unsigned)(PM * PK + wave * 1024));
+#pragma unroll
+    for (int q = 0; q < BPW; ++q)
+      glds16s(voffB + (unsigned)(q * 16 * d + st * PK), (unsigned long long)(size_t)D,
+              sbuf + (unsigned)(PM * PK + (wave * BPW + q) * 1024));
   };
 
-  i32x16 acc[2][2];
+  i32x16 acc[IA][JB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IA; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = i32x16{};
+    for (int j = 0; j < JB; ++j) acc[i][j] = i32x16{};
 
   const int sw = (c32 >> 2) & 3;
   const i32x4 flip = {(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
-  // ring of PNB stages, 3 DMA instructions per wave per stage: "stage st landed" is
-  // vmcnt <= 3 x (stages issued after it); tail stages re-read stage 0 to keep counts uniform
-  for (int j = 0; j < PNB - 1; ++j) issue(j < nst ? j : 0, j);
+  // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r] for k-step s of a stage
+  const unsigned offa[2] = {(unsigned)((wm * (PM / WM) + c32) * PK + ((h ^ sw) * 16)),
+                            (unsigned)((wm * (PM / WM) + c32) * PK + (((2 + h) ^ sw) * 16))};
+  const unsigned offb[2] = {(unsigned)(PM * PK + (wn * 64 + c32) * PK + ((h ^ sw) * 16)),
+                            (unsigned)(PM * PK + (wn * 64 + c32) * PK + (((2 + h) ^ sw) * 16))};
+  auto fa = [&](const uint8_t* sa, int ks, int i) {
+    return *reinterpret_cast<const i32x4*>(sa + offa[ks] + i * 32 * PK) ^ flip;
+  };
+  auto fb = [&](const uint8_t* sa, int ks, i32x4 (&bb)[JB]) {
+#pragma unroll
+    for (int j = 0; j < JB; ++j) bb[j] = *reinterpret_cast<const i32x4*>(sa + offb[ks] + j * 32 * PK);
+  };
+  // one k-step's MFMAs, row block by row block; each A fragment is refilled with the next
+  // k-step's as soon as its row block's MFMAs are issued
+  auto mma = [&](i32x4 (&a)[IA], const i32x4 (&bb)[JB], const uint8_t* nsa, int ns) {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+#pragma unroll
+      for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
+      a[i] = fa(nsa, ns, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Ring of PNB stages, 2 + BPW DMA instructions per wave per stage: "stage t landed" is
+  // vmcnt <= (2 + BPW) x (stages issued after it); tail stages re-read stage 0 so the count
+  // stays uniform.  As in the covariance SYRK (ef_cov_i8.hip), the one barrier per stage
+  // sits between its two k-steps (stage st+1 published, stage st's slot retired), so the
+  // next stage's first fragments are read, and the DMA into the retired slot issued, while
+  // the second k-step's MFMAs still run.
+  constexpr int Q = 2 + BPW;
+  for (int j = 0; j < PNB; ++j) issue(j < nst ? j : 0, j);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Q * (PNB - 1)) : "memory");  // stage 0 landed
+  __syncthreads();
+  i32x4 a[IA], b0[JB], b1[JB];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) a[i] = fa(smem, 0, i);
+  fb(smem, 0, b0);
   for (int64_t st = 0; st < nst; ++st) {
-    const int buf = (int)(st % PNB);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // stage st landed (2 newer stages pending)
-    __syncthreads();                                   // ... for every wave; stage st-1 consumed
+    const uint8_t* cur = smem + (st % PNB) * PSTAGE;
+    fb(cur, 1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a, b0, cur, 1);  // k-step 0; A refilled with k-step 1
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Q * (PNB - 2)) : "memory");  // stage st+1 landed
+    __syncthreads();  // every wave done reading stage st; stage st+1 visible
     {
-      const int64_t nx = st + PNB - 1;
-      issue(nx < nst ? nx : 0, (int)(nx % PNB));
+      const int64_t nx = st + PNB;
+      issue(nx < nst ? nx : 0, (int)(nx % PNB));  // into stage st's slot
     }
-    const uint8_t* sa = smem + buf * PSTAGE;
-    const uint8_t* sb = sa + PM * PK;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {  // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r]
-      const int pch = ((2 * s + h) ^ sw) * 16;
-      i32x4 a[2], b[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        a[i] = *reinterpret_cast<const i32x4*>(sa + (wm * 64 + i * 32 + c32) * PK + pch) ^ flip;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const i32x4*>(sb + (wn * 64 + j * 32 + c32) * PK + pch);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+    // (after the last stage these read a slot holding a re-read of the first stage:
+    // harmless, unused, and branch-free)
+    const uint8_t* nxt = smem + ((st + 1) % PNB) * PSTAGE;
+    fb(nxt, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a, b1, nxt, 0);  // k-step 1; A refilled with the next stage's k-step 0
   }
   dma_wait_all();
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IA; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < JB; ++j) {
       const int64_t col = n0 + wn * 64 + j * 32 + c32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t row = m0 + wm * (PM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row < n) C[row * ldc + col] = acc[i][j][r];
       }
     }
@@ -201,11 +238,19 @@ __global__ void proj_combine_kernel(const int* __restrict__ I, int64_t n, int kk
 
 struct ProjLayout {
   int64_t np, off_i, off_t, off_c, bytes;
+  int tn;  // digit-columns per tile (128 or 256)
 };
 static ProjLayout proj_layout(int64_t n, int64_t d, int kk) {
   auto a256 = [](int64_t v) { return (v + 255) / 256 * 256; };
   ProjLayout L;
-  L.np = (int64_t)(kDigits * kk + PN - 1) / PN * PN;
+  // 256-column tiles (two thirds of the L2 -> LDS bytes per MAC) unless they pad the digit
+  // columns by > 15 % more than 128-column tiles do
+  const int64_t p = (int64_t)kDigits * kk, n128 = (p + 127) / 128 * 128, n256 = (p + 255) / 256 * 256;
+  L.tn = n256 * 100 <= n128 * 115 ? 256 : 128;
+#ifdef EF_DIAGNOSTICS
+  if (const char* e = getenv("EF_PROJ_TN")) L.tn = atoi(e) == 256 ? 256 : 128;
+#endif
+  L.np = L.tn == 256 ? n256 : n128;
   L.off_i = a256(L.np * d);
   L.off_t = L.off_i + a256(n * L.np * (int64_t)sizeof(int));
   L.off_c = L.off_t + a256((int64_t)kk * sizeof(int));
@@ -234,11 +279,16 @@ hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
   hipLaunchKernelGGL(digit_scale_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, d, kk, tsh);
   hipLaunchKernelGGL(digits_kernel, dim3((unsigned)((d * kk + 255) / 256)), dim3(256), 0, s, E, w, d, kk, tsh, D);
   hipLaunchKernelGGL(cc_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, mu, d, kk, cc);
-  const int ntn = (int)(np / PN);
+  const int ntn = (int)(np / L.tn);
   const int64_t nblocks = (n + PM - 1) / PM * ntn;
   if (nblocks > (int64_t)1 << 30) return hipErrorInvalidValue;
   const int grid = (int)((nblocks + 7) / 8 * 8);
-  hipLaunchKernelGGL(proj_i8_kernel, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I, np);
+  if (L.tn == 256)
+    hipLaunchKernelGGL(proj_i8_kernel<256>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
+                       np);
+  else
+    hipLaunchKernelGGL(proj_i8_kernel<128>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
+                       np);
   hipLaunchKernelGGL(proj_combine_kernel, dim3((unsigned)((n * kk + 255) / 256)), dim3(256), 0, s, I, n, kk, np, tsh,
                      cc, F);
   return hipGetLastError();
