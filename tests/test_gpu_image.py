@@ -60,6 +60,8 @@ CASES = [  # frame (H, W), template (h, w)
     ((60, 500), (21, 380)),     # > 352 template columns: two pieces
     ((300, 300), (1, 1)),
     ((33, 33), (33, 33)),       # 1 x 1 result
+    ((200, 300), (40, 130)),    # widest 5-k-block piece: the 71 KiB correlation kernel
+    ((200, 300), (40, 131)),    # narrowest 6-k-block piece: the 148 KiB kernel
 ]
 
 
