@@ -4,7 +4,9 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <set>
 #include <utility>
 #include <vector>
@@ -225,6 +227,66 @@ static int stage_probes(ef_ctx* c, const void* P, int dtype, int64_t b, uint32_t
   EF_HIP(c, hipMemcpyAsync(c->p_stage.p, P, bytes, hipMemcpyHostToDevice, c->stream), "H2D probes");
   *Pd = c->p_stage.p;
   return EF_OK;
+}
+
+namespace {
+class HostPool {
+ public:
+  explicit HostPool(int workers) {
+    for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  void run(int n, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> job(job_mu_);  // one job at a time
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_ = 0;
+      done_ = 0;
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lk(mu_);
+    while (next_ < n_) {  // the caller takes tasks too (and finishes the job alone if
+      const int i = next_++;  // the workers are gone, e.g. in a forked child)
+      lk.unlock();
+      fn(i);
+      lk.lock();
+      ++done_;
+    }
+    done_cv_.wait(lk, [&] { return done_ == n_; });
+    fn_ = nullptr;
+    n_ = 0;
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return fn_ && next_ < n_; });
+      const int i = next_++;
+      const std::function<void(int)>* f = fn_;
+      lk.unlock();
+      (*f)(i);  // the job cannot end before this task is counted
+      lk.lock();
+      if (++done_ == n_) done_cv_.notify_all();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, next_ = 0, done_ = 0;
+  std::vector<std::thread> threads_;
+};
+}  // namespace
+
+void host_parallel(int n, const std::function<void(int)>& fn) {
+  if (n <= 1) {
+    if (n == 1) fn(0);
+    return;
+  }
+  // never destroyed: the workers block on the condition variable until the process exits
+  static HostPool* pool = new HostPool((int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()) - 1));
+  pool->run(n, fn);
 }
 
 hipError_t allow_dynamic_lds(const void* fn, int bytes) {

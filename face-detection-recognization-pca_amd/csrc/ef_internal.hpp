@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <utility>
 #include <vector>
@@ -189,6 +190,12 @@ hipError_t jpeg_quiesce(ef_ctx* c);
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (kernel, device),
 // thread-safe (several contexts may launch the same kernel on different devices)
 hipError_t allow_dynamic_lds(const void* fn, int bytes);
+
+// Runs fn(0) .. fn(n - 1) on a process-wide pool of host worker threads (created once, at
+// most 15, plus the calling thread, which takes tasks too) and returns when all are done.
+// Jobs from concurrent callers run one at a time.  Spawning threads per call cost ~1-2 ms
+// per 16 threads in the sandboxed containers, as much as the host work it split.
+void host_parallel(int n, const std::function<void(int)>& fn);
 // all-gather over the attached communicator on ctx->stream (bytes per rank)
 int comm_allgather(ef_ctx* c, const void* send, void* recv, size_t bytes_per_rank);
 hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,

@@ -1398,13 +1398,7 @@ void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* siz
   };
   std::vector<int> t_beg(nt + 1);
   for (int t = 0; t <= nt; ++t) t_beg[t] = (int)((int64_t)count * t / nt);
-  if (nt == 1) {
-    work(0, 0, count);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back(work, t, t_beg[t], t_beg[t + 1]);
-    for (auto& x : th) x.join();
-  }
+  host_parallel(nt, [&](int t) { work(t, t_beg[t], t_beg[t + 1]); });
   // merge in file order: thread-local table indices -> batch tables, then the layout
   for (int t = 0; t < nt; ++t) {
     // tables enter the batch lazily, in the order the accepted files use them
@@ -1497,13 +1491,7 @@ void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t*
   const int64_t bytes = B.words * 4;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t nt = bytes < ((int64_t)4 << 20) ? 1 : std::min<size_t>({16, hw, n});
-  if (nt <= 1) {
-    work(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (size_t t = 0; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
-  for (auto& t : th) t.join();
+  host_parallel((int)nt, [&](int t) { work(n * t / nt, n * (t + 1) / nt); });
 }
 
 // Chunk size: about 128k chunks for the batch (4 per SIMD lane group of the chip), kept in
@@ -1856,8 +1844,10 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
   int64_t call_chunk_bits = 0;
   auto prepare = [&](Part& P) {
     (void)hipSetDevice(c->device);  // a fresh host thread starts on device 0
+    StageTimer tm;
     P.st.assign(P.m, 0);
     build_batch(data, offsets + P.a, sizes + P.a, P.m, mode, nullptr, P.st.data(), P.B);
+    tm.mark("parse");
     if (P.B.imgs.empty()) return;
     Batch& B = P.B;
     B.file_img.assign((size_t)P.m, -1);  // file j of the part -> row j
