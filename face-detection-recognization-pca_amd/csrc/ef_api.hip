@@ -86,18 +86,27 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
   } while (0)
 
 // Search the probes already in ctx->q_pad (bpad rows, kp = ctx->g_kp) of this rank's
-// gallery: keys_dev[b] and, when match_dev is non-null, the fp64 match records.
+// gallery: keys_dev[b] and, when match_dev is non-null, the fp64 match records.  The search
+// kernels address probe rows with 32-bit byte offsets, so a batch with bpad x kp x 4 >= 2^31
+// (wide features, k > 512) is searched in pieces of whole 256-probe tiles.
 static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev, ef_match* match_dev) {
   if (c->n_gallery == 0) {
     EF_HIP(c, launch_keys_none(c->stream, keys_dev, b, match_dev), "keys");
     return EF_OK;
   }
-  const SearchPlan pl = search_plan(bpad, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
-  // workspace carve-out (16-byte aligned pieces)
+  const int64_t row_bytes = (int64_t)c->g_kp * 4;
+  const int64_t piece = std::max<int64_t>(kSearchProbeTile, ((int64_t)INT_MAX / row_bytes) / kSearchProbeTile * kSearchProbeTile);
+  const int64_t bpad_max = std::min(bpad, piece);
+  const SearchPlan pl_max = search_plan(bpad_max, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
+  // the last piece may be shorter, and a shorter piece's plan may have more chunks
+  const int64_t bpad_last = b > piece ? round_up(b - (b - 1) / piece * piece, kSearchProbeTile) : bpad_max;
+  const SearchPlan pl_last = search_plan(bpad_last, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
+  const size_t parts = (size_t)std::max<int64_t>(pl_max.nchunks * bpad_max, pl_last.nchunks * bpad_last);
+  // workspace carve-out (16-byte aligned pieces), sized for the largest piece
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  const size_t nkb = al((size_t)pl.nchunks * bpad * 8), nb2 = al((size_t)pl.nchunks * bpad * 4);
-  const size_t ncnt = al(16), nlist = al((size_t)bpad * 4), nthr = al((size_t)bpad * 4);
-  const size_t ncand = al((size_t)bpad * kCandMax * 4), ncc = al((size_t)bpad * 4);
+  const size_t nkb = al(parts * 8), nb2 = al(parts * 4);
+  const size_t ncnt = al(16), nlist = al((size_t)bpad_max * 4), nthr = al((size_t)bpad_max * 4);
+  const size_t ncand = al((size_t)bpad_max * kCandMax * 4), ncc = al((size_t)bpad_max * 4);
   EF_TRY(ensure(c, c->search_ws, nkb + nb2 + ncnt + nlist + nthr + ncand + ncc));
   char* base = static_cast<char*>(c->search_ws.p);
   SearchWs ws;
@@ -114,13 +123,12 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
   ws.cand = reinterpret_cast<int*>(base);
   base += ncand;
   ws.cand_cnt = reinterpret_cast<int*>(base);
-  ws.match = match_dev;
   const float* aux = static_cast<const float*>(metric == EF_METRIC_L2 ? c->gnorm2.p : c->ginv.p);
   const float* G3 = nullptr;
   float* Q3 = nullptr;
   if (c->opt_search_split_bf16) {  // split-bf16 scan
     if (c->g_kp > 128) {
-      EF_TRY(ensure(c, c->q3, (size_t)bpad * c->g_kp * sizeof(float)));
+      EF_TRY(ensure(c, c->q3, (size_t)bpad_max * c->g_kp * sizeof(float)));
       Q3 = static_cast<float*>(c->q3.p);
     }
     if (!c->g3_valid) {
@@ -131,11 +139,16 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
     }
     G3 = static_cast<const float*>(c->G3.p);
   }
-  EF_HIP(c,
-         launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p), Q3, bpad, b,
-                       static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset, c->gmax2_host, ws,
-                       keys_dev, c),
-         "search");
+  for (int64_t off = 0; off < b; off += piece) {
+    const int64_t bi = std::min(piece, b - off), bpad_i = round_up(bi, kSearchProbeTile);
+    const SearchPlan& pl = bpad_i == bpad_max ? pl_max : pl_last;
+    ws.match = match_dev ? match_dev + off : nullptr;
+    EF_HIP(c,
+           launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p) + off * c->g_kp, Q3,
+                         bpad_i, bi, static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset,
+                         c->gmax2_host, ws, keys_dev + off, c),
+           "search");
+  }
   return EF_OK;
 }
 
@@ -373,6 +386,12 @@ int ef_set_stream(ef_ctx* c, void* s) {
   return EF_OK;
 }
 
+int ef_get_stream(const ef_ctx* c, void** out) {
+  if (!c || !out) return EF_E_INVALID;
+  *out = static_cast<void*>(c->stream);
+  return EF_OK;
+}
+
 int ef_use_own_stream(ef_ctx* c) {
   if (!c) return EF_E_INVALID;
   c->stream = c->own_stream;
@@ -409,7 +428,7 @@ int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_
   if (!c) return EF_E_INVALID;
   if (!mean || !W || d < 1 || k < 1) return set_err(c, EF_E_INVALID, "ef_model_set: bad arguments");
   const int kp = feature_pad(k);
-  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_model_set: k > 512 is not supported by this build");
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_model_set: k > 65536 is not supported");
   (void)hipSetDevice(c->device);
   const bool bf16 = (flags & EF_MODEL_BF16) != 0;
   const int kpw = bf16 ? (kp + 127) / 128 * 128 : proj_pad(kp);  // bf16 kernel: 128-column tiles
@@ -495,7 +514,7 @@ int ef_gallery_set(ef_ctx* c, const float* G, int64_t n, int32_t k, int64_t offs
   if ((!G && n > 0) || n < 0 || k < 1 || offset < 0 || n + offset > (int64_t)UINT_MAX)
     return set_err(c, EF_E_INVALID, "ef_gallery_set: bad arguments");
   const int kp = feature_pad(k);
-  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 512 is not supported by this build");
+  if (kp < 0) return set_err(c, EF_E_INVALID, "ef_gallery_set: k > 65536 is not supported");
   (void)hipSetDevice(c->device);
   c->n_gallery = 0;
   c->g3_valid = false;

@@ -230,20 +230,20 @@ __global__ __launch_bounds__(256) void transpose_stats_lds_kernel(const uint8_t*
     }
     __syncthreads();
   }
-  // the four quarters of a pixel sit in lanes 4j .. 4j+3
+  // the four quarters of a pixel sit in lanes 4j .. 4j+3.  Each quarter's sums are exact in
+  // 32 bits (<= 4096 blocks x 16 samples x 255^2 < 2^32 per workgroup, launch bound), but
+  // four quarters of Σx² are not: widen before adding them.
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    s1[i] += __shfl_xor(s1[i], 1);
-    s1[i] += __shfl_xor(s1[i], 2);
-    s2[i] += __shfl_xor(s2[i], 1);
-    s2[i] += __shfl_xor(s2[i], 2);
-  }
-  if (q == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    unsigned long long a = s1[i], b = s2[i];
+    a += __shfl_xor(a, 1);
+    a += __shfl_xor(a, 2);
+    b += __shfl_xor(b, 1);
+    b += __shfl_xor(b, 2);
+    if (q == 0) {
       const int64_t col = c0 + (t >> 2) + 64 * i;
-      atomicAdd(&S1[col], (unsigned long long)s1[i]);
-      atomicAdd(&S2[col], (unsigned long long)s2[i]);
+      atomicAdd(&S1[col], a);
+      atomicAdd(&S2[col], b);
     }
   }
 }
@@ -691,7 +691,8 @@ hipError_t launch_cov_i8_prep(hipStream_t s, const uint8_t* X, int64_t n, int64_
   const int64_t nkb = cov_i8_kpad(n) / YK;
   if (S1 && S2) {
     if (!cov_i8_fused_stats(X, d)) return hipErrorInvalidValue;
-    // <= 4096 blocks of 64 rows per workgroup keeps the uint32 partials exact
+    // <= 4096 blocks of 64 rows per workgroup keeps each thread's uint32 partials exact (the
+    // LDS kernel adds its four sample quarters in 64 bits)
     int64_t gx = std::min<int64_t>(nkb, 128);
     gx = std::max<int64_t>(gx, (nkb + 4095) / 4096);
     bool lds = d % 256 == 0;

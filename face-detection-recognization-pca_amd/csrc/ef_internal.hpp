@@ -14,8 +14,12 @@
 namespace ef {
 
 // ---- padded widths ------------------------------------------------------------------
-// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,128,256,512}
-// (zero padding is exact for dot products and distances).
+// Gallery / probe features are stored with k zero-padded to KP in {16,32,64,128,256,512},
+// beyond 512 to a multiple of 128 (zero padding is exact for dot products and distances).
+// k > 512 arises from full-rank per-person models (train-v5.py:539-545 sets
+// n_components = face count).  The search kernels address a probe row with a 32-bit byte
+// offset, so a launch covers at most 2^31 / (4 KP) probes (longer batches run in pieces).
+constexpr int kMaxFeatureK = 1 << 16;
 inline int feature_pad(int k) {
   if (k <= 16) return 16;
   if (k <= 32) return 32;
@@ -23,9 +27,9 @@ inline int feature_pad(int k) {
   if (k <= 128) return 128;
   if (k <= 256) return 256;
   if (k <= 512) return 512;
+  if (k <= kMaxFeatureK) return (k + 127) / 128 * 128;
   return -1;
 }
-constexpr int kMaxK = 512;
 // The projection GEMM writes KPW = 64 or a multiple of 128 columns (128-column tiles).
 inline int proj_pad(int kp) { return kp <= 64 ? 64 : (kp + 127) / 128 * 128; }
 

@@ -237,7 +237,7 @@ hipError_t launch_project(hipStream_t s, int kpw, int p_dtype, const void* P, in
   if (kpw == 64)
     return p_dtype == EF_U8 ? proj_t<64, EF_U8>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps)
                             : proj_t<64, EF_F32>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps);
-  if (kpw % 128 == 0 && kpw <= kMaxK)
+  if (kpw % 128 == 0)
     return p_dtype == EF_U8 ? proj_t<128, EF_U8>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps)
                             : proj_t<128, EF_F32>(s, P, b, bpad, d, mean, W, kpw, part, nsplit, pps);
   return hipErrorInvalidValue;

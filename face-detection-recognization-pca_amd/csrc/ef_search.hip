@@ -688,11 +688,13 @@ __global__ __launch_bounds__(512, 4) void search16_kernel(
 }
 
 // One wave per probe: winner over chunks, global runner-up, fp64 re-score, ambiguity test.
+// KP = 0: row length kp_rt at run time (k > 512).
 template <int KP, int METRIC, bool S3 = false>
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ qpad, int64_t b, int64_t bpad,
                                                      int nchunks, const float* __restrict__ G, int64_t n,
                                                      int64_t g_offset, float gmax2, SearchWs ws,
-                                                     long long* __restrict__ keys) {
+                                                     long long* __restrict__ keys, int kp_rt) {
+  const int kpv = KP > 0 ? KP : kp_rt;
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= b) return;
@@ -724,12 +726,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
 
   const float b1 = key_value(kmin);
   const unsigned row = (unsigned)(kmin & 0xffffffffll);
-  const float* q = qpad + p * KP;
-  const double v = score64<KP, METRIC>(q, G + (int64_t)row * KP, lane);
+  const float* q = qpad + p * kpv;
+  const double v = score64<KP, METRIC>(q, G + (int64_t)row * kpv, lane, kpv);
   // rigorous bound on |fp32 score - exact score| (fp32 FMA chain of KP terms,
   // fp32 ||g||^2 / 1/||g||, final rounding), doubled for the two compared scores
   float qq = 0.f;
-  for (int c = lane; c < KP; c += 64) qq = __builtin_fmaf(q[c], q[c], qq);
+  for (int c = lane; c < kpv; c += 64) qq = __builtin_fmaf(q[c], q[c], qq);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) qq += __shfl_xor(qq, off);
   const float u = 5.9604645e-08f;  // 2^-24
@@ -742,21 +744,21 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
     const float es = 3.05f * 1.5258789e-05f;  // 3.05 * 2^-16
     if constexpr (METRIC == EF_METRIC_L2) {
       const float gm = sqrtf(gmax2);
-      delta = 2.f * (2.f * es * qn * gm + (3 * KP + 4) * 2.f * u * 1.01f * (2.02f * qn * gm + gmax2) +
-                     KP * u * gmax2 + 4.f * u * fabsf(b1)) + 1e-30f;
+      delta = 2.f * (2.f * es * qn * gm + (3 * kpv + 4) * 2.f * u * 1.01f * (2.02f * qn * gm + gmax2) +
+                     kpv * u * gmax2 + 4.f * u * fabsf(b1)) + 1e-30f;
     } else {
-      delta = 2.f * ((es + (3 * KP + 8) * 2.f * u) * 1.01f * qn) + 1e-30f;
+      delta = 2.f * ((es + (3 * kpv + 8) * 2.f * u) * 1.01f * qn) + 1e-30f;
     }
   } else if constexpr (METRIC == EF_METRIC_L2) {
     const float gm = sqrtf(gmax2);
-    delta = 2.f * ((KP + 4) * u * 1.01f * (2.f * qn * gm + gmax2) + 4.f * u * fabsf(b1));
+    delta = 2.f * ((kpv + 4) * u * 1.01f * (2.f * qn * gm + gmax2) + 4.f * u * fabsf(b1));
   } else {
-    delta = 2.f * ((KP + 8) * u * 1.01f * qn) + 1e-30f;
+    delta = 2.f * ((kpv + 8) * u * 1.01f * qn) + 1e-30f;
   }
   delta *= 2.f;  // safety factor
   double qq64 = 0.0;  // tie-tolerance scale of the fp64 resolution (resolve_kernel)
   if (METRIC == EF_METRIC_L2 && ws.match) {
-    for (int c = lane; c < KP; c += 64) qq64 = fma((double)q[c], (double)q[c], qq64);
+    for (int c = lane; c < kpv; c += 64) qq64 = fma((double)q[c], (double)q[c], qq64);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) qq64 += __shfl_xor(qq64, off);
   }
@@ -779,23 +781,24 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
 template <int KP, int METRIC>
 __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ qpad, const float* __restrict__ G,
                                                       int64_t n, int64_t g_offset, float gmax2, SearchWs ws,
-                                                      long long* __restrict__ keys) {
+                                                      long long* __restrict__ keys, int kp_rt) {
+  const int kpv = KP > 0 ? KP : kp_rt;
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (slot >= *ws.amb_count) return;
   const int64_t p = ws.amb_list[slot];
-  const float* q = qpad + p * KP;
+  const float* q = qpad + p * kpv;
   const int cnt = ws.cand_cnt[slot];
   const bool overflow = cnt > kCandMax;
   const int64_t m = overflow ? n : cnt;
   auto row_of = [&](int64_t j) -> int64_t { return overflow ? j : (int64_t)ws.cand[slot * kCandMax + j]; };
   double vmin = INFINITY;
   for (int64_t j = 0; j < m; ++j) {
-    const double v = score64<KP, METRIC>(q, G + row_of(j) * KP, lane);
+    const double v = score64<KP, METRIC>(q, G + row_of(j) * kpv, lane, kpv);
     vmin = v < vmin ? v : vmin;
   }
   double qq = 0.0;
-  for (int c = lane; c < KP; c += 64) qq = fma((double)q[c], (double)q[c], qq);
+  for (int c = lane; c < kpv; c += 64) qq = fma((double)q[c], (double)q[c], qq);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) qq += __shfl_xor(qq, off);
   const double scale = METRIC == EF_METRIC_L2 ? qq + (double)gmax2 : 1.0;
@@ -804,7 +807,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
   double best_v = vmin;
   for (int64_t j = 0; j < m; ++j) {
     const int64_t r = row_of(j);
-    const double v = score64<KP, METRIC>(q, G + r * KP, lane);
+    const double v = score64<KP, METRIC>(q, G + r * kpv, lane, kpv);
     if (v <= vmin + tol && r < best_row) { best_row = r; best_v = v; }
   }
   if (lane == 0 && best_row != LLONG_MAX) {
@@ -933,28 +936,29 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3) {
 // Split-bf16 search (KP <= 128): S3 kernel on the split gallery G3 for the scan and the
 // collect pass; reduce / resolve re-score from the fp32 gallery G as in the fp32 path.
 // KP > 128: the wide kernel streams the probes too, so they are split into Q3 first.
+// KP = 0: k > 512, row length kp at run time (wide kernels only).
 template <int KP, int M>
 static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* qpad, float* Q3, int64_t bpad,
                               int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
                               int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, TimerEvt* tev,
-                              ef_ctx* c) {
-  if constexpr (KP > 128) {
+                              ef_ctx* c, int kp) {
+  if constexpr (KP > 128 || KP == 0) {
     if (!Q3) return hipErrorInvalidValue;
-    hipError_t e = launch_split_rows(s, qpad, bpad, KP, Q3);
+    hipError_t e = launch_split_rows(s, qpad, bpad, kp, Q3);
     if (e != hipSuccess) return e;
     timer_begin(c, EF_KERNEL_SEARCH, tev);
     const int variant = c->opt_search_split_bf16 == 2 ? 2 : 1;  // 16x16x32 unless the 32x32x16 kernel is asked for
-    e = launch_search_wide(s, KP, M, false, variant, pl, Q3, G3, aux, n, bpad, ws);
+    e = launch_search_wide(s, kp, M, false, variant, pl, Q3, G3, aux, n, bpad, ws);
     timer_end(c, tev);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     const dim3 pgrid((unsigned)((b + 3) / 4));
     hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
-                       g_offset, gmax2, ws, keys);
-    e = launch_search_wide(s, KP, M, true, variant, pl, Q3, G3, aux, n, bpad, ws);
+                       g_offset, gmax2, ws, keys, kp);
+    e = launch_search_wide(s, kp, M, true, variant, pl, Q3, G3, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+    hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys, kp);
     return hipGetLastError();
   } else {
     (void)Q3;
@@ -975,14 +979,14 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
     if (e != hipSuccess) return e;
     const dim3 pgrid((unsigned)((b + 3) / 4));
     hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
-                       g_offset, gmax2, ws, keys);
+                       g_offset, gmax2, ws, keys, kp);
     if (k16)
       hipLaunchKernelGGL((search16_kernel<M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G3, aux, n,
                          pl.c_chunks, pl.c_tpc, bpad, ws);
     else
       hipLaunchKernelGGL((search_kernel<KP, M, true, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G3,
                          aux, n, pl.c_chunks, pl.c_tpc, bpad, ws);
-    hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+    hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys, kp);
     return hipGetLastError();
   }
 }
@@ -991,13 +995,13 @@ template <int KP, int M>
 static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpad, float* Q3, int64_t bpad,
                            int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
                            int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, bool timed_main,
-                           TimerEvt* tev, ef_ctx* c) {
-  constexpr bool wide = KP > 128;
-  if (G3) return search_s3_t<KP, M>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, tev, c);
+                           TimerEvt* tev, ef_ctx* c, int kp) {
+  constexpr bool wide = KP > 128 || KP == 0;
+  if (G3) return search_s3_t<KP, M>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, tev, c, kp);
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (timed_main) timer_begin(c, EF_KERNEL_SEARCH, tev);
   if constexpr (wide) {
-    const hipError_t e = launch_search_wide(s, KP, M, false, 0, pl, qpad, G, aux, n, bpad, ws);
+    const hipError_t e = launch_search_wide(s, kp, M, false, 0, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
 #ifdef EF_DIAGNOSTICS
@@ -1023,16 +1027,16 @@ static hipError_t search_t(hipStream_t s, const SearchPlan& pl, const float* qpa
   if (e != hipSuccess) return e;
   const dim3 pgrid((unsigned)((b + 3) / 4));
   hipLaunchKernelGGL((reduce_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n, g_offset,
-                     gmax2, ws, keys);
+                     gmax2, ws, keys, kp);
   // queued (fp32-ambiguous) probes: collect + fp64 resolve; both exit at once when none
   if constexpr (wide) {
-    e = launch_search_wide(s, KP, M, true, 0, pl, qpad, G, aux, n, bpad, ws);
+    e = launch_search_wide(s, kp, M, true, 0, pl, qpad, G, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
   } else {
     hipLaunchKernelGGL((search_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,
                        pl.c_chunks, pl.c_tpc, bpad, ws);
   }
-  hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys);
+  hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys, kp);
   return hipGetLastError();
 }
 
@@ -1045,9 +1049,9 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
   case KPV:                                                                                                 \
     return metric == EF_METRIC_L2                                                                           \
                ? search_t<KPV, EF_METRIC_L2>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, \
-                                             true, &tev, c)                                                       \
+                                             true, &tev, c, kp)                                                   \
                : search_t<KPV, EF_METRIC_COSINE>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, \
-                                                 keys, true, &tev, c);
+                                                 keys, true, &tev, c, kp);
   switch (kp) {
     EF_SEARCH_CASE(16)
     EF_SEARCH_CASE(32)
@@ -1055,8 +1059,13 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
     EF_SEARCH_CASE(128)
     EF_SEARCH_CASE(256)
     EF_SEARCH_CASE(512)
-    default:
-      return hipErrorInvalidValue;
+    default:  // k > 512 (a multiple of 128): the wide kernels with the row length at run time
+      if (kp <= 512 || kp % 128 != 0) return hipErrorInvalidValue;
+      return metric == EF_METRIC_L2
+                 ? search_t<0, EF_METRIC_L2>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys, true,
+                                             &tev, c, kp)
+                 : search_t<0, EF_METRIC_COSINE>(s, pl, qpad, Q3, bpad, b, G, G3, aux, n, g_offset, gmax2, ws, keys,
+                                                 true, &tev, c, kp);
   }
 #undef EF_SEARCH_CASE
 }

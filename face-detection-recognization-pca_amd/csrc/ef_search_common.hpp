@@ -22,11 +22,12 @@ __device__ __forceinline__ float key_value(long long key) {
 
 // fp64 score of gallery row `row` for probe q (L2: squared distance in difference form;
 // cosine: -q.g/(|q||g|), 0 for a zero vector — sklearn normalize semantics).
+// KP = 0: the row length is kp_rt (k > 512, any multiple of 128).
 template <int KP, int METRIC>
-__device__ __forceinline__ double score64(const float* __restrict__ q, const float* __restrict__ g, int lane) {
+__device__ __forceinline__ double score64(const float* __restrict__ q, const float* __restrict__ g, int lane,
+                                          int kp_rt = KP) {
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll
-  for (int c = lane; c < KP; c += 64) {
+  auto term = [&](int c) {
     const double qv = q[c], gv = g[c];
     if constexpr (METRIC == EF_METRIC_L2) {
       const double dv = qv - gv;
@@ -36,6 +37,12 @@ __device__ __forceinline__ double score64(const float* __restrict__ q, const flo
       s1 = fma(qv, qv, s1);
       s2 = fma(gv, gv, s2);
     }
+  };
+  if constexpr (KP > 0) {
+#pragma unroll
+    for (int c = lane; c < KP; c += 64) term(c);
+  } else {
+    for (int c = lane; c < kp_rt; c += 64) term(c);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -52,7 +59,8 @@ __device__ __forceinline__ double score64(const float* __restrict__ q, const flo
   }
 }
 
-// Wide search (KP in {256, 512}): probes streamed through LDS with the gallery.
+// Wide search (KP in {256, 512}, or KP = 0 with a run-time row length kp > 512, a
+// multiple of 128): probes streamed through LDS with the gallery.
 constexpr int kWideRowTile = 128;    // gallery rows per tile
 constexpr int kWideProbeTile = 128;  // probes per workgroup
 constexpr int kWide3RowTile = 256;    // split-bf16 wide kernel: gallery rows per tile

@@ -1,5 +1,6 @@
 // Distance GEMM + fused arg-best for wide features, KP in {256, 512} (BASELINE.json
-// config 5: k = 512 eigenfaces).  Same contract as search_kernel in ef_search.hip (per
+// config 5: k = 512 eigenfaces) and any multiple of 128 above (KP = 0 instantiations: the
+// full-rank per-person models of train-v5.py:539-545, k = face count).  Same contract as search_kernel in ef_search.hip (per
 // chunk best key + runner-up into SearchWs, or COLLECT of the rows within a queued
 // probe's threshold) so reduce_kernel / resolve_kernel finish it unchanged.
 //
@@ -17,6 +18,7 @@
 //     ef_search.hip, once per 128-row tile (<= 6 % of the tile's MFMA time at KP = 256).
 #include "ef_search_common.hpp"
 
+#include <algorithm>
 #include <climits>
 
 namespace ef {
@@ -54,11 +56,30 @@ __device__ __forceinline__ bf16x8w as_bf16x8w(const float4& v) {
   return r;
 }
 
+// Row geometry of a sweep: KP > 0 is a compile-time row length (256 | 512); KP = 0 takes
+// kp_rt, any multiple of 128 above 512 (full-rank per-person models, train-v5.py:539-545),
+// at run time.  A sweep is (tile, slice) pairs flattened into one counter it; for KP = 0
+// the split is a 32-bit division by a wave-uniform value (wide_t checks n_it < 2^31).
+template <int KP>
+struct WideGeom {
+  int kp, ns;  // floats per row, 32-k slices per row
+  __device__ __forceinline__ explicit WideGeom(int kp_rt) : kp(KP > 0 ? KP : kp_rt), ns((KP > 0 ? KP : kp_rt) / WBK) {}
+  __device__ __forceinline__ int64_t tile(int64_t it) const {
+    if constexpr (KP > 0) return it / (KP / WBK);
+    else return (int64_t)((unsigned)it / (unsigned)ns);
+  }
+  __device__ __forceinline__ int slice(int64_t it) const {
+    if constexpr (KP > 0) return (int)(it % (KP / WBK));
+    else return (int)((unsigned)it % (unsigned)ns);
+  }
+};
+
 template <int KP, int METRIC, bool COLLECT>
 __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     const float* __restrict__ qpad, const float* __restrict__ G, const float* __restrict__ aux, int64_t n,
-    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
-  constexpr int NS = KP / WBK;  // slices per tile
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws, int kp_rt) {
+  const WideGeom<KP> geo(kp_rt);
+  const int NS = geo.ns;  // slices per tile
   // [stage 0: gallery | probes][stage 1: gallery | probes][aux of even | odd tiles]
   // (aux is double-buffered by tile: the cosine epilogue reads it in the tile's last
   // slice, when the DMA of the next tile's first slice is already in flight)
@@ -102,8 +123,8 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
     int qrow = slot;
     if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
     const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 7)) * 16);
-    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
-    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (geo.kp * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (geo.kp * 4) + lch16;
   }
   const unsigned aoff = (unsigned)lane * 4;
   float thr = -__builtin_inff();
@@ -119,16 +140,16 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
   const int64_t n_it = (t1 - t0) * NS;
   // DMA of slice it into buffer buf, piece jj of this wave's four (+ the tile's aux).
   auto issue_piece = [&](int64_t it, int buf, int jj) {
-    const int64_t t = t0 + it / NS;
-    const int sl = (int)(it % NS);
+    const int64_t t = t0 + geo.tile(it);
+    const int sl = geo.slice(it);
     const int nrem = (int)((n - t * WR) < WR ? (n - t * WR) : WR);
-    const unsigned long long gb = (unsigned long long)(size_t)(G + t * WR * KP + sl * WBK);
+    const unsigned long long gb = (unsigned long long)(size_t)(G + t * WR * geo.kp + sl * WBK);
     const unsigned long long qb = (unsigned long long)(size_t)(qpad + sl * WBK);
     const int j = wave * 4 + jj;
     unsigned go = goff[jj];
     if (nrem < WR) {  // tail tile: rows past the end re-read the last row (masked later)
-      const unsigned row = go / (KP * 4);
-      go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
+      const unsigned row = go / (geo.kp * 4);
+      go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (geo.kp * 4) + go % (geo.kp * 4);
     }
     glds16s(go, gb, lds_base + (unsigned)((buf * 2 * WSL + j * 256) * 4));
     glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * WSL + WSL + j * 256) * 4));
@@ -189,8 +210,8 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
   f32x16 acc[4];
   for (int64_t it = 0; it < n_it; ++it) {
     const int buf = (int)(it & 1);
-    const int sl = (int)(it % NS);
-    const float* const sAux = smem + 4 * WSL + (int)((it / NS) & 1) * WR;
+    const int sl = geo.slice(it);
+    const float* const sAux = smem + 4 * WSL + (int)(geo.tile(it) & 1) * WR;
 #if EF_WIDE_INTERLEAVE == 0
 #if EF_WIDE_ABL == 3
     if (it + 1 < 2)
@@ -241,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void search_wide_kernel(
 #endif
     }
     if (sl == NS - 1) {
-      const int64_t t = t0 + it / NS;
+      const int64_t t = t0 + geo.tile(it);
       const int tbase = (int)(t * WR);
       const bool tail = (t + 1) * WR > n;
 #pragma unroll
@@ -328,8 +349,9 @@ static_assert(W3R == kWide3RowTile && W3P == kWide3ProbeTile, "plan and kernel t
 template <int KP, int METRIC, bool COLLECT>
 __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
     const float* __restrict__ q3, const float* __restrict__ G3, const float* __restrict__ aux, int64_t n,
-    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
-  constexpr int NS = KP / WBK;
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws, int kp_rt) {
+  const WideGeom<KP> geo(kp_rt);
+  const int NS = geo.ns;
   __shared__ __attribute__((aligned(16))) float smem[4 * W3SL + 2 * W3R];
 
   // one (gallery chunk gc, probe tile pt) work item
@@ -372,8 +394,8 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
     int qrow = slot;
     if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
     const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 7)) * 16);
-    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
-    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (geo.kp * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (geo.kp * 4) + lch16;
   }
   float thr[2] = {-__builtin_inff(), -__builtin_inff()};
   if constexpr (COLLECT) {
@@ -388,18 +410,18 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
   const unsigned lds_base = lds_addr(smem);
   const int64_t n_it = (t1 - t0) * NS;
   auto issue = [&](int64_t it, int buf) {
-    const int64_t t = t0 + it / NS;
-    const int sl = (int)(it % NS);
+    const int64_t t = t0 + geo.tile(it);
+    const int sl = geo.slice(it);
     const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
-    const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * KP + sl * WBK);
+    const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * geo.kp + sl * WBK);
     const unsigned long long qb = (unsigned long long)(size_t)(q3 + sl * WBK);
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int j = wave * 4 + jj;
       unsigned go = goff[jj];
       if (nrem < W3R) {  // tail tile: rows past the end re-read the last row (masked later)
-        const unsigned row = go / (KP * 4);
-        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
+        const unsigned row = go / (geo.kp * 4);
+        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (geo.kp * 4) + go % (geo.kp * 4);
       }
       glds16s(go, gb, lds_base + (unsigned)((buf * 2 * W3SL + j * 256) * 4));
       glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * W3SL + W3SL + j * 256) * 4));
@@ -456,8 +478,8 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
   f32x16 acc[4][2];
   for (int64_t it = 0; it < n_it; ++it) {
     const int buf = (int)(it & 1);
-    const int sl = (int)(it % NS);
-    const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
+    const int sl = geo.slice(it);
+    const float* const sAux = smem + 4 * W3SL + (int)(geo.tile(it) & 1) * W3R + 128 * rh;
 #if EF_WIDE_ABL == 3
     if (it + 1 < 2)  // diagnostic builds only: no slice DMA after the first (results invalid)
 #else
@@ -507,7 +529,7 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
       }
     }
     if (sl == NS - 1) {
-      const int64_t t = t0 + it / NS;
+      const int64_t t = t0 + geo.tile(it);
       const int tbase = (int)(t * W3R) + 128 * rh;
       const bool tail = (t + 1) * W3R > n;
 #pragma unroll
@@ -615,8 +637,9 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
 template <int KP, int METRIC, bool COLLECT>
 __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     const float* __restrict__ q3, const float* __restrict__ G3, const float* __restrict__ aux, int64_t n,
-    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws) {
-  constexpr int NS = KP / WBK;
+    int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws, int kp_rt) {
+  const WideGeom<KP> geo(kp_rt);
+  const int NS = geo.ns;
   __shared__ __attribute__((aligned(16))) float smem[4 * W3SL + 2 * W3R];
 
   auto body = [&](const int gc, const int pt, const int n_amb) {
@@ -658,8 +681,8 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     int qrow = slot;
     if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
     const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 5)) * 16);
-    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (KP * 4) + lch16;
-    qoff[jj] = (unsigned)qrow * (KP * 4) + lch16;
+    goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (geo.kp * 4) + lch16;
+    qoff[jj] = (unsigned)qrow * (geo.kp * 4) + lch16;
   }
   float thr[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
   if constexpr (COLLECT) {
@@ -676,16 +699,16 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
   // DMA piece p (0..7) of slice it into buffer buf: p >> 1 = this wave's piece jj, p & 1 =
   // gallery (0) or probes (1)
   auto issue_piece = [&](int64_t it, int buf, int p) {
-    const int64_t t = t0 + it / NS;
-    const int sl = (int)(it % NS);
+    const int64_t t = t0 + geo.tile(it);
+    const int sl = geo.slice(it);
     const int jj = p >> 1, j = wave * 4 + jj;
     if ((p & 1) == 0) {
       const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
-      const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * KP + sl * WBK);
+      const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * geo.kp + sl * WBK);
       unsigned go = goff[jj];
       if (nrem < W3R) {  // tail tile: rows past the end re-read the last row (masked later)
-        const unsigned row = go / (KP * 4);
-        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (KP * 4) + go % (KP * 4);
+        const unsigned row = go / (geo.kp * 4);
+        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (geo.kp * 4) + go % (geo.kp * 4);
       }
       glds16s(go, gb, lds_base + (unsigned)((buf * 2 * W3SL + j * 256) * 4));
     } else {
@@ -694,8 +717,8 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     }
   };
   auto issue = [&](int64_t it, int buf) {
-    const int64_t t = t0 + it / NS;
-    const int sl = (int)(it % NS);
+    const int64_t t = t0 + geo.tile(it);
+    const int sl = geo.slice(it);
     const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
 #pragma unroll
     for (int p = 0; p < 8; ++p) issue_piece(it, buf, p);
@@ -761,8 +784,8 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
   f32x4 acc[8][4];
   for (int64_t it = 0; it < n_it; ++it) {
     const int buf = (int)(it & 1);
-    const int sl = (int)(it % NS);
-    const float* const sAux = smem + 4 * W3SL + (int)((it / NS) & 1) * W3R + 128 * rh;
+    const int sl = geo.slice(it);
+    const float* const sAux = smem + 4 * W3SL + (int)(geo.tile(it) & 1) * W3R + 128 * rh;
 #if EF_WIDE_ABL == 3
     const bool more = it + 1 < 2;  // diagnostic builds only: no slice DMA after the first (results invalid)
 #else
@@ -811,7 +834,7 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
 #endif
     }
     if (sl == NS - 1) {
-      const int64_t t = t0 + it / NS;
+      const int64_t t = t0 + geo.tile(it);
       const int tbase = (int)(t * W3R) + 128 * rh;
       const bool tail = (t + 1) * W3R > n;
 #pragma unroll
@@ -914,7 +937,7 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
 
 template <int KP, int M>
 static hipError_t wide3_t(hipStream_t s, bool collect, bool w16, const SearchPlan& pl, const float* q3,
-                          const float* G3, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
+                          const float* G3, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws, int kp) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0 || bpad % W3P != 0)
@@ -922,35 +945,41 @@ static hipError_t wide3_t(hipStream_t s, bool collect, bool w16, const SearchPla
   if (w16) {
     if (collect)
       hipLaunchKernelGGL((search_wide16_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux,
-                         n, pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
+                         n, pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws, kp);
     else
       hipLaunchKernelGGL((search_wide16_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
-                         pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+                         pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws, kp);
   } else if (collect) {
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux, n,
-                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
+                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws, kp);
   } else {
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws, kp);
   }
   return hipGetLastError();
 }
 
 template <int KP, int M>
 static hipError_t wide_t(hipStream_t s, bool collect, int s3, const SearchPlan& pl, const float* qpad,
-                         const float* G, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws) {
+                         const float* G, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws, int kp) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(256);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
+  // 32-bit geometry of the kernels: probe rows addressed by unsigned byte offsets, and (KP = 0)
+  // the flattened (tile, slice) counter of a sweep divided in 32 bits
+  const int64_t ns = kp / WBK;
+  if (kp % 128 != 0 || bpad * (int64_t)kp * 4 >= ((int64_t)1 << 31) ||
+      (int64_t)std::max(pl.tiles_per_chunk, pl.c_tpc) * ns >= ((int64_t)1 << 31))
+    return hipErrorInvalidValue;
   // plan from search_plan(.., true); s3 = 1: the 16x16x32 kernel, 2: the 32x32x16 one
-  if (s3) return wide3_t<KP, M>(s, collect, s3 != 2, pl, qpad, G, aux, n, bpad, ws);
+  if (s3) return wide3_t<KP, M>(s, collect, s3 != 2, pl, qpad, G, aux, n, bpad, ws, kp);
   if (collect)
     hipLaunchKernelGGL((search_wide_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G, aux, n,
-                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws);
+                       pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws, kp);
   else
     hipLaunchKernelGGL((search_wide_kernel<KP, M, false>), grid, block, 0, s, qpad, G, aux, n, pl.n_ptiles,
-                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws);
+                       pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws, kp);
   return hipGetLastError();
 }
 
@@ -960,13 +989,15 @@ hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, i
   const bool l2 = metric == EF_METRIC_L2;
   switch (kp) {
     case 256:
-      return l2 ? wide_t<256, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws)
-                : wide_t<256, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws);
+      return l2 ? wide_t<256, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp)
+                : wide_t<256, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp);
     case 512:
-      return l2 ? wide_t<512, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws)
-                : wide_t<512, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws);
-    default:
-      return hipErrorInvalidValue;
+      return l2 ? wide_t<512, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp)
+                : wide_t<512, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp);
+    default:  // k > 512: row length at run time
+      if (kp <= 512) return hipErrorInvalidValue;
+      return l2 ? wide_t<0, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp)
+                : wide_t<0, EF_METRIC_COSINE>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp);
   }
 }
 

@@ -70,6 +70,7 @@ _SIGS = {
     "ef_last_error": ([vp], C.c_char_p),
     "ef_set_stream": ([vp, vp], C.c_int),
     "ef_use_own_stream": ([vp], C.c_int),
+    "ef_get_stream": ([vp, C.POINTER(vp)], C.c_int),
     "ef_synchronize": ([vp], C.c_int),
     "ef_trim": ([vp], C.c_int),
     "ef_fit": ([vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
@@ -145,7 +146,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 4:
+        if h.ef_api_version() != 5:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

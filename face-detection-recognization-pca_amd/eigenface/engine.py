@@ -6,6 +6,7 @@ not mix the two.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import sys
 from dataclasses import dataclass
@@ -144,6 +145,34 @@ class Engine:
     def synchronize(self):
         self._chk(self._lib.ef_synchronize(self._h))
 
+    def stream_handle(self) -> int:
+        """The hipStream_t the engine launches on (0 = the default stream)."""
+        s = C.c_void_p()
+        self._chk(self._lib.ef_get_stream(self._h, C.byref(s)))
+        return int(s.value or 0)
+
+    @contextlib.contextmanager
+    def _torch_order(self, *outs):
+        """Stream order of a call on device tensors when the engine runs on its own stream:
+        the engine's stream first waits for torch's current stream (the inputs' producers),
+        then torch's current stream waits for the engine's (the outputs' consumers), and the
+        output tensors are marked as used on the engine's stream (so the caching allocator
+        does not hand their memory out before the engine's kernels are done).  No host
+        wait either way; a no-op when the engine already runs on torch's stream."""
+        import torch
+        h = self.stream_handle()
+        cur = torch.cuda.current_stream(self.device)
+        if h == cur.cuda_stream:
+            yield
+            return
+        ext = torch.cuda.ExternalStream(h, device=self.device) if h else torch.cuda.default_stream(self.device)
+        ext.wait_stream(cur)
+        yield
+        cur.wait_stream(ext)
+        for t in outs:
+            if t is not None:
+                t.record_stream(ext)
+
     def trim(self):
         """Free the fit workspaces the context keeps between fits (ef_trim)."""
         self._chk(self._lib.ef_trim(self._h))
@@ -241,9 +270,10 @@ class Engine:
         k_out = C.c_int32(0)
         it = C.c_int32(0)
         flags = (N.EF_FIT_STANDARDIZE if standardize else 0) | (N.EF_MEM_DEVICE if dev else 0)
-        self._chk(self._lib.ef_fit_ex(
-            self._h, xp, xdt, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
-            ptr(proj) if proj is not None else None, ptr(tv), C.byref(k_out), C.byref(it)))
+        with (self._torch_order() if dev else contextlib.nullcontext()):
+            self._chk(self._lib.ef_fit_ex(
+                self._h, xp, xdt, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
+                ptr(proj) if proj is not None else None, ptr(tv), C.byref(k_out), C.byref(it)))
         if dev:
             self.synchronize()
         return FitResult(mean, var, scale, comps, eig, proj, float(tv[0]), int(k_out.value), int(it.value))
@@ -260,7 +290,9 @@ class Engine:
             import torch
             mean = torch.empty(d, dtype=torch.float64, device=x.device)
             var = torch.empty(d, dtype=torch.float64, device=x.device)
-            self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, N.EF_MEM_DEVICE, mean.data_ptr(), var.data_ptr()))
+            with self._torch_order(mean, var):
+                self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, N.EF_MEM_DEVICE, mean.data_ptr(),
+                                                var.data_ptr()))
             self.synchronize()
             return mean, var
         mean, var = np.empty(d), np.empty(d)
@@ -323,7 +355,8 @@ class Engine:
             if out is None:
                 out = torch.empty((b, self.model_k), dtype=torch.float32, device=p.device)
             self._dev_out(out, (b, self.model_k), torch.float32, "out")
-            self._chk(self._lib.ef_project(self._h, pp, dtype, b, out.data_ptr(), N.EF_MEM_DEVICE))
+            with self._torch_order(out):
+                self._chk(self._lib.ef_project(self._h, pp, dtype, b, out.data_ptr(), N.EF_MEM_DEVICE))
             return out
         p = np.asarray(P)
         dtype = N.EF_U8 if p.dtype == np.uint8 else N.EF_F32
@@ -366,7 +399,8 @@ class Engine:
             if keys is None:
                 keys = torch.empty(b, dtype=torch.int64, device=q.device)
             self._dev_out(keys, (b,), torch.int64, "keys")
-            self._chk(self._lib.ef_search(self._h, qp, b, mt, keys.data_ptr(), N.EF_MEM_DEVICE))
+            with self._torch_order(keys):
+                self._chk(self._lib.ef_search(self._h, qp, b, mt, keys.data_ptr(), N.EF_MEM_DEVICE))
             return keys
         q, qp = _host(Q, np.float32)
         if q.ndim != 2 or q.shape[1] != self.gallery_k:
@@ -398,7 +432,8 @@ class Engine:
             fp = None
             if feats is not None:
                 fp = self._dev_out(feats, (b, self.model_k), torch.float32, "feats").data_ptr()
-            self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, keys.data_ptr(), fp, N.EF_MEM_DEVICE))
+            with self._torch_order(keys, feats):
+                self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, keys.data_ptr(), fp, N.EF_MEM_DEVICE))
             return keys
         p = np.asarray(P)
         dtype = N.EF_U8 if p.dtype == np.uint8 else N.EF_F32
@@ -444,11 +479,12 @@ class Engine:
             if out is None:
                 out = torch.empty((b, 3), dtype=torch.int64, device=x.device)
             self._dev_out(out, (b, 3), torch.int64, "out")
-            if search:
-                self._chk(self._lib.ef_search_matches(self._h, xp, b, mt, out.data_ptr(), N.EF_MEM_DEVICE))
-            else:
-                self._chk(self._lib.ef_recognize_matches(self._h, xp, dtype, b, mt, out.data_ptr(), None,
-                                                         N.EF_MEM_DEVICE))
+            with self._torch_order(out):
+                if search:
+                    self._chk(self._lib.ef_search_matches(self._h, xp, b, mt, out.data_ptr(), N.EF_MEM_DEVICE))
+                else:
+                    self._chk(self._lib.ef_recognize_matches(self._h, xp, dtype, b, mt, out.data_ptr(), None,
+                                                             N.EF_MEM_DEVICE))
             return out
         if search:
             x, xp = _host(X, np.float32)
@@ -489,8 +525,9 @@ class Engine:
                   and keys.device == parts.device):
             raise ValueError(f"keys must be a contiguous int64 tensor of shape ({b},) on {parts.device}")
         if b:
-            self._chk(self._lib.ef_matches_merge(self._h, parts.data_ptr(), nparts, b, keys.data_ptr(), None,
-                                                 N.EF_MEM_DEVICE))
+            with self._torch_order(keys):
+                self._chk(self._lib.ef_matches_merge(self._h, parts.data_ptr(), nparts, b, keys.data_ptr(), None,
+                                                     N.EF_MEM_DEVICE))
         return keys
 
     def recognize(self, P, metric="l2", return_features=False):
@@ -533,9 +570,10 @@ class Engine:
         if out is not None:  # device output: stage the pixels on the device too
             import torch
             dbuf = torch.from_numpy(buf).to(out.device)
-            self._chk(self._lib.ef_preprocess(self._h, dbuf.data_ptr(), offs.ctypes.data, hs.ctypes.data,
-                                              ws.ctypes.data, cs.ctypes.data, n, oh, ow, out.data_ptr(),
-                                              flags | N.EF_MEM_DEVICE))
+            with self._torch_order(out, dbuf):
+                self._chk(self._lib.ef_preprocess(self._h, dbuf.data_ptr(), offs.ctypes.data, hs.ctypes.data,
+                                                  ws.ctypes.data, cs.ctypes.data, n, oh, ow, out.data_ptr(),
+                                                  flags | N.EF_MEM_DEVICE))
             return out
         res = np.empty((n, oh * ow), np.uint8)
         self._chk(self._lib.ef_preprocess(self._h, buf.ctypes.data, offs.ctypes.data, hs.ctypes.data,
@@ -575,10 +613,10 @@ class Engine:
         """Fused GPU decode + grey + INTER_LINEAR resize of JPEG files
         (ef_jpeg_ingest): (rows uint8 (n, h*w) — or device tensor ``out`` filled —,
         status int32 (n,)).  Rows of files with status != 0 are zero.  With ``out`` the
-        call returns once the decode is queued on the engine's stream (status is final):
-        synchronise (``synchronize()``, or run the engine on torch's stream) before
-        reading ``out``; back-to-back calls overlap one batch's host staging with the
-        previous batch's decode."""
+        call returns once the decode is queued on the engine's stream (status is final);
+        torch's current stream is ordered after it (no host wait), so torch work on ``out``
+        queued afterwards sees the decoded rows, and back-to-back calls overlap one batch's
+        host staging with the previous batch's decode."""
         m = _jpeg_mode(mode)
         ow, oh = int(size[0]), int(size[1])
         n = len(blobs)
@@ -590,8 +628,9 @@ class Engine:
             import torch
             o, op = _dev(out, torch.uint8)
             self._dev_out(o, (n, oh * ow), torch.uint8, "out")
-            self._chk(self._lib.ef_jpeg_ingest(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,
-                                               oh, ow, op, st.ctypes.data, N.EF_MEM_DEVICE))
+            with self._torch_order(o):
+                self._chk(self._lib.ef_jpeg_ingest(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,
+                                                   oh, ow, op, st.ctypes.data, N.EF_MEM_DEVICE))
             return out, st
         rows = np.empty((n, oh * ow), np.uint8)
         self._chk(self._lib.ef_jpeg_ingest(self._h, data, offs.ctypes.data, sizes.ctypes.data, n, m,

@@ -82,7 +82,7 @@ class ManualPCA:
         if self._folded is None:
             self._folded = (np.ascontiguousarray(self.mean_, dtype=np.float32),
                             np.ascontiguousarray(self.components_.T, dtype=np.float32))
-        eng = _model_engine(self._folded[0], self._folded[1], self.device)
+        eng = _model_engine(self._folded[0], self._folded[1], self.device, "manual")
         x = np.asarray(X)
         x = x if x.dtype == np.uint8 else np.asarray(x, dtype=np.float32)
         return eng.project(np.atleast_2d(x)).astype(np.float64)
@@ -98,7 +98,7 @@ def project_face_to_eigenspace(face_vector, eigenfaces, mean_face, device=0):
     a batch (b, d) -> (b, k), float64; computed by the GPU projection (fp32 MFMA)."""
     ef = np.asarray(eigenfaces)
     mu = np.asarray(mean_face)
-    eng = _model_engine(mu, ef, device)
+    eng = _model_engine(mu, ef, device, "manual")
     v = np.asarray(face_vector)
     p = v if v.dtype == np.uint8 else np.asarray(v, dtype=np.float32)
     f = eng.project(np.atleast_2d(p)).astype(np.float64)
@@ -107,8 +107,11 @@ def project_face_to_eigenspace(face_vector, eigenfaces, mean_face, device=0):
 
 def cosine_similarity(vec1, vec2, device=0):
     """useless/scan.py:58-78: ``vec1 . vec2 / (|vec1| |vec2|)``, 0.0 when either norm is
-    0.  The product is scored by the GPU search (a one-row gallery; the match record's
-    score is the fp64 similarity of the fp32 inputs)."""
+    0, for vectors of any length up to 65536.  The product is scored by the GPU search (a
+    one-row gallery; the match record's score is the fp64 similarity of the fp32 inputs),
+    on the helpers' own engine, so it never evicts a resident recognition gallery.  One
+    call is one GPU round trip: to score a face against a whole gallery (the loop of
+    useless/scan.py:122-124) call ``recognize_faces`` / ``Engine.search`` once instead."""
     a = np.asarray(vec1, dtype=np.float64).ravel()
     b = np.asarray(vec2, dtype=np.float64).ravel()
     if a.shape != b.shape:
@@ -116,6 +119,6 @@ def cosine_similarity(vec1, vec2, device=0):
     if np.linalg.norm(a) == 0 or np.linalg.norm(b) == 0:  # :70-74
         return 0.0
     g = np.ascontiguousarray(b[None, :], dtype=np.float32)
-    eng = _gallery_engine(g, device)
+    eng = _gallery_engine(g, device, "manual")
     m = eng.search_matches(np.ascontiguousarray(a[None, :], dtype=np.float32), "cosine")
     return float(-m["score"][0])

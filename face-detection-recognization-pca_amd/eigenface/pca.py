@@ -18,17 +18,20 @@ import numpy as np
 
 from .engine import Engine
 
-_engines: dict[int, Engine] = {}
+_engines: dict[tuple[int, str], Engine] = {}
 _elock = threading.Lock()
 
 
-def get_engine(device: int = 0) -> Engine:
-    """Process-wide Engine for a device (created on first use)."""
+def get_engine(device: int = 0, pool: str = "shared") -> Engine:
+    """Process-wide Engine for a device (created on first use).  ``pool`` names separate
+    engines on one device: the manual helpers (``eigenface.manual``) keep their one-off
+    models and one-row galleries on their own engine, so they never evict the model and
+    gallery that the recognise functions keep resident on the shared one."""
     with _elock:
-        e = _engines.get(device)
+        e = _engines.get((device, pool))
         if e is None:
             e = Engine(device)
-            _engines[device] = e
+            _engines[(device, pool)] = e
         return e
 
 
@@ -187,14 +190,11 @@ def manual_pca(data_matrix, n_components=None, device=0):
 # ------------------------------------------------------------------ recognize
 class _ArrayToken:
     """Owner token of an uploaded host array: the array itself (kept alive, so its id
-    cannot be reused), its data pointer, shape and dtype, plus a digest of its bytes (so
-    in-place edits re-upload).  The digest covers every byte of arrays up to
-    FULL_DIGEST_BYTES (≈1 ms); above that it covers a strided sample of ~1 MiB of rows
-    plus the first and last row, so a per-call check of a 1M-row gallery costs
-    microseconds instead of a full hash.  After editing a large array in place outside
-    that sample, call :func:`invalidate_uploads`."""
-
-    FULL_DIGEST_BYTES = 16 << 20
+    cannot be reused), its data pointer, shape and dtype, plus a digest of ALL its bytes,
+    so an in-place edit anywhere (re-enrolling one person's row of a large gallery) makes
+    the next call re-upload — the reference reads the array it is given on every call.
+    The digest is xxh3-128 (~20 GB/s on one host core: a 1M x 128 fp32 gallery costs
+    ~25 ms, half of what its re-upload over PCIe would), blake2b where xxhash is absent."""
 
     def __init__(self, a):
         self.a = a
@@ -207,30 +207,34 @@ class _ArrayToken:
                 and a.__array_interface__["data"][0] == self.ptr and _digest(a) == self.digest)
 
 
+try:
+    import xxhash as _xxhash
+except ImportError:  # pragma: no cover - the image ships xxhash
+    _xxhash = None
+
+
 def _digest(a):
+    b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    if _xxhash is not None:
+        return _xxhash.xxh3_128_digest(b)
     import hashlib
-    a = np.asarray(a)
-    if a.nbytes > _ArrayToken.FULL_DIGEST_BYTES and a.ndim >= 1 and a.shape[0] > 2:
-        rows = a.shape[0]
-        row_bytes = max(1, a.nbytes // rows)
-        step = max(1, rows * row_bytes // (1 << 20))
-        a = np.concatenate([a[::step], a[-1:]])
-    return hashlib.blake2b(np.ascontiguousarray(a).view(np.uint8), digest_size=16).digest()
+    return hashlib.blake2b(b, digest_size=16).digest()
 
 
 def invalidate_uploads(device: int = 0):
-    """Forget which host arrays the device's resident model and gallery came from: the
-    next recognise call re-uploads them (needed only after an in-place edit of a large
-    array that the sampled digest of :class:`_ArrayToken` may miss)."""
-    eng = get_engine(device)
-    eng.model_owner = None
-    eng.gallery_owner = None
+    """Forget which host arrays the device's resident models and galleries came from: the
+    next recognise call re-uploads them (the digest already catches in-place edits; this
+    is for arrays changed behind numpy's back, e.g. by a foreign buffer writer)."""
+    for (dev, _pool), eng in list(_engines.items()):
+        if dev == device:
+            eng.model_owner = None
+            eng.gallery_owner = None
 
 
-def _gallery_engine(features, device):
+def _gallery_engine(features, device, pool="shared"):
     """Engine whose resident gallery holds ``features`` (uploaded when the engine's owner
     token is not this array's token)."""
-    eng = get_engine(device)
+    eng = get_engine(device, pool)
     a = features if isinstance(features, np.ndarray) else np.asarray(features)
     tok = eng.gallery_owner
     if not (isinstance(tok, _ArrayToken) and tok.matches(a)):
@@ -238,9 +242,9 @@ def _gallery_engine(features, device):
     return eng
 
 
-def _model_engine(mean, W, device):
+def _model_engine(mean, W, device, pool="shared"):
     """Engine whose resident model is (mean, W) (same owner-token rule)."""
-    eng = get_engine(device)
+    eng = get_engine(device, pool)
     tok = eng.model_owner
     if not (isinstance(tok, tuple) and len(tok) == 2 and tok[0].matches(mean) and tok[1].matches(W)):
         eng.set_model(np.asarray(mean, dtype=np.float32), np.asarray(W, dtype=np.float32),

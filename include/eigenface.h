@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 4
+#define EF_API_VERSION 5
 
 /* status codes */
 #define EF_OK 0
@@ -79,6 +79,10 @@ const char* ef_last_error(const ef_ctx* ctx);
  * non-blocking stream (the default after ef_create). */
 int ef_set_stream(ef_ctx* ctx, void* hip_stream);
 int ef_use_own_stream(ef_ctx* ctx);
+/* The hipStream_t the ctx launches on now (*out; NULL = the default stream): lets a caller
+ * order its own stream after an asynchronous EF_MEM_DEVICE call (hipStreamWaitEvent, or
+ * torch.cuda.ExternalStream + wait_stream). */
+int ef_get_stream(const ef_ctx* ctx, void** out);
 int ef_synchronize(ef_ctx* ctx);
 /* ef_fit keeps its device workspaces (operand copies, covariance, subspace blocks) in
  * the context between calls, so repeated fits do not pay hipMalloc/hipFree; ef_trim
@@ -130,7 +134,9 @@ int ef_colstats(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t 
 /* --------------------------------------------------------------- projection
  * Recognition model f = (p - mean) . W  (useless/scan.py:93-96; sklearn
  * scaler.transform + pca.transform folded, scan-template-v4.py:265-266).
- * mean[d], W[d*k] float32, row-major (d rows of k), k <= 512.  Kept resident.
+ * mean[d], W[d*k] float32, row-major (d rows of k), 1 <= k <= 65536 (k > 512 is padded
+ * to a multiple of 128: the full-rank per-person models of train-v5.py:539-545).  Kept
+ * resident.
  * EF_MODEL_BF16: f = (p - round(mean)).bf16(W) - (mean - round(mean)).W with
  * fp32 accumulation (exact bf16 inputs for uint8 pixels; only W is rounded). */
 int ef_model_set(ef_ctx* ctx, const float* mean, const float* W, int64_t d, int32_t k, uint32_t flags);
@@ -138,7 +144,8 @@ int ef_model_set(ef_ctx* ctx, const float* mean, const float* W, int64_t d, int3
 int ef_project(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, float* F, uint32_t flags);
 
 /* ------------------------------------------------------------------ search
- * Gallery rows G[n*k] float32 (face_features / projected_data), kept resident.
+ * Gallery rows G[n*k] float32 (face_features / projected_data), kept resident; any
+ * 1 <= k <= 65536 (as ef_model_set).
  * global_offset is added to every returned index (row sharding across ranks). */
 int ef_gallery_set(ef_ctx* ctx, const float* G, int64_t n, int32_t k, int64_t global_offset,
                    uint32_t flags);

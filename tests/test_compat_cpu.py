@@ -77,3 +77,24 @@ def test_gallery_cache_roundtrip(tmp_path):
     import pytest
     with pytest.raises(ValueError):
         load_gallery_cache(tmp_path / "bad.npy")
+
+
+def test_upload_token_sees_any_inplace_edit():
+    """The owner token of an uploaded gallery digests every byte: editing one row of a
+    large gallery in place (re-enrolling a person) is seen, wherever the row is, so the
+    next recognise call re-uploads instead of searching a stale device copy (the
+    reference reads the array it is given on every call)."""
+    from eigenface.pca import _ArrayToken
+    rng = np.random.default_rng(0)
+    g = rng.standard_normal((200_000, 32)).astype(np.float32)  # 25.6 MB
+    tok = _ArrayToken(g)
+    assert tok.matches(g)
+    for row in (0, 1, 12_345, 99_999, 199_999):
+        old = g[row].copy()
+        g[row, 7] += 1.0
+        assert not tok.matches(g), row
+        g[row] = old
+        assert tok.matches(g)
+    assert not tok.matches(g.copy())  # another array with the same bytes is another owner
+    import eigenface
+    assert callable(eigenface.invalidate_uploads)

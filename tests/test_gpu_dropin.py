@@ -123,3 +123,56 @@ def test_train_v5_dropin_full_rank_vs_oracle(tmp_path):
         np.testing.assert_allclose(C[:n - 1][gap], ref["pca"]["components_"][:n - 1][gap], atol=1e-7)
         F = md["face_features"]
         assert np.abs(F[:, -1]).max() < 1e-6 * np.abs(F).max()
+
+
+def test_train_v5_601_faces_recognised_at_full_rank(tmp_path, monkeypatch):
+    """The reference's own faces/lock_version/shun holds 601 crops, so train-v5.py
+    (n_components = face count, train-v5.py:539-545) writes a k = 601 model.  Recognition
+    against it (scan-template-v4.py:265-287, batched as recognize_faces_all_models) runs the
+    k > 512 projection and cosine search and returns the oracle's first-argmax identities."""
+    root = str(tmp_path)
+    n = 601
+    xs = _write_person(root, "shun", n, 21, size=(64, 64))
+    r = _run("train-v5.py", root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Successful trainings: 1" in r.stdout
+    base = tmp_path / "faces" / "lock_version" / "shun"
+    md = pickle.load(open(base / "face_model.pkl", "rb"))
+    assert md["n_components"] == n and md["face_features"].shape == (n, n)
+    from eigenface.compat import load_all_models, recognize_faces_all_models
+    monkeypatch.chdir(root)
+    models = load_all_models(".")
+    assert list(models) == ["shun"]
+    # probes: 40 training crops (their own rows must win) + 24 unseen faces of the same kind
+    unseen, _ = orc.synth_faces(24, 64, r=32, seed=99)
+    pick = np.arange(0, n, 15)[:40]
+    probes = np.concatenate([xs[pick], unseen])
+    res = recognize_faces_all_models([p.reshape(64, 64) for p in probes], models, 0.8)
+    assert len(res) == len(probes)
+    # oracle: sklearn transform of the pickled estimators in fp64, cosine first-argmax vs the
+    # pickled training features, threshold >= (scan-template-v4.py:265-287)
+    sc, pca = md["scaler"], md["pca"]
+    f = orc.sklearn_transform(probes, (sc.mean_, sc.var_, sc.scale_),
+                              {"components_": pca.components_, "mean_": pca.mean_})
+    s = orc.cosine_scores(f, md["face_features"])
+    ref_idx = np.argmax(s, axis=1)
+    srt = np.sort(s, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-5
+    assert clear[:40].all()
+    for j, (pid, name, conf) in enumerate(res):
+        assert abs(conf - s[j, ref_idx[j]]) < 1e-5
+        if not clear[j]:
+            continue
+        if s[j, ref_idx[j]] >= 0.8:
+            assert pid == md["face_labels"][ref_idx[j]] and name == "shun"
+        else:
+            assert pid == -1 and name == "shun"  # below threshold: the model's person name
+    # the training crops are recognised as themselves (labels are all shun's id)
+    assert all(res[j][1] == "shun" and res[j][2] > 0.999 for j in range(40))
+    # and the engine's own argmax row for them is the crop's own training row
+    from eigenface.compat import extract_faces_features
+    from eigenface.pca import _gallery_engine
+    feats = extract_faces_features(probes[:40], md)
+    idx, _ = _gallery_engine(md["face_features"], 0).search(feats.astype(np.float32), "cosine")
+    np.testing.assert_array_equal(idx, ref_idx[:40])
+    np.testing.assert_array_equal(idx, pick)

@@ -282,3 +282,33 @@ def _c3_probe_matrices(d):
     r = np.random.default_rng([5]).integers(0, 2, size=(d, 8)).astype(np.float64) * 2.0 - 1.0
     px = np.sort(np.random.default_rng([6]).choice(d, size=256, replace=False))
     return r, px
+
+
+def test_fused_column_stats_exact_beyond_32bit_quarters():
+    """transpose_stats_lds_kernel (d % 256 == 0, covariance path): a workgroup covers
+    nkb / 128 blocks of 64 samples; past ~1060 blocks the four sample quarters' Σx² of one
+    pixel exceed 2^32 together (near-255 pixels), so they are added in 64 bits.  n = 9M
+    samples (1100 blocks per workgroup) vs exact integer sums: StandardScaler mean and var
+    (train-v4.py:131) to the last bits."""
+    import torch
+    from eigenface import get_engine
+    n, d = 9_000_000, 256
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(249, 256, (n, d), dtype=torch.uint8, device="cuda", generator=g)
+    s1 = torch.zeros(d, dtype=torch.int64, device="cuda")
+    s2 = torch.zeros(d, dtype=torch.int64, device="cuda")
+    for i in range(0, n, 1 << 20):
+        c = x[i:i + (1 << 20)].to(torch.int64)
+        s1 += c.sum(0)
+        s2 += (c * c).sum(0)
+    s1, s2 = [int(v) for v in s1.cpu()], [int(v) for v in s2.cpu()]
+    assert max(s2) // 128 > (1 << 32)  # one workgroup's share of Σx² needs 64 bits
+    r = get_engine(0).fit(x, 100, standardize=True, projection=False)  # k > 80: direct Jacobi
+    mean, var = r.mean.cpu().numpy(), r.var.cpu().numpy()
+    from fractions import Fraction
+    m_ref = np.array([float(Fraction(a, n)) for a in s1])
+    v_ref = np.array([float(Fraction(n * b - a * a, n * n)) for a, b in zip(s1, s2)])
+    np.testing.assert_allclose(mean, m_ref, rtol=1e-15)
+    np.testing.assert_allclose(var, v_ref, rtol=1e-12)
+    del x
+    torch.cuda.empty_cache()

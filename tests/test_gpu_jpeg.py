@@ -179,6 +179,29 @@ def test_back_to_back_device_ingests(eng):
                                       io_oracle.preprocess(J.decode_ref(batches[1][i], "bgr"), (32, 32)))
 
 
+def test_device_ingest_ordered_on_torch_stream(eng):
+    """A device-output ingest on the engine's own stream orders torch's current stream
+    after the decode (event wait, no host sync): torch work queued after the call — a
+    clone, and a reduction read after only a stream-level synchronize — sees the decoded
+    rows, and the output's memory is not reused while the decode still writes it."""
+    import torch
+    eng.use_own_stream()
+    blobs = [J.encode(J.smooth_image(60 + k % 50, 70 + k % 40, 3, 500 + k), quality=80, subsampling=k % 3)
+             for k in range(900)]
+    ref, ref_st = eng.ingest_jpegs(blobs, (32, 32), "bgr")
+    out = torch.empty((len(blobs), 32 * 32), dtype=torch.uint8, device="cuda")
+    st = eng.ingest_jpegs(blobs, (32, 32), "bgr", out=out)[1]
+    copy = out.clone()                      # queued on torch's stream right after the call
+    total = out.to(torch.int64).sum()
+    del out                                 # its block may be reused only after the decode
+    junk = torch.full((len(blobs), 32 * 32), 7, dtype=torch.uint8, device="cuda")
+    torch.cuda.current_stream().synchronize()
+    np.testing.assert_array_equal(st, ref_st)
+    np.testing.assert_array_equal(copy.cpu().numpy(), ref)
+    assert int(total) == int(ref.astype(np.int64).sum())
+    assert int(junk.sum()) == 7 * junk.numel()
+
+
 def test_ingest_wide_sources_read_planes_directly(eng):
     """Sources whose band of rows exceeds the fused resize's LDS budget (large frames) take its
     direct-read path; small ones in the same call the LDS-staged path — both equal libjpeg's

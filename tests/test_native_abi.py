@@ -61,7 +61,7 @@ def test_one_hip_runtime_per_process():
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
-    assert lib.ef_api_version() == 4
+    assert lib.ef_api_version() == 5
     n = ctypes.c_int(-1)
     assert lib.ef_device_count(ctypes.byref(n)) == 0
     if n.value == 0:  # build container: creating a context must fail cleanly, not crash
