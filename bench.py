@@ -56,28 +56,44 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(P, mean, W, G, targets, budget_s):
-    """Oracle fp32 BLAS restatement on the host cores, bounded sample."""
+def _thread_env():
+    return {v: os.environ.get(v) for v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS")}
+
+
+def cpu_baseline(P, mean, W, G, targets, budget_s, warmups=2, repeats=5):
+    """Oracle fp32 BLAS restatement on the host cores, bounded sample, timed to BASELINE.md's
+    protocol: the same probe sample `warmups` times untimed, then the median of `repeats`
+    timed runs; the BLAS thread count in use and the thread variables are recorded."""
     sys.path.insert(0, ROOT)
     from oracle import eigenface_oracle as orc
     cores = _blas_threads()
     gn = np.einsum("ij,ij->i", G, G)
-    # calibrate on 32 probes, then size the sample for ~budget_s
+    # calibrate on 32 probes, then size the sample so warm-ups + repeats fit in ~budget_s
     t = time.perf_counter()
     orc.recognize_l2_f32(P[:32], mean, W, G, gn)
     per = (time.perf_counter() - t) / 32
-    b = int(min(len(P), max(32, budget_s / max(per, 1e-9))))
+    b = int(min(len(P), max(32, budget_s / (warmups + repeats) / max(per, 1e-9))))
     b = max(32, (b // 32) * 32)
-    t = time.perf_counter()
-    idx, _ = orc.recognize_l2_f32(P[:b], mean, W, G, gn)
-    dt = time.perf_counter() - t
+    for _ in range(warmups):
+        orc.recognize_l2_f32(P[:b], mean, W, G, gn)
+    times = []
+    for _ in range(repeats):
+        t = time.perf_counter()
+        idx, _ = orc.recognize_l2_f32(P[:b], mean, W, G, gn)
+        times.append(time.perf_counter() - t)
+    dt = float(np.median(times))
     return {
         "value": b / dt,
         "unit": "faces/s",
         "cores": int(cores),
         "kind": "port",
         "sample": f"{b} probes x full {len(G)}-row gallery, fp32 NumPy/OpenBLAS "
-                  f"(oracle.recognize_l2_f32), {dt:.1f} s",
+                  f"(oracle.recognize_l2_f32), median of {repeats} runs after {warmups} warm-ups, "
+                  f"{dt:.2f} s each",
+        "warmups": warmups,
+        "repeats": [round(b / x, 2) for x in times],
+        "thread_env": _thread_env(),
+        "host_cpus": os.cpu_count(),
         "match": float((idx == targets[:b]).mean()),
     }
 
@@ -113,6 +129,123 @@ def reference_pattern(P, mean, W, G64, m, budget_s):
     return {"value": round(done / dt, 3), "unit": "faces/s", "cores": _blas_threads(), "kind": "port",
             "sample": f"{done} probes, one sklearn scaler/pca.transform + cosine_similarity + argmax each "
                       f"against the full {len(G64)}-row float64 gallery (scan-template-v4.py:253-287)"}
+
+
+def scan_roofline(split, avg_ms, bsz, rows, k, split_opt=1):
+    """Roofline of one gallery-scan launch.  fp32 scan: algorithmic 2 B N k flop against the
+    fp32 MFMA peak; split-bf16 scan: its MFMA work (3 bf16 products per fp32 product, at
+    the padded k) against the dense bf16 peak, plus the power-limited ceiling of a bare
+    LDS-fed loop of the same MFMA shape."""
+    flops_launch = 2.0 * bsz * rows * k
+    kpad = next(p for p in (16, 32, 64, 128, 256, 512) if p >= k) if k <= 512 else (k + 127) // 128 * 128
+    if split:
+        mflops = 3.0 * 2.0 * bsz * rows * kpad
+        a = mflops / (avg_ms * 1e-3) / 1e12
+        shape16 = split_opt != 2 and k > 64
+        kname = ("search16_kernel" if shape16 else "search_kernel<S3>") if k <= 128 else \
+            ("search_wide16_kernel" if shape16 else "search_wide3_kernel")
+        rec = {"bound": "mfma", "kernel": kname + " (split-bf16: 3 x bf16 MFMA per fp32 "
+               "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
+               "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
+               "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
+               "algorithmic_flops_per_launch": flops_launch,
+               "algorithmic_TFLOPs": round(flops_launch / (avg_ms * 1e-3) / 1e12, 2)}
+        ceil = bf16_ceiling("16x16x32 lds" if shape16 else "32x32x16 lds")
+        if ceil:
+            rec["power_limited_ceiling_TFLOPs"] = ceil[0]
+            rec["frac_of_power_limited_ceiling"] = round(a / ceil[0], 4)
+            rec["ceiling_source"] = ceil[1]
+        return rec
+    a = flops_launch / (avg_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
+            + " (fp32 MFMA distance GEMM + fused arg-best)", "achieved": round(a, 2),
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_FP32_TFLOPS, 4),
+            "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops_launch}
+
+
+def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cpu_budget: float,
+             split_opt: int = 1):
+    """BASELINE.json configs[4] on one GPU, as a sub-record of the default run: 1M-row
+    gallery, 256x256 uint8 probes, k = 512, bf16 projection, fp32-accumulated distances (the
+    split-bf16 scan: bf16 MFMA products, fp32 accumulation, fp64-resolved identities); the
+    fp32 scan on the same step as a side leg whose keys must be identical; the bf16
+    projection's tolerance vs fp32; planted-match check; the CPU fp32 restatement."""
+    import torch
+    from eigenface import decode_keys, synth
+    n, side, k, bsz, precision = CONFIGS["c5"]
+    d = side * side
+    t_setup = time.perf_counter()
+    B = synth.basis(d, k, 0)
+    mean = synth.mean_face(side).astype(np.float32)
+    W = B.astype(np.float32)
+    G = synth.gallery_rows(0, n, k)
+    targets = np.random.default_rng(2024).integers(0, n, bsz)
+    P = synth.probes(targets, n, k, side, B=B)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    eng.set_model(mean, W, precision=precision)
+    eng.set_gallery(G)
+    P_dev = torch.from_numpy(P).to(dev)
+    keys = {o: torch.empty(bsz, dtype=torch.int64, device=dev) for o in (split_opt, 0)}
+    torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+    legs = {}
+    for opt in (split_opt, 0):  # headline: split-bf16 scan; side leg: fp32 scan
+        eng.set_option("search_split_bf16", opt)
+        for _ in range(warmup):
+            eng.recognize_keys(P_dev, "l2", keys=keys[opt])
+        eng.timing(True)
+        eng.timing_reset()
+        reps = []
+        for _ in range(max(1, repeats)):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                eng.recognize_keys(P_dev, "l2", keys=keys[opt])
+            torch.cuda.synchronize(dev)
+            reps.append(time.perf_counter() - t0)
+        eng.timing(False)
+        s_ms, s_n = eng.timing_get("search")
+        legs[opt] = (reps, s_ms / max(s_n, 1), s_n)
+    eng.set_option("search_split_bf16", 0)
+    reps, s_avg, s_n = legs[split_opt]
+    el = float(np.median(reps))
+    idx, _ = decode_keys(keys[split_opt].cpu().numpy(), "l2")
+    traffic, traffic_src = pmc_traffic("c5s3")
+    out = {"config": f"C5: gallery {n} x k={k}, {side}x{side} uint8 faces, probe batch {bsz}, metric l2, "
+                     "bf16 projection, split-bf16 distance scan (fp32 accumulate, fp64-resolved)",
+           "value": round(bsz * steps / el, 1), "unit": "faces/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(el / steps * 1e3, 4),
+           "repeats_ms_per_step": [round(r / steps * 1e3, 4) for r in reps],
+           "roofline": dict(scan_roofline(True, s_avg, bsz, n, k, split_opt), traffic=traffic,
+                            traffic_source=traffic_src, launches=s_n),
+           "setup_s": round(setup_s, 1)}
+    reps32, s32_avg, s32_n = legs[0]
+    el32 = float(np.median(reps32))
+    traffic32, src32 = pmc_traffic("c5")
+    out["scan_fp32"] = {"value": round(bsz * steps / el32, 1), "unit": "faces/s",
+                        "ms_per_step": round(el32 / steps * 1e3, 4),
+                        "keys_identical_to_headline": bool(torch.equal(keys[0], keys[split_opt])),
+                        "roofline": dict(scan_roofline(False, s32_avg, bsz, n, k), traffic=traffic32,
+                                         traffic_source=src32, launches=s32_n)}
+    # bf16 projection vs fp32 projection on the same step (SURVEY 8(d) C5 tolerance)
+    f16 = torch.empty((bsz, k), dtype=torch.float32, device=dev)
+    f32 = torch.empty_like(f16)
+    k16 = eng.recognize_keys(P_dev, "l2", feats=f16).clone()
+    eng.set_model(mean, W, precision="fp32")
+    k32 = eng.recognize_keys(P_dev, "l2", feats=f32).clone()
+    torch.cuda.synchronize(dev)
+    out["bf16_projection_tolerance"] = {
+        "features_max_rel_err_l2": ((f16 - f32).norm(dim=1) / f32.norm(dim=1).clamp_min(1e-30)).max().item(),
+        "argmin_agreement_bf16_vs_fp32_projection": float(((k16 & 0xFFFFFFFF) == (k32 & 0xFFFFFFFF))
+                                                          .float().mean().item()),
+        "stated_bound": "|f_bf16 - f_fp32| <= 2^-8 sum|p - round(mu)||W| per feature (tests/test_gpu_project.py)"}
+    out["check"] = {"planted_match": float((idx == targets).mean())}
+    if with_cpu:
+        out["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, cpu_budget)
+        out["cpu_baseline"]["speedup"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    eng.use_own_stream()
+    return out
 
 
 def c2_bench(eng, with_cpu: bool, steps=20, repeats=5, cpu_budget=6.0):
@@ -619,6 +752,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary fit timing")
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 recognition line")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 sub-record of the default run")
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
     ap.add_argument("--gallery", type=int, default=0, help="override the gallery size (per-rank studies)")
     ap.add_argument("--search", default=None, choices=["fp32", "split_bf16"],
@@ -793,37 +927,10 @@ def main():
         ms_step = el / args.steps * 1e3
         value = bsz * args.steps / el
         search_avg_ms = s_ms / max(s_n, 1)
-        flops_launch = 2.0 * bsz * (hi - lo) * k  # algorithmic: 2 k N per face x B faces
 
         def roof(split, avg_ms):
-            # fp32 scan: priced against the fp32 MFMA peak; split-bf16 scan: its MFMA work
-            # (3 bf16 products per fp32 product, at the padded k) against the dense bf16 peak
-            if split:
-                mflops = 3.0 * 2.0 * bsz * (hi - lo) * kpad
-                a = mflops / (avg_ms * 1e-3) / 1e12
-                shape16 = args.split_opt != 2 and k > 64
-                kname = ("search16_kernel" if shape16 else "search_kernel<S3>") if k <= 128 else \
-                    ("search_wide16_kernel" if shape16 else "search_wide3_kernel")
-                rec = {"bound": "mfma", "kernel": kname + " (split-bf16: 3 x bf16 MFMA per fp32 "
-                       "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
-                       "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
-                       "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
-                       "algorithmic_flops_per_launch": flops_launch,
-                       "algorithmic_TFLOPs": round(flops_launch / (avg_ms * 1e-3) / 1e12, 2)}
-                ceil = bf16_ceiling("16x16x32 lds" if shape16 else "32x32x16 lds")
-                if ceil:  # the power-limited rate of a bare LDS-fed loop of the same MFMA shape
-                    rec["power_limited_ceiling_TFLOPs"] = ceil[0]
-                    rec["frac_of_power_limited_ceiling"] = round(a / ceil[0], 4)
-                    rec["ceiling_source"] = ceil[1]
-                return rec
-            a = flops_launch / (avg_ms * 1e-3) / 1e12
-            return {"bound": "mfma", "kernel": ("search_kernel" if k <= 128 else "search_wide_kernel")
-                    + " (fp32 MFMA distance GEMM + fused arg-best)", "achieved": round(a, 2),
-                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_FP32_TFLOPS, 4),
-                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops_launch}
+            return scan_roofline(split, avg_ms, bsz, hi - lo, k, args.split_opt)
 
-        kpad = next(p for p in (16, 32, 64, 128, 256, 512) if p >= k)
-        achieved = flops_launch / (search_avg_ms * 1e-3) / 1e12
         traffic, traffic_src = (pmc_traffic(args.config + ("s3" if split_main else "")) if world == 1
                                 else (None, None))
         rec = {
@@ -881,6 +988,9 @@ def main():
             rec["cpu_baseline"] = None
         if world == 1 and args.config == "c3" and not args.no_c2:
             rec["c2"] = c2_bench(eng, not args.no_cpu)
+        if world == 1 and args.config == "c3" and not args.no_c5:
+            rec["c5"] = c5_bench(eng, dev, not args.no_cpu, args.steps, args.warmup, args.repeats,
+                                 min(args.cpu_budget, 8.0), args.split_opt)
         if world == 1 and not args.no_fit:
             rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu), "c2": fit_bench(eng, not args.no_cpu)}
         if world == 1 and not args.no_image:

@@ -183,9 +183,11 @@ __global__ __launch_bounds__(512, 1) void project_bf16_wide_kernel(const uint8_t
 
   // XCD-aware deal: consecutive block ids go round-robin over the 8 XCDs; give XCD x the
   // contiguous run [x * per, (x + 1) * per) of (split, m-tile, n-tile) items, split-major
+  // (the grid is total rounded up to a multiple of 8; the few padding workgroups exit)
   const int total = mt * nt * ns;
-  const int per = total / 8;  // host guarantees total % 8 == 0
+  const int per = (total + 7) / 8;
   const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (item >= total) return;
   const int split = item / (mt * nt);
   const int rem = item - split * (mt * nt);
   const int mi = rem / nt, ni = rem - (rem / nt) * nt;
@@ -385,11 +387,12 @@ int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int6
     const int64_t wsteps = d / WKS;
     const int nt = ldw % 256 == 0 ? ldw / 256 : ldw / 128;
     const int64_t tiles = (bpad + WM - 1) / WM * nt;
-    // fill the 256 CUs with one workgroup each; the item count must be a multiple of 8
+    // fill the 256 CUs with one workgroup each (an item count that is a multiple of 8
+    // deals evenly over the XCDs; the launcher pads the grid otherwise)
     int64_t ns = (256 + tiles - 1) / tiles;
     if (ns > wsteps) ns = wsteps;
     if (ns < 1) ns = 1;
-    while ((tiles * ns) % 8 != 0) ++ns;
+    while ((tiles * ns) % 8 != 0 && ns < wsteps) ++ns;
     const int64_t steps_per = (wsteps + ns - 1) / ns;
     *pix_per_split = steps_per * WKS;
     return (int)((d + *pix_per_split - 1) / *pix_per_split);
@@ -412,14 +415,14 @@ hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_
     const bool n256 = ldw % 256 == 0;
     const int nt = n256 ? ldw / 256 : ldw / 128;
     const int mt = (int)((bpad + WM - 1) / WM);
-    const int total = mt * nt * nsplit;
-    if (total % 8 != 0 || bpad % WM != 0) return hipErrorInvalidValue;
+    const int grid = (mt * nt * nsplit + 7) / 8 * 8;  // XCD deal over a multiple of 8
+    if (bpad % WM != 0 || pps % WKS != 0) return hipErrorInvalidValue;
     const uint8_t* p8 = static_cast<const uint8_t*>(P);
     if (n256)
-      hipLaunchKernelGGL((project_bf16_wide_kernel<256, WKS>), dim3((unsigned)total), dim3(512), 0, s, p8, b, d, mean_u8,
+      hipLaunchKernelGGL((project_bf16_wide_kernel<256, WKS>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d, mean_u8,
                          Wt16, ldw, part, bpad, pps, mt, nt, nsplit);
     else
-      hipLaunchKernelGGL((project_bf16_wide_kernel<128, WKS>), dim3((unsigned)total), dim3(512), 0, s, p8, b, d, mean_u8,
+      hipLaunchKernelGGL((project_bf16_wide_kernel<128, WKS>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d, mean_u8,
                          Wt16, ldw, part, bpad, pps, mt, nt, nsplit);
     return hipGetLastError();
   }

@@ -417,7 +417,22 @@ def int_synth_spectrum(r):
     return np.array([math.isqrt(4096 * 4096 // (j + 1)) for j in range(r)], dtype=np.int64)
 
 
-def int_synth_faces(n, side, r=160, seed=0, rows=None):
+def light_like_spectrum(lam, r):
+    """Integer factor weights whose covariance spectrum follows the eigenvalue profile
+    ``lam`` of a real training set (tests/golden/light_stats.npz: the reference's
+    faces/Light_version, useless/train.py:56-128) — its clustered eigen-gaps, the regime
+    where eigenvector parity is hardest — then decays as 1/(j+1) past len(lam):
+    ``s_j = round(4096 sqrt(lam_j / lam_0))`` (pure integer inputs for int_synth_faces)."""
+    lam = np.asarray(lam, dtype=np.float64)
+    w = np.empty(r)
+    m = min(r, len(lam))
+    w[:m] = np.sqrt(lam[:m] / lam[0])
+    if r > m:
+        w[m:] = w[m - 1] * np.sqrt(m / (np.arange(m, r) + 1.0))
+    return np.maximum(1, np.rint(4096.0 * w)).astype(np.int64)
+
+
+def int_synth_faces(n, side, r=160, seed=0, rows=None, spectrum=None):
     """Bit-reproducible synthetic faces for fit-parity fixtures at large shapes.
 
     ``X = clip(M + rint((Z.diag(s)).Bq / 2^20) + eps, 0, 255)`` with integer-valued
@@ -429,12 +444,14 @@ def int_synth_faces(n, side, r=160, seed=0, rows=None):
     pixels on the build container and on the GPU box.  Rows come in blocks of
     INT_SYNTH_BLOCK, each from its own seeded stream, so ``rows=(lo, hi)`` regenerates
     any slice.  The spectrum (eigenvalues ~ 1/(j+1) for r factors, noise floor far
-    below) keeps the top-128 eigen-gaps meaningful for eigenvector parity.
+    below) keeps the top-128 eigen-gaps meaningful for eigenvector parity; ``spectrum``
+    (r integers in 0..4096) replaces it, e.g. :func:`light_like_spectrum`.
     """
     d = side * side
     lo, hi = (0, n) if rows is None else rows
     bq = np.random.default_rng([seed, 0]).integers(-128, 128, size=(r, d)).astype(np.float64)
-    s = int_synth_spectrum(r).astype(np.float64)
+    s = (int_synth_spectrum(r) if spectrum is None else np.asarray(spectrum, dtype=np.int64)).astype(np.float64)
+    assert s.shape == (r,) and s.min() >= 0 and s.max() <= 4096, "integer weights 0..4096 keep the product exact"
     yy, xx = np.mgrid[0:side, 0:side]
     dy, dx = yy - side // 2, xx - side // 2
     m = (170 - (dx * dx + dy * dy) * 80 // max(side * side // 2, 1)).ravel().astype(np.float64)
