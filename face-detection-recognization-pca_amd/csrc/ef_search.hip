@@ -920,7 +920,10 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3) {
   pl.c_tpc = (int)std::max<int64_t>(1, (tiles + 511) / 512);
   pl.c_chunks = (int)((tiles + pl.c_tpc - 1) / pl.c_tpc);
   pl.c_grid = w3 ? 256 : 512;
-  const int pb = w3 ? 4 : 8;
+#ifndef EF_WIDE3_PB  // probe tiles per XCD block of the split-bf16 wide scan (variant builds: experiments)
+#define EF_WIDE3_PB 4
+#endif
+  const int pb = w3 ? EF_WIDE3_PB : 8;
   pl.pblk = pl.n_ptiles;
   pl.cblk = 1;
   if (wide && pl.n_ptiles % pb == 0 && pl.n_ptiles > pb) {

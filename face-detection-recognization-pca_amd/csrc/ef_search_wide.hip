@@ -34,6 +34,9 @@ namespace ef {
 #ifndef EF_WIDE_INTERLEAVE
 #define EF_WIDE_INTERLEAVE 0
 #endif
+#ifndef EF_WIDE_SERP  // wide16: 1 = serpentine k-slice order over a sweep's tiles (experiment)
+#define EF_WIDE_SERP 0
+#endif
 
 constexpr int WR = kWideRowTile;    // gallery rows per tile
 constexpr int WP = kWideProbeTile;  // probes per workgroup
@@ -700,7 +703,12 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
   // gallery (0) or probes (1)
   auto issue_piece = [&](int64_t it, int buf, int p) {
     const int64_t t = t0 + geo.tile(it);
-    const int sl = geo.slice(it);
+    int sl = geo.slice(it);
+#if EF_WIDE_SERP
+    // serpentine k order: odd tiles of the sweep walk the slices backwards, so the probe
+    // slices used last by one tile are the first the next tile re-reads (L2 reuse)
+    if ((t - t0) & 1) sl = NS - 1 - sl;
+#endif
     const int jj = p >> 1, j = wave * 4 + jj;
     if ((p & 1) == 0) {
       const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);

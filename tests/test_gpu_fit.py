@@ -312,3 +312,119 @@ def test_fused_column_stats_exact_beyond_32bit_quarters():
     np.testing.assert_allclose(var, v_ref, rtol=1e-12)
     del x
     torch.cuda.empty_cache()
+
+
+def _signs_vs_fixture(comps, g):
+    """Per-component sign alignment against a fixture's sign-normalised components (the
+    svd_flip rule: largest |entry| positive), accounting for every flip: allowed only
+    where the fixture's two largest |entries| are tied within the fits' difference there
+    (then the GPU's own largest entry is the runner-up pixel).  Returns the signs."""
+    R, px = _c3_probe_matrices(comps.shape[1])
+    np.testing.assert_array_equal(px, g["px"])
+    s = np.sign(((comps @ R) * g["comps_R"]).sum(axis=1))
+    ti, tv = g["top_idx"], g["top_val"]
+    for c in np.nonzero(s < 0)[0]:
+        gv = -comps[c, ti[c]]
+        margin = abs(tv[c, 0]) - abs(tv[c, 1])
+        assert margin <= np.abs(gv - tv[c]).sum() + 1e-15, f"component {c}: sign flipped with a clear max entry"
+        assert int(np.argmax(np.abs(comps[c]))) == int(ti[c, 1]) and comps[c, ti[c, 1]] > 0
+    return s
+
+
+@pytest.mark.parametrize("name", ["fit_hard", "fit_c2"])
+def test_fit_vs_reference_manual_pca(name):
+    """manual_pca (useless/train.py:56-128) on the GPU vs the REFERENCE's own manual_pca
+    run on the same exact-integer synthetic pixels (tests/golden/make_goldens.py
+    fit_shapes; the box regenerates them bit for bit):
+
+    * fit_hard: n = 229, d = 100 x 100 (faces/Light_version's shape) with the real Light
+      set's eigenvalue profile, so its sample spectrum has the real set's clustered gaps
+      (min relative gap 1.1 %): ALL 50 components at the north star's 1e-4 relative;
+    * fit_c2: BASELINE.json configs[1]'s fit shape, n = 10000, d = 16384, k = 64: the Gram
+      path at order 10000 (int8 Gram, subspace iteration, A^T.V back-projection).
+
+    Eigenvalues rtol 1e-9; unit components through a +-1 probe matrix (|c.R| ~ |c| = 1, so
+    atol 1e-4 is 1e-4 relative) and at 256 pixels; projections 1e-4 of their scale."""
+    from eigenface import manual_pca
+    g = golden(name + ".npz")
+    spec = g["spectrum"] if "spectrum" in g.files else None
+    x = orc.int_synth_faces(int(g["n"]), int(g["side"]), r=int(g["r"]), seed=int(g["seed"]), spectrum=spec)
+    k = int(g["k"])
+    eig, mean, proj, lam = manual_pca(x, k)
+    assert eig.shape == (x.shape[1], k) and proj.shape == (x.shape[0], k)
+    np.testing.assert_allclose(mean.sum(), float(g["mean_sum"]), rtol=1e-13)
+    np.testing.assert_allclose(lam, g["eigenvalues"], rtol=1e-9)
+    comps = eig.T
+    s = _signs_vs_fixture(comps, g)
+    R, px = _c3_probe_matrices(x.shape[1])
+    err_r = np.abs((comps @ R) * s[:, None] - g["comps_R"]).max()
+    err_px = np.abs(comps[:, px] * s[:, None] - g["comps_px"]).max()
+    f = proj[:64] * s[None, :]
+    err_f = np.abs(f - g["projected"]).max() / np.abs(g["projected"]).max()
+    print(f"{name}: {k} components, max |dc.R| {err_r:.2e}, max |dc| at 256 px {err_px:.2e}, "
+          f"projection rel {err_f:.2e}, flips {int((s < 0).sum())}")
+    assert err_r <= 1e-4 and err_px <= 1e-4 and err_f <= 1e-4
+    np.testing.assert_allclose(np.linalg.norm(proj, axis=0), g["proj_colnorm"], rtol=1e-8)
+
+
+def test_fit_c3_full_size_properties():
+    """The 1M-face C3 fit itself (train-v4.py:126-146 at n = 1M, d = 16384, k = 128: the
+    8 K-split int32 SYRK slabs at <= 131,008 samples each, the order-16384 subspace
+    iteration), checked by properties no fixture can hold at this size, with an
+    independent fp64 checker (torch fp64 GEMMs on the GPU over the standardised data
+    Z = (X - mean) / scale, streamed in chunks):
+
+    * components orthonormal (|V^T V - I| <= 1e-10);
+    * Rayleigh quotients v^T C v equal the returned eigenvalues (rtol 1e-9);
+    * residuals |C v - lambda v| <= 1e-6 lambda_1 for every component;
+    * mean / scale equal exact integer column statistics."""
+    import torch
+    from eigenface import get_engine, synth
+    n, side, k, r = 1_000_000, 128, 128, 256
+    d = side * side
+    dev = torch.device("cuda", 0)
+    B = torch.from_numpy(synth.basis(d, r, 5)).to(dev, torch.float32)
+    sp = torch.from_numpy(synth.spectrum(r)).to(dev, torch.float32)
+    mu = torch.from_numpy(synth.mean_face(side)).to(dev, torch.float32)
+    X = torch.empty((n, d), dtype=torch.uint8, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(77)
+    for a in range(0, n, 32768):
+        e = min(n, a + 32768)
+        z = torch.randn((e - a, r), generator=gen, device=dev) * sp
+        X[a:e] = (mu + z @ B.T + 2.0 * torch.randn((e - a, d), generator=gen, device=dev)).round_().clamp_(0, 255) \
+            .to(torch.uint8)
+    del B, z
+    res = get_engine(0).fit(X, k, standardize=True, projection=False)
+    V = res.components.T.contiguous()  # d x k fp64
+    lam = res.eigenvalues
+    # exact column statistics
+    s1 = torch.zeros(d, dtype=torch.float64, device=dev)
+    s2 = torch.zeros(d, dtype=torch.float64, device=dev)
+    for a in range(0, n, 65536):
+        c = X[a:a + 65536].to(torch.float64)
+        s1 += c.sum(0)
+        s2 += (c * c).sum(0)
+    m_ref = s1 / n
+    var_ref = s2 / n - m_ref * m_ref
+    torch.testing.assert_close(res.mean, m_ref, rtol=1e-13, atol=0)
+    sc_ref = torch.where(var_ref > 0, var_ref.sqrt(), torch.ones_like(var_ref))
+    torch.testing.assert_close(res.scale, sc_ref, rtol=1e-9, atol=0)
+    # C V = Z^T (Z V) / (n - 1), streamed
+    inv = 1.0 / res.scale
+    CV = torch.zeros((d, k), dtype=torch.float64, device=dev)
+    for a in range(0, n, 32768):
+        zc = (X[a:a + 32768].to(torch.float64) - res.mean) * inv
+        CV += zc.T @ (zc @ V)
+    CV /= n - 1
+    orth = (V.T @ V - torch.eye(k, dtype=torch.float64, device=dev)).abs().max().item()
+    rq = (V * CV).sum(0)
+    rq_err = ((rq - lam).abs() / lam).max().item()
+    resid = (CV - V * lam).norm(dim=0)
+    res_rel = (resid / lam[0]).max().item()
+    print(f"C3 1M fit: {res.iters} iterations, |V'V-I| {orth:.2e}, Rayleigh rel {rq_err:.2e}, "
+          f"max |Cv - lv| / l1 {res_rel:.2e}, per-component max |Cv - lv| / l_i {(resid / lam).max().item():.2e}")
+    assert orth <= 1e-10
+    assert rq_err <= 1e-9
+    assert res_rel <= 1e-6
+    del X, CV
+    torch.cuda.empty_cache()

@@ -113,3 +113,20 @@ def test_int_synth_is_exact_and_sliceable():
     assert int(g["n"]) == 20000 and int(g["side"]) == 128
     # the fixture's scaler mean pins all 20000 rows; spot-check the generator on 64 rows
     assert x.dtype == np.uint8 and 100 < x.mean() < 200 and x.std() > 10
+
+
+def test_oracle_manual_pca_on_light_like_hard_spectrum():
+    """The oracle's manual_pca restatement against the reference's own manual_pca output
+    on the Light-like clustered-gap set (tests/golden/fit_hard.npz): eigenvalues and all
+    50 sign-normalised components."""
+    g = golden("fit_hard.npz")
+    x = orc.int_synth_faces(int(g["n"]), int(g["side"]), r=int(g["r"]), seed=int(g["seed"]),
+                            spectrum=g["spectrum"])
+    eig, mean, proj, lam = orc.manual_pca(x, int(g["k"]))
+    np.testing.assert_allclose(lam, g["eigenvalues"], rtol=1e-10)
+    np.testing.assert_allclose(mean.sum(), float(g["mean_sum"]), rtol=1e-14)
+    comps = eig.T
+    comps = comps * np.sign(comps[np.arange(len(comps)), np.argmax(np.abs(comps), axis=1)])[:, None]
+    R = np.random.default_rng([5]).integers(0, 2, size=(x.shape[1], 8)).astype(np.float64) * 2.0 - 1.0
+    np.testing.assert_allclose(comps @ R, g["comps_R"], atol=1e-8)
+    np.testing.assert_allclose(comps[:, g["px"]], g["comps_px"], atol=1e-10)
