@@ -255,6 +255,28 @@ __global__ __launch_bounds__(256) void transpose_stats_lds_kernel(const uint8_t*
 // ~30 B/clk per CU): a stage moves (256 + TJ) x 64 B for 256 x TJ x 64 MACs, i.e. 32 B per
 // MFMA-clock at TJ = 256 and 26.7 B at TJ = 384 (192 accumulator VGPRs per lane, the most
 // two waves per SIMD can hold next to their fragments).
+// When each wave issues the DMA pieces of the stage NB ahead, as positions in the second
+// k-step of a stage (0 = right after the stage's barrier, n = after row block n - 1's
+// MFMAs): pieces [0, EF_SYRK_SPLIT) at position A, the rest at position B, separately for
+// waves 0..3 (LO) and 4..7 (HI) — the two waves sharing a SIMD.  Issuing every wave's
+// burst right after the barrier (all positions 0) left both waves of a SIMD in their DMA
+// issue at once; measured (C3 SYRK, profiles/r04/syrk_stagger_ab*.txt): all at 0 105.9 ms,
+// HI at 1: 99.9, LO at 1 + HI at 3: 94.6.
+#ifndef EF_SYRK_LO_A
+#define EF_SYRK_LO_A 1
+#endif
+#ifndef EF_SYRK_LO_B
+#define EF_SYRK_LO_B EF_SYRK_LO_A
+#endif
+#ifndef EF_SYRK_HI_A
+#define EF_SYRK_HI_A 3
+#endif
+#ifndef EF_SYRK_HI_B
+#define EF_SYRK_HI_B EF_SYRK_HI_A
+#endif
+#ifndef EF_SYRK_SPLIT
+#define EF_SYRK_SPLIT 3
+#endif
 template <int TJ, int NB>
 __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                          int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
@@ -297,10 +319,11 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   // kSyrkPadBytes the allocation carries past the last one: finite values whose products
   // land only in outputs the epilogue masks.
   const unsigned voff = (unsigned)(lrow * YK + lchunk * 16);
-  auto issue = [&](int64_t st, int buf) {
+  auto issue = [&](int64_t st, int buf, int q0 = 0, int q1 = 1 << 30) {
     const uint8_t* base = At + st * blk;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
+      if (q < q0 || q >= q1) continue;
       const int p = wave * PPW + q;
       const int64_t r0 = p < NPA ? i0 + p * 16 : j0 + (p - NPA) * 16;
       glds16s(voff, (unsigned long long)(size_t)(base + r0 * YK), lds_base + (unsigned)(buf * STG + p * 1024));
@@ -331,15 +354,17 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
   // One k-step's MFMAs, row block by row block; each A fragment is refilled with the
   // next k-step's as soon as its row block's MFMAs are issued (one A set + two B sets live:
   // 40 fragment VGPRs next to the 64 * NJ accumulators).
-  auto mma = [&](i32x4 (&a)[4], const i32x4 (&b)[NJ], const uint8_t* nsa, int ns) {
+  auto mma = [&](i32x4 (&a)[4], const i32x4 (&b)[NJ], const uint8_t* nsa, int ns, auto&& mid) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
       a[i] = fa(nsa, ns, i);
+      mid(i + 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  auto none = [](int) {};
   // Ring of NB stages.  Each stage is PPW DMA instructions per wave, so "stage t landed" is
   // vmcnt <= PPW x (stages issued after it); tail stages past nst are issued as harmless
   // re-reads of the first stage so the count stays uniform.  One barrier per stage, placed
@@ -359,19 +384,24 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
       const uint8_t* cur = smem + (st % NB) * STG;
       fb(cur, 1, b1);
       __builtin_amdgcn_sched_barrier(0);
-      mma(a, b0, cur, 1);  // k-step 0; A refilled with k-step 1
+      mma(a, b0, cur, 1, none);  // k-step 0; A refilled with k-step 1
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 2)) : "memory");  // stage st+1 landed
       __syncthreads();  // every wave done reading stage st; stage st+1 visible
-      {
-        const int64_t nx = st + NB;
-        issue(sb + (nx < nst ? nx : 0), (int)(nx % NB));  // into stage st's slot
-      }
+      const int64_t nx = st + NB;
+      auto issue_next = [&](int q0, int q1) { issue(sb + (nx < nst ? nx : 0), (int)(nx % NB), q0, q1); };  // into stage st's slot
+      // this wave's pieces at positions (A, B) of k-step 1 (EF_SYRK_* above)
+      const int pa = wave < 4 ? EF_SYRK_LO_A : EF_SYRK_HI_A, pb = wave < 4 ? EF_SYRK_LO_B : EF_SYRK_HI_B;
+      auto at_pos = [&](int pos) {
+        if (pos == pa) issue_next(0, EF_SYRK_SPLIT);
+        if (pos == pb) issue_next(EF_SYRK_SPLIT, PPW);
+      };
+      at_pos(0);
       // (after the last stage these read a slot holding a re-read of the first stage:
       // harmless, unused, and branch-free)
       const uint8_t* nxt = smem + ((st + 1) % NB) * STG;
       fb(nxt, 0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      mma(a, b1, nxt, 0);  // k-step 1; A refilled with the next stage's k-step 0
+      mma(a, b1, nxt, 0, at_pos);  // k-step 1; A refilled with the next stage's k-step 0
     }
     dma_wait_all();
   }
@@ -436,10 +466,11 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
   const int lchunk = (lane & 3) ^ syrk16_swz((lane >> 4) & 3);
   const int64_t blk = dim * YK;
   const unsigned voff = (unsigned)(lrow * YK + lchunk * 16);
-  auto issue = [&](int64_t st, int buf) {
+  auto issue = [&](int64_t st, int buf, int q0 = 0, int q1 = 1 << 30) {
     const uint8_t* base = At + st * blk;
 #pragma unroll
     for (int q = 0; q < PPW; ++q) {
+      if (q < q0 || q >= q1) continue;
       const int p = wave * PPW + q;
       if (p < NP) {
         const int64_t r0 = p < NPA ? i0 + p * 16 : j0 + (p - NPA) * 16;

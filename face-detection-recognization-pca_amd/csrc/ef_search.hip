@@ -921,7 +921,7 @@ SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3) {
   pl.c_chunks = (int)((tiles + pl.c_tpc - 1) / pl.c_tpc);
   pl.c_grid = w3 ? 256 : 512;
 #ifndef EF_WIDE3_PB  // probe tiles per XCD block of the split-bf16 wide scan (variant builds: experiments)
-#define EF_WIDE3_PB 4
+#define EF_WIDE3_PB 8
 #endif
   const int pb = w3 ? EF_WIDE3_PB : 8;
   pl.pblk = pl.n_ptiles;

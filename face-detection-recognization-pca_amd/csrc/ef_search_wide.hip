@@ -35,7 +35,7 @@ namespace ef {
 #define EF_WIDE_INTERLEAVE 0
 #endif
 #ifndef EF_WIDE_SERP  // wide16: 1 = serpentine k-slice order over a sweep's tiles (experiment)
-#define EF_WIDE_SERP 0
+#define EF_WIDE_SERP 1  // with EF_WIDE3_PB 8: C5 HBM fetch 12.0 -> 8.1 GB per launch, same time (profiles/r04/c5_hbm_ab.txt)
 #endif
 
 constexpr int WR = kWideRowTile;    // gallery rows per tile

@@ -138,3 +138,28 @@ def test_manual_pca_accepts_float_data(eng):
     o_e, o_m, o_p, o_l = orc.manual_pca(xf, 8)
     np.testing.assert_allclose(lam, o_l, rtol=1e-9)
     np.testing.assert_allclose(e, o_e * np.sign((e * o_e).sum(0)), atol=1e-6)
+
+
+def test_manual_helpers_keep_recognition_gallery_resident():
+    """cosine_similarity / project_face_to_eigenspace run on the helpers' own engine, so a
+    per-face cosine check between recognise calls does not evict (and force a re-upload
+    of) the gallery and model the recognise functions keep resident; any vector length
+    works (the reference's useless/scan.py:58-78 takes any)."""
+    from eigenface import cosine_similarity, get_engine, project_face_to_eigenspace, recognize_face_with_model
+    rng = np.random.default_rng(12)
+    feats = rng.standard_normal((300, 40))
+    md = {"face_features": feats, "face_labels": np.zeros(300, np.int64), "person_id_map": {"p": 0}}
+    pid, name, sim = recognize_face_with_model(feats[7], md, 0.5)
+    assert (pid, name) == (0, "p") and sim > 0.999
+    shared = get_engine(0)
+    tok = shared.gallery_owner
+    for n in (3, 40, 513, 1000):
+        a, b = rng.standard_normal(n), rng.standard_normal(n)
+        ref = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+        assert abs(cosine_similarity(a, b) - ref) < 1e-6
+    ef = rng.standard_normal((64, 10))
+    f = project_face_to_eigenspace(rng.integers(0, 256, 64).astype(np.uint8), ef, np.full(64, 100.0))
+    assert f.shape == (10,)
+    assert shared.gallery_owner is tok  # still resident: no re-upload on the next recognise
+    assert recognize_face_with_model(feats[7], md, 0.5)[:2] == (0, "p")
+    assert shared.gallery_owner is tok
