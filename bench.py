@@ -867,6 +867,12 @@ def main():
 
     idx, best = decode_keys(keys.cpu().numpy(), args.metric)
     match = float((idx == targets).mean())
+    exchange_ms = None
+    if world > 1:  # the step's collectives alone (upper bound of their share; max over ranks)
+        t = torch.tensor([shard.exchange_ms(bsz, k, dev)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exchange_ms = float(t.item())
     ranks_agree = None
     if world > 1:  # every rank must hold the same merged keys
         h = torch.tensor([int(np.bitwise_xor.reduce(keys.cpu().numpy() * np.int64(0x9E3779B1)))
@@ -963,6 +969,8 @@ def main():
             "roofline": dict(roof(split_main, search_avg_ms), traffic=traffic, traffic_source=traffic_src,
                              launches=s_n),
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
+            "exchange_ms_per_step": round(exchange_ms, 4) if exchange_ms is not None else None,
+            "exchange_share_of_step": round(exchange_ms / ms_step, 4) if exchange_ms is not None else None,
             "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
             "check": {"planted_match": match, "ranks_agree": ranks_agree, "host_buffer_keys_identical": host_same},
         }

@@ -304,7 +304,13 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     // Rayleigh-Ritz at iterations 1, 2, 4 (small orders only: there they re-order the block
     // early enough to matter; at order >= 12288 they cost 26 of 62 Jacobi sweeps and change
     // no iteration count), 8, then every rr_period(dim)
+#ifdef EF_DIAGNOSTICS
+    static const int early_rule = [] { const char* e = getenv("EF_FIT_EARLY"); return e ? atoi(e) : 0; }();
+    const bool early = early_rule == 0 ? dim < 12288 && (it <= 2 || it == 4)
+                     : early_rule == 1 ? (it <= 2 || it == 4) : it == early_rule;
+#else
     const bool early = dim < 12288 && (it <= 2 || it == 4);
+#endif
     const bool rr = early || it == next_rr || it == max_iters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
@@ -333,9 +339,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
 #else
       (void)wi;
 #endif
-      double coarse_tol = 1e-4;
+      double coarse_tol = 1e-4, coarse_pred = 1e-6;
 #ifdef EF_DIAGNOSTICS
       if (const char* e = getenv("EF_FIT_COARSE_TOL")) coarse_tol = atof(e);
+      if (const char* e = getenv("EF_FIT_COARSE_PRED")) coarse_pred = atof(e);
 #endif
       // Chebyshev rate: the k-th Ritz value's error shrinks per product by 1 / rho^2,
       // rho = x + sqrt(x^2 - 1), x = theta_k / sigma - 1 on the next interval [0, theta_m]
@@ -352,7 +359,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       // previous step's error, which the products since then shrank by rate_prev each
       const double e_now = have_prev && rate_prev > 0.0 ? worst * std::pow(rate_prev, it - last_rr_it) : worst;
       // fp64 products from the next iteration on once the fp32 phase has done its part
-      if (coarse && (worst < coarse_tol || (rate_prev > 0.0 && e_now < 1e-6))) coarse = false;
+      if (coarse && (worst < coarse_tol || (rate_prev > 0.0 && e_now < coarse_pred))) coarse = false;
       // Schedule the next Rayleigh-Ritz step.  The test above passes once the PREVIOUS
       // step's Ritz values were already within 1e-13, so with the change per period
       // shrinking geometrically (worst now vs worst at the previous step) the current error

@@ -186,3 +186,38 @@ class ShardedGallery:
             return self._gather_merge(self.engine.recognize_matches(P, metric), b, keys)
         q = self.project_sharded(P)
         return self._gather_merge(self._local(q, metric), b, keys)
+
+    def exchange_ms(self, b: int, k: int, device, reps: int = 20) -> float:
+        """Milliseconds per step of this rank's collectives alone — the feature all-gather of
+        ceil(b / world) x k fp32 rows per rank and the all-gather of b fp64 match records —
+        on the same transport as recognize_keys (RCCL stream-ordered, or gloo through the
+        host), averaged over `reps` after one warm-up.  The caller takes the max over ranks."""
+        import time
+
+        import torch
+        import torch.distributed as dist
+
+        c = (b + self.world - 1) // self.world
+        loc = torch.zeros((c, k), dtype=torch.float32, device=device)
+        full = torch.empty((self.world * c, k), dtype=torch.float32, device=device)
+        rec = torch.zeros((b, 3), dtype=torch.int64, device=device)
+        gloo = dist.get_backend(self.group) != "nccl"
+        parts = torch.empty((self.world * b, 3), dtype=torch.int64, device=device)
+
+        def one():
+            self._allgather_rows(loc, full)
+            if gloo:
+                chunks = [torch.empty((b, 3), dtype=torch.int64) for _ in range(self.world)]
+                dist.all_gather(chunks, rec.cpu(), group=self.group)
+                parts.copy_(torch.cat(chunks))
+            else:
+                dist.all_gather_into_tensor(parts, rec, group=self.group)
+
+        one()
+        torch.cuda.synchronize(device)
+        dist.barrier(group=self.group)
+        t = time.perf_counter()
+        for _ in range(reps):
+            one()
+        torch.cuda.synchronize(device)
+        return (time.perf_counter() - t) / reps * 1e3

@@ -43,6 +43,10 @@ def test_bench_two_ranks_one_gpu(metric):
     assert rec["config"]["rows_per_rank"] == 100_000
     assert rec["steps"] == 3 and len(rec["repeats_ms_per_step"]) == 2
     assert rec["value"] > 0 and rec["cpu_baseline"] is None
+    # the collectives alone (gloo through the host here: an upper bound of RCCL's share)
+    assert rec["exchange_ms_per_step"] > 0 and 0 < rec["exchange_share_of_step"]
+    print(f"2 ranks / one GPU, gloo: step {rec['ms_per_step']} ms, exchange {rec['exchange_ms_per_step']} ms "
+          f"({100 * rec['exchange_share_of_step']:.1f} %)")
 
 
 def test_bench_rejects_gpus_world_mismatch():
