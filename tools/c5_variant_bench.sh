@@ -9,7 +9,7 @@ mkdir -p $O
 for rep in 1 2; do
   for v in base "$@"; do
     if [ "$v" = base ]; then unset EF_LIB_VARIANT; else export EF_LIB_VARIANT=$v; fi
-    timeout -k 10 240 python bench.py --config c5 --no-cpu --no-fit --no-image --no-c2 --no-split --steps 10 \
+    timeout -k 10 240 python bench.py --config c5 --no-cpu --no-fit --no-image --no-c2 --no-c5 --no-split --steps 10 \
       --repeats 3 > $O/$v.$rep.json 2> $O/$v.$rep.err || exit $?
     python -c "import json; d=json.loads(open('$O/$v.$rep.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['check']['planted_match'])" >> $O/summary.txt
   done
