@@ -375,13 +375,13 @@ def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu
     if syrk_n > 0 and syrk_ms > 0:
         ops = float(n) * d * (d + 1)
         tops = ops / (syrk_ms * 1e-3) / 1e12
-        roof = {"kernel": "syrk_i8_kernel<384,4>", "bound": "mfma", "achieved": round(tops, 1),
+        roof = {"kernel": "syrk16_i8_kernel<6,4> (v_mfma_i32_16x16x64_i8, 256 x 384 tiles)", "bound": "mfma", "achieved": round(tops, 1),
                 "peak": 5000.0, "unit": "TOP/s (int8)", "frac": round(tops / 5000.0, 4),
                 "syrk_ms": round(syrk_ms, 3), "syrk_share_of_fit": round(syrk_ms * 1e-3 / t_fit, 3),
                 "ops_per_fit": ops,
                 "note": "ops = n d (d+1) (upper triangle of X'^T X', 2 per MAC); peak = 2 x the 2.5 PF bf16 "
                         "dense figure (MI355X_MICROARCH.md: I8 at 2x the BF16 rate per clock)"}
-        ceil = bf16_ceiling("i8 32x32x32 lds", "i8_clock.json")
+        ceil = bf16_ceiling("i8 16x16x64 lds", "i8_clock.json")
         if ceil:
             roof["power_limited_ceiling_TOPs"] = ceil[0]
             roof["frac_of_power_limited_ceiling"] = round(tops / ceil[0], 4)

@@ -419,12 +419,14 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
     }
 }
 
-#ifdef EF_DIAGNOSTICS
-// Diagnostic-build experiment (EF_SYRK16 = 5 | 6), not used by the product library: the int8
+// The product SYRK for orders >= 2048 (256 x 384 tiles, NJB = 6; round 4).  The int8
 // 16x16x64 MFMA holds a higher clock than 32x32x32 under load (tools/micro/bf16_clock i:
-// 2.06 vs 1.78 GHz with LDS-fed operands, profiles/r03/i8_clock.json), but this kernel
-// measured no faster in the C3 fit (NJB = 6: 0.165 vs 0.163-0.168 s; NJB = 5: 0.176 s;
-// identical results) — the SYRK stays on the L2 -> LDS stream's limit.
+// 2.06 vs 1.78 GHz with LDS-fed operands, profiles/r03/i8_clock.json); in round 3 this
+// kernel measured no faster in the C3 fit (NJB = 6: 0.165 vs 0.163-0.168 s) while every
+// wave issued its stage's DMA right after the barrier.  With the issue staggered over the
+// two waves of a SIMD (EF_S16_LO / EF_S16_HI below) it takes 91.8-92.7 ms against the
+// staggered 32x32x32 kernel's 98.6-99.5 ms on the same box (C3, three alternations,
+// identical eigenvalues; profiles/r04/syrk16_stagger_ab.txt).
 // The same item on v_mfma_i32_16x16x64_i8 (one 64-sample k-step per stage): wave (wm, wn)
 // owns 128 rows x 16 NJB columns as 8 x NJB 16 x 16 blocks (4 accumulator VGPRs each).
 // Lane l supplies row l & 15 of a block and samples 16 (l >> 4) .. +15 (the K order inside a
@@ -436,6 +438,12 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
 // visible, slot st retired) sits before the last column, during which the A fragments are
 // refilled with stage st+1's.
 __device__ __forceinline__ int syrk16_swz(int b) { return (0x78 >> (2 * b)) & 3; }
+#ifndef EF_S16_LO  // measured (C3 SYRK): (LO, HI) = (0, 0) 109 ms, (1, 3) 92-93, (1, 2) 104,
+#define EF_S16_LO 1  // (1, 4) 108, (1, 5) 104, (1, 6) 105, (2, 3) 106, (2, 4) 120, (0, 3) 115
+#endif
+#ifndef EF_S16_HI
+#define EF_S16_HI 3
+#endif
 
 template <int NJB, int NB>
 __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
@@ -501,6 +509,17 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = fa(smem, i);
     bq = fb(smem, 0);
+    // DMA issue position of this wave (EF_S16_LO / EF_S16_HI for waves 0-3 / 4-7): 0 = right
+    // after the barrier, 1 = after the last column's MFMAs, 2 + j = after column j of the
+    // next stage (the pending stage index is carried across the iteration)
+    const int dpos = wave < 4 ? EF_S16_LO : EF_S16_HI;
+    int64_t pend = -1;
+    auto flush = [&](int pos) {
+      if (pos == dpos && pend >= 0) {
+        issue(sb + (pend < nst ? pend : 0), (int)(pend % NB));
+        pend = -1;
+      }
+    };
     for (int64_t st = 0; st < nst; ++st) {
       const uint8_t* cur = smem + (st % NB) * STG;
       const uint8_t* nxt = smem + ((st + 1) % NB) * STG;
@@ -510,15 +529,18 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][j], 0, 0, 0);
         bq = bn;
+        flush(2 + j);
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if (pend >= 0) {  // a position past this stage's columns: issue before the wait below
+        issue(sb + (pend < nst ? pend : 0), (int)(pend % NB));
+        pend = -1;
       }
       // every read of stage st is issued (the barrier waits for them); stage st+1 landed
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (NB - 2)) : "memory");
       __syncthreads();
-      {
-        const int64_t nx = st + NB;
-        issue(sb + (nx < nst ? nx : 0), (int)(nx % NB));  // into stage st's slot
-      }
+      pend = st + NB;  // into stage st's slot
+      flush(0);
       bn = fb(nxt, 0);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -526,6 +548,7 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
         a[i] = fa(nxt, i);
       }
       bq = bn;
+      flush(1);
       __builtin_amdgcn_sched_barrier(0);
     }
     dma_wait_all();
@@ -543,7 +566,6 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
       }
     }
 }
-#endif  // EF_DIAGNOSTICS
 
 // ---------------------------------------------------------------- exact finishing
 // R[r] = sum_k At[.][r][k] * c[k]   (Gram path; exact in int64)
@@ -677,9 +699,11 @@ CovPlan cov_i8_plan(int64_t dim, int64_t K, int64_t slab_budget) {
   CovPlan p;
   p.nst = cov_i8_kpad(K) / YK;
   p.tj = syrk_tile_cols(dim);
-#ifdef EF_DIAGNOSTICS  // EF_SYRK16=5|6: the 16x16x64 kernel with 16*n-column wave blocks
+  if (p.tj == 384) p.njb = 6;  // the 16x16x64 kernel (syrk16_i8_kernel<6>) on the 384-column tiles
+#ifdef EF_DIAGNOSTICS  // EF_SYRK16 = 0: the 32x32x32 kernel; 5 | 6: the 16x16x64 kernel with 16 n-column wave blocks
   if (const char* e = getenv("EF_SYRK16")) {
     const int v = atoi(e);
+    if (v == 0) p.njb = 0;
     if ((v == 5 || v == 6) && dim >= 2048) p.njb = v, p.tj = 64 * v;
   }
 #endif
@@ -766,16 +790,15 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
   for (int pass = 0; pass < p.passes; ++pass) {
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
-#ifdef EF_DIAGNOSTICS
     if (p.njb == 6)
       hipLaunchKernelGGL((syrk16_i8_kernel<6, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+#ifdef EF_DIAGNOSTICS
     else if (p.njb == 5)
       hipLaunchKernelGGL((syrk16_i8_kernel<5, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
-    else
 #endif
-    if (p.tj == 384)
+    else if (p.tj == 384)
       hipLaunchKernelGGL((syrk_i8_kernel<384, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
     else

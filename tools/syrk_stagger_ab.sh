@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 9
 O=gpurun_out/$1; shift
 mkdir -p $O
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in base "$@"; do
     if [ "$v" = base ]; then unset EF_LIB_VARIANT; else export EF_LIB_VARIANT=$v; fi
     timeout -k 10 200 python tools/prof_fit.py > $O/$v.$rep.txt 2>&1 || exit $?
