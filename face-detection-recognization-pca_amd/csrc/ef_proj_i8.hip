@@ -94,6 +94,12 @@ __global__ void cc_kernel(const double* __restrict__ E, const double* __restrict
   if (threadIdx.x == 0) cc[c] = red[0];
 }
 
+#ifndef EF_PROJ_LO  // DMA issue position (0 = after the barrier, n = after row block n - 1)
+#define EF_PROJ_LO 1   // of waves 0-3 and 4-7 (the covariance SYRK's measured best)
+#endif
+#ifndef EF_PROJ_HI
+#define EF_PROJ_HI 3
+#endif
 template <int TN>
 __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
                                                          const int8_t* __restrict__ D, int ntn, int nblocks,
@@ -164,15 +170,17 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   };
   // one k-step's MFMAs, row block by row block; each A fragment is refilled with the next
   // k-step's as soon as its row block's MFMAs are issued
-  auto mma = [&](i32x4 (&a)[IA], const i32x4 (&bb)[JB], const uint8_t* nsa, int ns) {
+  auto mma = [&](i32x4 (&a)[IA], const i32x4 (&bb)[JB], const uint8_t* nsa, int ns, auto&& mid) {
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
 #pragma unroll
       for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
       a[i] = fa(nsa, ns, i);
+      mid(i + 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  auto none = [](int) {};
   // Ring of PNB stages, 2 + BPW DMA instructions per wave per stage: "stage t landed" is
   // vmcnt <= (2 + BPW) x (stages issued after it); tail stages re-read stage 0 so the count
   // stays uniform.  As in the covariance SYRK (ef_cov_i8.hip), the one barrier per stage
@@ -191,19 +199,23 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
     const uint8_t* cur = smem + (st % PNB) * PSTAGE;
     fb(cur, 1, b1);
     __builtin_amdgcn_sched_barrier(0);
-    mma(a, b0, cur, 1);  // k-step 0; A refilled with k-step 1
+    mma(a, b0, cur, 1, none);  // k-step 0; A refilled with k-step 1
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Q * (PNB - 2)) : "memory");  // stage st+1 landed
     __syncthreads();  // every wave done reading stage st; stage st+1 visible
-    {
-      const int64_t nx = st + PNB;
-      issue(nx < nst ? nx : 0, (int)(nx % PNB));  // into stage st's slot
-    }
+    const int64_t nx = st + PNB;
+    // the DMA into stage st's slot, at this wave's position of k-step 1 (the SYRK's stagger:
+    // the two waves of a SIMD do not pay the pieces' issue cost at the same time)
+    const int dpos = wave < 4 ? EF_PROJ_LO : EF_PROJ_HI;
+    auto at_pos = [&](int pos) {
+      if (pos == dpos) issue(nx < nst ? nx : 0, (int)(nx % PNB));
+    };
+    at_pos(0);
     // (after the last stage these read a slot holding a re-read of the first stage:
     // harmless, unused, and branch-free)
     const uint8_t* nxt = smem + ((st + 1) % PNB) * PSTAGE;
     fb(nxt, 0, b0);
     __builtin_amdgcn_sched_barrier(0);
-    mma(a, b1, nxt, 0);  // k-step 1; A refilled with the next stage's k-step 0
+    mma(a, b1, nxt, 0, at_pos);  // k-step 1; A refilled with the next stage's k-step 0
   }
   dma_wait_all();
 #pragma unroll

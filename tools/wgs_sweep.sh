@@ -7,7 +7,7 @@ O=gpurun_out/$1; shift
 mkdir -p $O
 export EF_LIB_VARIANT=diag
 for w in "$@"; do
-  EF_SEARCH_WGS=$w timeout -k 10 200 python bench.py --no-cpu --no-fit --no-image --no-c2 > $O/w$w.json 2> $O/w$w.err || exit $?
+  EF_SEARCH_WGS=$w timeout -k 10 200 python bench.py --no-cpu --no-fit --no-image --no-c2 --no-c5 --gallery ${GALLERY:-1000000} > $O/w$w.json 2> $O/w$w.err || exit $?
   python -c "import json; d=json.loads(open('$O/w$w.json').read().strip().splitlines()[-1]); s=d['scan_split_bf16']; print('$w', d['value'], d['roofline']['avg_launch_ms'], s['value'], s['roofline']['avg_launch_ms'], s['keys_identical_to_headline'])" >> $O/summary.txt
 done
 echo done
