@@ -390,6 +390,8 @@ __global__ __launch_bounds__(512, 1) void syrk_i8_kernel(const uint8_t* __restri
       const int64_t nx = st + NB;
       auto issue_next = [&](int q0, int q1) { issue(sb + (nx < nst ? nx : 0), (int)(nx % NB), q0, q1); };  // into stage st's slot
       // this wave's pieces at positions (A, B) of k-step 1 (EF_SYRK_* above)
+      static_assert(EF_SYRK_LO_A <= 4 && EF_SYRK_LO_B <= 4 && EF_SYRK_HI_A <= 4 && EF_SYRK_HI_B <= 4,
+                    "issue positions must exist (4 row blocks): every wave issues its pieces each stage");
       const int pa = wave < 4 ? EF_SYRK_LO_A : EF_SYRK_HI_A, pb = wave < 4 ? EF_SYRK_LO_B : EF_SYRK_HI_B;
       auto at_pos = [&](int pos) {
         if (pos == pa) issue_next(0, EF_SYRK_SPLIT);
@@ -512,6 +514,7 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
     // DMA issue position of this wave (EF_S16_LO / EF_S16_HI for waves 0-3 / 4-7): 0 = right
     // after the barrier, 1 = after the last column's MFMAs, 2 + j = after column j of the
     // next stage (the pending stage index is carried across the iteration)
+    static_assert(EF_S16_LO <= NJB && EF_S16_HI <= NJB, "issue positions must exist: 0 .. NJB");
     const int dpos = wave < 4 ? EF_S16_LO : EF_S16_HI;
     int64_t pend = -1;
     auto flush = [&](int pos) {

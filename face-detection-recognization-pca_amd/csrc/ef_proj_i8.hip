@@ -205,7 +205,9 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
     const int64_t nx = st + PNB;
     // the DMA into stage st's slot, at this wave's position of k-step 1 (the SYRK's stagger:
     // the two waves of a SIMD do not pay the pieces' issue cost at the same time)
-    const int dpos = wave < 4 ? EF_PROJ_LO : EF_PROJ_HI;
+    // (positions past the wave's last row block — IA is 2 for the TN = 128 tiles — clamp to it:
+    // every wave must issue its Q pieces each stage, or the vmcnt accounting breaks)
+    const int dpos = (wave < 4 ? EF_PROJ_LO : EF_PROJ_HI) < IA ? (wave < 4 ? EF_PROJ_LO : EF_PROJ_HI) : IA;
     auto at_pos = [&](int pos) {
       if (pos == dpos) issue(nx < nst ? nx : 0, (int)(nx % PNB));
     };

@@ -8,7 +8,7 @@ O=gpurun_out/$1
 mkdir -p $O
 # the C5 headline scan is the split-bf16 one (search_wide16_kernel); the fp32 wide kernel is
 # the bench's side leg (its r02 PMC summary stays in profiles/r02/pmc_summary_c5.json)
-B="bench.py --config c5 --steps 3 --warmup 1 --no-cpu --no-fit --no-split"
+B="bench.py --config c5 --steps 3 --warmup 1 --no-cpu --no-fit --no-split --no-image"
 R="search_wide16"
 timeout -k 10 300 python bench.py --config c5 --steps 5 --warmup 2 --no-cpu --no-fit > $O/bench.txt 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B > $O/t.txt 2>&1 || exit $?

@@ -18,7 +18,7 @@ step pytest 600 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovid
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step bench 600 python bench.py || exit $?
 [ "$2" = quick ] && { echo done >> $O/steps.log; exit 0; }
-B="bench.py --steps 5 --warmup 2 --no-cpu --no-fit"
+B="bench.py --steps 5 --warmup 2 --no-cpu --no-fit --no-c2 --no-c5 --no-image"
 step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $B || exit $?
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $B || exit $?
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $B || exit $?
