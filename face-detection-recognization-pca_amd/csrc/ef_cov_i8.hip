@@ -643,15 +643,25 @@ __global__ __launch_bounds__(256) void cov_finalize_kernel(const int* __restrict
   const __int128 nn = n;
   const __int128 q = gram ? (__int128)(((unsigned __int128)Q2[1] << 64) | Q2[0]) : 0;
   const double den = gram ? (double)n * (double)n * (double)(n - 1) : (double)n * (double)(n - 1);
+  // covariance numerator in int64 when it provably fits: |s| <= 128^2 n, |cvec| <= 128 n,
+  // so n s and cvec_i cvec_j are at most 2^14 n^2 <= 2^60 for n <= 2^23, and their
+  // difference fits; (double) of the same integer rounds identically from either width
+  // (the int128 form goes through a software conversion, the int64 one is one instruction)
+  const bool narrow = !gram && n <= (int64_t(1) << 23);
   for (int e = threadIdx.x; e < FB * FB; e += blockDim.x) {
     const int li = e / FB, lj = e & (FB - 1);
     const int64_t i = bi * FB + li, j = bj * FB + lj;
     if (i >= dim || j >= dim) continue;
     long long s = S64 ? S64[i * dim + j] : 0;
     for (int t = 0; t < nslab; ++t) s += slabs[(int64_t)t * dim * dim + i * dim + j];
-    const __int128 num = gram ? nn * nn * (__int128)s - nn * ((__int128)R[i] + R[j]) + q
-                              : nn * (__int128)s - (__int128)cvec[i] * cvec[j];
-    double v = (double)num / den;
+    double v;
+    if (narrow) {
+      v = (double)((long long)n * s - cvec[i] * cvec[j]) / den;
+    } else {
+      const __int128 num = gram ? nn * nn * (__int128)s - nn * ((__int128)R[i] + R[j]) + q
+                                : nn * (__int128)s - (__int128)cvec[i] * cvec[j];
+      v = (double)num / den;
+    }
     if (w) v *= w[i] * w[j];
     C[i * dim + j] = v;
     tr[lj][li] = v;

@@ -22,6 +22,8 @@
 // k > 80 (BASELINE.json config 3: k = 128; config 5: k = 512) and for direct solves of
 // moderate orders.  Quadratic convergence: a nearly diagonal input (warm subspace) needs
 // 2-3 sweeps.
+#include <cstdlib>
+
 #include "ef_linalg.hpp"
 
 namespace ef {
@@ -148,39 +150,106 @@ __device__ __forceinline__ Rot lds_rotation(const double (*S)[33], int r, int t)
   return R;
 }
 
-// One workgroup per block pair of round r: diagonalise S = G[P][P] (32 x 32) in LDS,
-// Z[pair] = the accumulated rotations.  256 threads: thread (t, u) owns the 2 x 2 block
-// {p_t, q_t} x {p_u, q_u} of each inner round (ping-pong S, one barrier per round).
-__global__ __launch_bounds__(256) void bj_solve_kernel(const double* __restrict__ G, double* __restrict__ Gout, int mp,
-                                                       int r, double* __restrict__ Zall, int* __restrict__ flag) {
-  const int nb = mp / BJ, pair = blockIdx.x;
+constexpr int BS = 2 * BJ;  // order of a pair problem
+typedef double Tile[BS][BS + 1];
+
+// (Z^T A)[a][b] and (X Z)[a][b] of 32 x 32 LDS tiles, k ascending: the one summation order
+// every product of a pair rotation uses (the solve's recomputed blocks equal the apply's)
+__device__ __forceinline__ double zt_dot(const Tile& Z, int a, const Tile& A, int b) {
+  double acc = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < BS; ++k) acc = fma(Z[k][a], A[k][b], acc);
+  return acc;
+}
+__device__ __forceinline__ double xz_dot(const Tile& X, int a, const Tile& Z, int b) {
+  double acc = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < BS; ++k) acc = fma(X[a][k], Z[k][b], acc);
+  return acc;
+}
+
+// the pair of round r holding block blk, and its half (0: the lower block of the pair)
+__device__ __forceinline__ void bj_locate(int r, int nb, int blk, int* pair, int* half) {
+  for (int t = 0; t < nb / 2; ++t) {
+    int a, b;
+    bj_pair(r, t, nb, &a, &b);
+    if (a == blk) *pair = t, *half = 0;
+    if (b == blk) *pair = t, *half = 1;
+  }
+}
+
+// Solve of round r, one workgroup per block pair: diagonalise S = G[P][P] (32 x 32) in LDS,
+// Zcur[pair] = the accumulated rotations, the diagonalised block into Gnext.  256 threads:
+// thread (t, u) owns the 2 x 2 block {p_t, q_t} x {p_u, q_u} of each inner round
+// (ping-pong S, one barrier per round).  S's diagonal 16-blocks come from Gcur (written
+// by the previous round's solve); with a pending apply (Zprev: the rotations of round rp,
+// not yet applied to Gcur's off-diagonal blocks) the two off-diagonal 16-blocks are
+// recomputed here from Gprev exactly as the apply computes them, so this round need not
+// wait for that apply.
+__device__ __forceinline__ void bj_solve_part(const double* __restrict__ Gprev, const double* Gcur,
+                                              double* __restrict__ Gnext, int mp, int r, int rp,
+                                              const double* __restrict__ Zprev, double* __restrict__ Zcur,
+                                              int* __restrict__ flag, int pair, Tile* sm) {
+  const int nb = mp / BJ;
   int I, J;
   bj_pair(r, pair, nb, &I, &J);
-  __shared__ double S[2][2 * BJ][33];
-  __shared__ double Z[2 * BJ][33];
+  Tile(&S)[2] = *reinterpret_cast<Tile(*)[2]>(sm);
+  Tile& Z = sm[2];
   __shared__ int any;
+  __shared__ Rot rot[BJ];
   const int tid = threadIdx.x;
+  int PI = 0, hI = 0, PJ = 0, hJ = 0;
+  if (Zprev) {
+    bj_locate(rp, nb, I, &PI, &hI);
+    bj_locate(rp, nb, J, &PJ, &hJ);
+  }
+  const bool own = !Zprev || PI == PJ;  // the off-diagonal blocks are final in Gcur
   if (tid == 0) any = 0;
-  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+  for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
-    S[0][a][b] = G[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)];
+    if (own || (a < BJ) == (b < BJ)) S[0][a][b] = Gcur[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)];
     Z[a][b] = a == b ? 1.0 : 0.0;
+  }
+  if (!own) {
+    Tile &A = sm[3], &ZP = sm[4], &ZQ = sm[5], &T = sm[6];
+    for (int side = 0; side < 2; ++side) {  // rows I, columns J; then rows J, columns I
+      const int Pr = side ? PJ : PI, hr = side ? hJ : hI, Pc = side ? PI : PJ, hc = side ? hI : hJ;
+      int IP, JP, IQ, JQ;
+      bj_pair(rp, Pr, nb, &IP, &JP);
+      bj_pair(rp, Pc, nb, &IQ, &JQ);
+      __syncthreads();  // the scratch tiles are free
+      const double* zp = Zprev + (int64_t)Pr * BS * BS;
+      const double* zq = Zprev + (int64_t)Pc * BS * BS;
+      for (int e = tid; e < BS * BS; e += 256) {
+        const int a = e >> 5, b = e & 31;
+        A[a][b] = Gprev[(int64_t)bj_index(IP, JP, a) * mp + bj_index(IQ, JQ, b)];
+        ZP[a][b] = zp[e];
+        ZQ[a][b] = zq[e];
+      }
+      __syncthreads();
+      for (int e = tid; e < BJ * BS; e += 256) {  // T = Z_P^T A, the rows of half hr
+        const int a = BJ * hr + (e >> 5), b = e & 31;
+        T[a][b] = zt_dot(ZP, a, A, b);
+      }
+      __syncthreads();
+      const int a = BJ * hr + (tid >> 4), b = BJ * hc + (tid & 15);
+      S[0][(side ? BJ : 0) + (tid >> 4)][(side ? 0 : BJ) + (tid & 15)] = xz_dot(T, a, ZQ, b);
+    }
   }
   __syncthreads();
   // outer convergence: any off-diagonal entry above 1e-12 of its diagonal scale
-  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+  for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
     if (a != b && fabs(S[0][a][b]) > 1e-12 * sqrt(fabs(S[0][a][a] * S[0][b][b]))) any = 1;
   }
   __syncthreads();
   if (any) *flag = 1;
   const int t = tid >> 4, u = tid & 15;
-  __shared__ Rot rot[BJ];
   int cur = 0;
   for (int sw = 0; sw < kInnerSweeps && any; ++sw) {
     __syncthreads();
     if (tid == 0) any = 0;
-    for (int rr = 0; rr < 2 * BJ - 1; ++rr) {
+    for (int rr = 0; rr < BS - 1; ++rr) {
       // the round's 16 rotations, computed once (the fp64 sqrt/div chain is the round's latency)
       if (tid < BJ) {
         const Rot R = lds_rotation(S[cur], rr, tid);
@@ -219,34 +288,34 @@ __global__ __launch_bounds__(256) void bj_solve_kernel(const double* __restrict_
   }
   // the diagonalised pair block goes out as computed (rotated pivots exactly zero), so
   // rounding noise of a Z^T S Z product never re-triggers the convergence flag
-  double* Zp = Zall + (int64_t)pair * 4 * BJ * BJ;
-  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+  double* Zp = Zcur + (int64_t)pair * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
     Zp[e] = Z[a][b];
-    Gout[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)] = S[cur][a][b];
+    Gnext[(int64_t)bj_index(I, J, a) * mp + bj_index(I, J, b)] = S[cur][a][b];
   }
 }
 
-// Gout[P][Q] = Z_P^T Gin[P][Q] Z_Q for every pair of block pairs (blockIdx.y < npair), and
-// V[R][Q] <- V[R][Q] Z_Q for 32-row tiles R of V (blockIdx.y >= npair; in place: a tile is
-// read completely before it is written).
-__global__ __launch_bounds__(256) void bj_apply_kernel(const double* __restrict__ Gin, double* __restrict__ Gout,
-                                                       double* __restrict__ V, int mp, int r,
-                                                       const double* __restrict__ Zall) {
+// Apply of round rp: Gout[P][Q] = Z_P^T Gin[P][Q] Z_Q for pair q's columns and pair py's
+// rows (py < npair; the pair's own block P = Q is the solve's), or V[R][Q] <- V[R][Q] Z_Q
+// for the 32-row tile R = py - npair of V (in place: a tile is read completely before it
+// is written).
+__device__ __forceinline__ void bj_apply_part(const double* __restrict__ Gin, double* Gout, double* __restrict__ V,
+                                              int mp, int rp, const double* __restrict__ Zall, int q, int py,
+                                              Tile* sm) {
   const int nb = mp / BJ, npair = nb / 2;
-  const int q = blockIdx.x, py = blockIdx.y;
   int IQ, JQ;
-  bj_pair(r, q, nb, &IQ, &JQ);
-  __shared__ double A[2 * BJ][33], T[2 * BJ][33], ZP[2 * BJ][33], ZQ[2 * BJ][33];
+  bj_pair(rp, q, nb, &IQ, &JQ);
+  Tile &A = sm[0], &T = sm[1], &ZP = sm[2], &ZQ = sm[3];
   const int tid = threadIdx.x;
   const bool isv = py >= npair;
-  if (!isv && py == q) return;  // the pair's own block: written by bj_solve_kernel
+  if (!isv && py == q) return;
   int IP = 0, JP = 0;
-  if (!isv) bj_pair(r, py, nb, &IP, &JP);
-  const int64_t r0 = (int64_t)(py - npair) * 2 * BJ;  // V row tile
-  const double* zq = Zall + (int64_t)q * 4 * BJ * BJ;
-  const double* zp = Zall + (int64_t)py * 4 * BJ * BJ;
-  for (int e = tid; e < 4 * BJ * BJ; e += 256) {
+  if (!isv) bj_pair(rp, py, nb, &IP, &JP);
+  const int64_t r0 = (int64_t)(py - npair) * BS;  // V row tile
+  const double* zq = Zall + (int64_t)q * BS * BS;
+  const double* zp = Zall + (int64_t)py * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
     const int64_t col = bj_index(IQ, JQ, b);
     A[a][b] = isv ? V[(r0 + a) * mp + col] : Gin[(int64_t)bj_index(IP, JP, a) * mp + col];
@@ -257,28 +326,58 @@ __global__ __launch_bounds__(256) void bj_apply_kernel(const double* __restrict_
   const int a0 = tid >> 5, b = tid & 31;  // thread: rows a0 + 8j, column b
   if (!isv) {  // T = Z_P^T A
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = a0 + 8 * j;
-      double acc = 0.0;
-#pragma unroll 8
-      for (int k = 0; k < 2 * BJ; ++k) acc += ZP[k][a] * A[k][b];
-      T[a][b] = acc;
-    }
+    for (int j = 0; j < 4; ++j) T[a0 + 8 * j][b] = zt_dot(ZP, a0 + 8 * j, A, b);
     __syncthreads();
   }
-  const double (*X)[33] = isv ? A : T;
+  const Tile& X = isv ? A : T;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int a = a0 + 8 * j;
-    double acc = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < 2 * BJ; ++k) acc += X[a][k] * ZQ[k][b];
+    const double v = xz_dot(X, a, ZQ, b);
     const int64_t col = bj_index(IQ, JQ, b);
     if (isv)
-      V[(r0 + a) * mp + col] = acc;
+      V[(r0 + a) * mp + col] = v;
     else
-      Gout[(int64_t)bj_index(IP, JP, a) * mp + col] = acc;
+      Gout[(int64_t)bj_index(IP, JP, a) * mp + col] = v;
   }
+}
+
+// One launch per round g of the block method: workgroups [0, nsolve) solve round r (the
+// pairs of G^(g)), the others apply round rp's rotations (Zprev) to G^(g-1) -> the
+// off-diagonal pair blocks of G^(g) in Gcur, and to V.  Neither half waits for the other:
+// the solve recomputes the two off-diagonal blocks it needs (bj_solve_part), so a round
+// costs one solve instead of a solve plus an apply, in one launch instead of two.  G^(g-1),
+// G^(g), G^(g+1) rotate through three buffers (the apply still reads G^(g-1) while the
+// solve writes G^(g+1)); Z ping-pongs.
+__global__ __launch_bounds__(256) void bj_round_kernel(const double* __restrict__ Gprev, double* Gcur,
+                                                       double* __restrict__ Gnext, double* __restrict__ V, int mp,
+                                                       int r, int rp, int nsolve, const double* __restrict__ Zprev,
+                                                       double* __restrict__ Zcur, int* __restrict__ flag) {
+  __shared__ Tile sm[7];
+  const int b = blockIdx.x;
+  if (b < nsolve) {
+    bj_solve_part(Gprev, Gcur, Gnext, mp, r, rp, Zprev, Zcur, flag, b, sm);
+    return;
+  }
+  const int npair = mp / BS, a = b - nsolve;
+  bj_apply_part(Gprev, Gcur, V, mp, rp, Zprev, a % npair, a / npair, sm);
+}
+
+// G^(-1) = G^(0) = the symmetrised input in buffers 2 and 0, V = I, Z^(-1) = I: the first
+// round's pending apply is an exact identity
+__global__ void bj_init_kernel(const double* __restrict__ A, int m, int64_t lda, int mp, double* __restrict__ G0,
+                               double* __restrict__ G2, double* __restrict__ V, double* __restrict__ Zid) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < (int64_t)(mp / BS) * BS * BS) {
+    const int w = (int)(e % (BS * BS));
+    Zid[e] = (w >> 5) == (w & 31) ? 1.0 : 0.0;
+  }
+  if (e >= (int64_t)mp * mp) return;
+  const int i = (int)(e / mp), j = (int)(e - (e / mp) * mp);
+  const double g = (i < m && j < m) ? 0.5 * (A[(int64_t)i * lda + j] + A[(int64_t)j * lda + i]) : 0.0;
+  G0[e] = g;
+  G2[e] = g;
+  V[e] = i == j ? 1.0 : 0.0;
 }
 
 // descending order (ties -> lower index first); evecs[r][rank] = V[r][i]
@@ -305,46 +404,40 @@ static int padded_order(int m) { return m >= kBlockJacobiMin ? (m + 2 * BJ - 1) 
 
 size_t jacobi_big_work_elems(int m) {
   const int64_t mp = padded_order(m);
-  return (size_t)(3 * mp * mp + 2 * BJ * mp) + 64;  // G ping-pong, V, pair rotations
+  // scalar: G ping-pong + V; block: G^(g-1), G^(g), G^(g+1), V, two sets of pair rotations
+  return (size_t)(4 * mp * mp + 4 * BJ * mp) + 64;
 }
 
-// One sweep (mp - 1 rounds) per graph; two graphs for the two ping-pong parities.
+static inline int mod_pos(int x, int n) { return ((x % n) + n) % n; }
+
 void JacobiBig::destroy() {
-  for (auto& g : exec)
+  for (auto& g : exec) {
     if (g) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
-  exec[0] = exec[1] = nullptr;
+    g = nullptr;
+  }
 }
 
+// Graphs: one sweep per graph.  Scalar path: two graphs for the two ping-pong parities.
+// Block path: one graph per phase (first global round of the sweep) mod 6 — the three G
+// buffers and the two Z buffers cycle with the global round count.
 hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t capture) {
   destroy();
   m = m_;
   mp = padded_order(m);
   block = m >= kBlockJacobiMin;
+  fused = true;
+#ifdef EF_DIAGNOSTICS  // EF_BJ_FUSED=0: the solve and the apply of a round as two launches (A/B)
+  if (const char* e = getenv("EF_BJ_FUSED")) fused = atoi(e) != 0;
+#endif
   work = work_;
   flag = flag_;
-  double* G[2] = {work, work + (int64_t)mp * mp};
-  double* V = work + 2 * (int64_t)mp * mp;
-  const int np = mp / 2;
-  const int64_t threads = (int64_t)np * np + (int64_t)mp * np;
-  const dim3 grid((unsigned)((threads + 255) / 256));
-  const int nb = mp / BJ, npair = nb / 2;
-  double* Z = work + 3 * (int64_t)mp * mp;
-  for (int par = 0; par < 2; ++par) {
+  const int64_t mm = (int64_t)mp * mp;
+  const int R = rounds();
+  auto capture_graph = [&](int slot, auto&& body) -> hipError_t {
     hipError_t e = hipStreamBeginCapture(capture, hipStreamCaptureModeRelaxed);
     if (e != hipSuccess) return e;
     (void)hipMemsetAsync(flag, 0, sizeof(int), capture);
-    int cur = par;
-    for (int r = 0; r < rounds(); ++r) {
-      if (block) {
-        hipLaunchKernelGGL(bj_solve_kernel, dim3((unsigned)npair), dim3(256), 0, capture, G[cur], G[cur ^ 1], mp, r, Z,
-                           flag);
-        hipLaunchKernelGGL(bj_apply_kernel, dim3((unsigned)npair, (unsigned)(npair + mp / (2 * BJ))), dim3(256), 0,
-                           capture, G[cur], G[cur ^ 1], V, mp, r, Z);
-      } else {
-        hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, capture, G[cur], G[cur ^ 1], V, mp, r, flag);
-      }
-      cur ^= 1;
-    }
+    body();
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(capture, &g);
     if (e != hipSuccess) return e;
@@ -352,23 +445,83 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
     e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return e;
-    exec[par] = x;
+    exec[slot] = x;
+    return hipSuccess;
+  };
+  if (!block) {
+    double* G[2] = {work, work + mm};
+    double* V = work + 2 * mm;
+    const int np = mp / 2;
+    const int64_t threads = (int64_t)np * np + (int64_t)mp * np;
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    for (int par = 0; par < 2; ++par) {
+      hipError_t e = capture_graph(par, [&] {
+        int cur = par;
+        for (int r = 0; r < R; ++r) {
+          hipLaunchKernelGGL(jbig_round_kernel, grid, dim3(256), 0, capture, G[cur], G[cur ^ 1], V, mp, r, flag);
+          cur ^= 1;
+        }
+      });
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  double* G[3] = {work, work + mm, work + 2 * mm};
+  double* V = work + 3 * mm;
+  double* Z[2] = {work + 4 * mm, work + 4 * mm + (int64_t)BS * mp};
+  const int npair = mp / BS;
+  const unsigned napply = (unsigned)(npair * (npair + mp / BS));
+  if (!fused) {
+    for (int par = 0; par < 2; ++par) {
+      hipError_t e = capture_graph(par, [&] {
+        int cur = par;
+        for (int r = 0; r < R; ++r) {
+          hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair), dim3(256), 0, capture, G[cur], G[cur],
+                             G[cur ^ 1], V, mp, r, r, npair, nullptr, Z[0], flag);
+          hipLaunchKernelGGL(bj_round_kernel, dim3(napply), dim3(256), 0, capture, G[cur], G[cur ^ 1], G[cur ^ 1],
+                             V, mp, r, r, 0, Z[0], Z[1], flag);
+          cur ^= 1;
+        }
+      });
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  for (int k = 0; k < 6; ++k) {
+    const int ph = (k * R) % 6;
+    if (exec[ph]) continue;
+    hipError_t e = capture_graph(ph, [&] {
+      for (int r = 0; r < R; ++r) {
+        const int g = ph + r;
+        hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair + napply), dim3(256), 0, capture,
+                           G[mod_pos(g - 1, 3)], G[g % 3], G[(g + 1) % 3], V, mp, r, r == 0 ? R - 1 : r - 1, npair,
+                           Z[mod_pos(g - 1, 2)], Z[g % 2], flag);
+      }
+    });
+    if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
 int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv,
                      int max_sweeps, int* sweeps_out, hipError_t* err) {
-  double* G[2] = {work, work + (int64_t)mp * mp};
-  double* V = work + 2 * (int64_t)mp * mp;
-  const int64_t tot = (int64_t)mp * mp;
-  hipLaunchKernelGGL(jbig_init_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G[0], V);
-  int cur = 0, sweep = 0;
+  const int64_t mm = (int64_t)mp * mp;
+  const int R = rounds();
+  double* G[3] = {work, work + mm, work + 2 * mm};
+  double* V = work + (block ? 3 : 2) * mm;
+  double* Z[2] = {work + 4 * mm, work + 4 * mm + (int64_t)BS * mp};
+  if (block)
+    hipLaunchKernelGGL(bj_init_kernel, dim3((unsigned)((mm + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G[0], G[2],
+                       V, Z[1]);
+  else
+    hipLaunchKernelGGL(jbig_init_kernel, dim3((unsigned)((mm + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G[0], V);
+  const bool three = block && fused;
+  int cur = 0, sweep = 0;  // cur: the ping-pong parity, or (three buffers) the global round count
   bool converged = false;
   for (; sweep < max_sweeps; ++sweep) {
-    *err = hipGraphLaunch(static_cast<hipGraphExec_t>(exec[cur]), s);
+    *err = hipGraphLaunch(static_cast<hipGraphExec_t>(exec[three ? cur % 6 : cur]), s);
     if (*err != hipSuccess) return -1;
-    cur ^= rounds() & 1;  // an odd number of rounds swaps the buffers
+    cur = three ? cur + R : cur ^ (R & 1);  // an odd number of rounds swaps the ping-pong buffers
     int hflag = 0;
     *err = hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
     if (*err == hipSuccess) *err = hipStreamSynchronize(s);
@@ -378,7 +531,15 @@ int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals,
       break;
     }
   }
-  hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, G[cur], V, m, mp, evals, evecs, ldv);
+  const double* Gfinal = G[cur];
+  if (three) {
+    // the last round's rotations still go to V (and to G's off-diagonal blocks)
+    const int npair = mp / BS, gl = cur - 1;
+    hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)(npair * (npair + mp / BS))), dim3(256), 0, s, G[gl % 3],
+                       G[cur % 3], G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag);
+    Gfinal = G[cur % 3];
+  }
+  hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, Gfinal, V, m, mp, evals, evecs, ldv);
   *err = hipGetLastError();
   if (*err != hipSuccess) return -1;
   if (sweeps_out) *sweeps_out = sweep + 1;

@@ -121,10 +121,11 @@ size_t jacobi_big_work_elems(int m);
 struct JacobiBig {
   int m = 0, mp = 0;
   bool block = false;  // block-Jacobi rounds (orders >= 128)
+  bool fused = true;   // block path: a round's solve and the previous round's apply in one launch
   int rounds() const { return block ? mp / 16 - 1 : mp - 1; }
   double* work = nullptr;
   int* flag = nullptr;
-  void* exec[2] = {nullptr, nullptr};
+  void* exec[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipError_t init(int m, double* work, int* flag, hipStream_t capture);
   int solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv, int max_sweeps,
             int* sweeps_out, hipError_t* err);
