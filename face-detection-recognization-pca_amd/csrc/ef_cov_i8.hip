@@ -675,6 +675,64 @@ __global__ __launch_bounds__(256) void cov_finalize_kernel(const int* __restrict
   }
 }
 
+// cov_finalize_kernel for dim % 4 == 0: four columns per thread — 16-byte slab loads (four
+// times the bytes in flight per load instruction: the one-int form ran at ~2 TB/s) and
+// 32-byte row stores; the per-element arithmetic is the same expression as above.
+__global__ __launch_bounds__(256) void cov_finalize4_kernel(const int* __restrict__ slabs, int nslab,
+                                                            const long long* __restrict__ S64, int64_t dim, int64_t n,
+                                                            int gram, const long long* __restrict__ cvec,
+                                                            const long long* __restrict__ R,
+                                                            const unsigned long long* __restrict__ Q2,
+                                                            const double* __restrict__ w, double* __restrict__ C) {
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bi > bj) return;
+  __shared__ double tr[FB][FB + 1];
+  const __int128 nn = n;
+  const __int128 q = gram ? (__int128)(((unsigned __int128)Q2[1] << 64) | Q2[0]) : 0;
+  const double den = gram ? (double)n * (double)n * (double)(n - 1) : (double)n * (double)(n - 1);
+  const bool narrow = !gram && n <= (int64_t(1) << 23);
+  for (int e = threadIdx.x; e < FB * FB / 4; e += blockDim.x) {
+    const int li = e >> 4, lj = (e & 15) * 4;
+    const int64_t i = bi * FB + li, j = bj * FB + lj;
+    if (i >= dim || j >= dim) continue;
+    long long s[4] = {0, 0, 0, 0};
+    if (S64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] = S64[i * dim + j + u];
+    }
+    for (int t = 0; t < nslab; ++t) {
+      const int4 v = *reinterpret_cast<const int4*>(slabs + (int64_t)t * dim * dim + i * dim + j);
+      s[0] += v.x;
+      s[1] += v.y;
+      s[2] += v.z;
+      s[3] += v.w;
+    }
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t jj = j + u;
+      if (narrow) {
+        v[u] = (double)((long long)n * s[u] - cvec[i] * cvec[jj]) / den;
+      } else {
+        const __int128 num = gram ? nn * nn * (__int128)s[u] - nn * ((__int128)R[i] + R[jj]) + q
+                                  : nn * (__int128)s[u] - (__int128)cvec[i] * cvec[jj];
+        v[u] = (double)num / den;
+      }
+      if (w) v[u] *= w[i] * w[jj];
+      tr[lj + u][li] = v[u];
+    }
+    *reinterpret_cast<double2*>(C + i * dim + j) = make_double2(v[0], v[1]);
+    *reinterpret_cast<double2*>(C + i * dim + j + 2) = make_double2(v[2], v[3]);
+  }
+  if (bi == bj) return;
+  __syncthreads();
+  for (int e = threadIdx.x; e < FB * FB; e += blockDim.x) {
+    const int lj = e / FB, li = e & (FB - 1);
+    const int64_t i = bi * FB + li, j = bj * FB + lj;
+    if (i < dim && j < dim) C[j * dim + i] = tr[lj][li];
+  }
+}
+
 // ---------------------------------------------------------------- host side
 int64_t cov_i8_kpad(int64_t K) { return (K + YK - 1) / YK * YK; }
 
@@ -829,9 +887,13 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
     hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)n), dim3(256), 0, s, At, n, d, cvec, R);
     hipLaunchKernelGGL(sumsq128_kernel, dim3(1), dim3(256), 0, s, cvec, d, Q2);
   }
-  hipLaunchKernelGGL(cov_finalize_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s,
-                     p.passes > 1 ? nullptr : slabs, p.passes > 1 ? 0 : p.splits,
-                     p.passes > 1 ? S64 : nullptr, dim, n, gram ? 1 : 0, cvec, R, Q2, w, C);
+  bool vec4 = dim % 4 == 0;
+#ifdef EF_DIAGNOSTICS
+  if (const char* v = std::getenv("EF_FINALIZE4")) vec4 = vec4 && std::atoi(v) != 0;
+#endif
+  hipLaunchKernelGGL(vec4 ? cov_finalize4_kernel : cov_finalize_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256),
+                     0, s, p.passes > 1 ? nullptr : slabs, p.passes > 1 ? 0 : p.splits, p.passes > 1 ? S64 : nullptr,
+                     dim, n, gram ? 1 : 0, cvec, R, Q2, w, C);
   return hipGetLastError();
 }
 

@@ -1,7 +1,9 @@
-"""Block-Jacobi fused rounds (EF_BJ_FUSED, diagnostic build): the one-launch round (the
-solve recomputing its off-diagonal blocks, the previous round's apply alongside) against
-the two-launch round.  Same arithmetic, so the fits must agree bit for bit; then the C3
-fit time of both, alternated.  usage: EF_LIB_VARIANT=diag python tools/bj_fused_check.py"""
+"""A/B of a fit-path diagnostic switch whose two settings must give bit-identical fits
+(diagnostic build): EF_BJ_FUSED (block-Jacobi rounds as one launch: the solve recomputing
+its off-diagonal blocks, the previous round's apply alongside, vs two launches),
+EF_FINALIZE4 (the 4-column covariance finalize vs one column per thread).  Four fit
+shapes must agree bit for bit; then the C3 fit time of both settings, alternated.
+usage: EF_LIB_VARIANT=diag python tools/bj_fused_check.py [VAR]   (default EF_BJ_FUSED)"""
 import os
 import sys
 import time
@@ -18,10 +20,11 @@ from eigenface import Engine, synth  # noqa: E402
 torch.cuda.set_device(0)
 eng = Engine(0)
 rng = np.random.default_rng(3)
+VAR = sys.argv[1] if len(sys.argv) > 1 else "EF_BJ_FUSED"
 
 
 def fit(X, k, std, fused):
-    os.environ["EF_BJ_FUSED"] = str(fused)
+    os.environ[VAR] = str(fused)
     r = eng.fit(X, k, standardize=std, projection=False)
     return np.asarray(r.components), np.asarray(r.eigenvalues), r.iters
 
@@ -61,7 +64,7 @@ res = {0: [], 1: []}
 comp = {}
 for rep in range(3):
     for fused in (1, 0):
-        os.environ["EF_BJ_FUSED"] = str(fused)
+        os.environ[VAR] = str(fused)
         torch.cuda.synchronize()
         t = time.perf_counter()
         rr = eng.fit(X, 128, standardize=True, projection=False)
@@ -69,7 +72,7 @@ for rep in range(3):
         comp[fused] = rr.components.cpu().numpy() if hasattr(rr.components, "cpu") else np.asarray(rr.components)
 same = np.array_equal(comp[0], comp[1])
 ok &= same
-print(f"C3 fit s: fused {[round(x, 4) for x in res[1]]} two-launch {[round(x, 4) for x in res[0]]} "
+print(f"C3 fit s: {VAR}=1 {[round(x, 4) for x in res[1]]} {VAR}=0 {[round(x, 4) for x in res[0]]} "
       f"median {np.median(res[1]):.4f} vs {np.median(res[0]):.4f}; identical={same}", flush=True)
 eng.close()
 print("ALL_IDENTICAL" if ok else "MISMATCH", flush=True)
