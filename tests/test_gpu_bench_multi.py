@@ -49,6 +49,22 @@ def test_bench_two_ranks_one_gpu(metric):
           f"({100 * rec['exchange_share_of_step']:.1f} %)")
 
 
+@pytest.mark.parametrize("ranks,gallery", [(4, 200_000), (3, 200_003)])
+def test_bench_more_ranks_one_gpu(ranks, gallery):
+    """Rehearsal of the driver's N = 4 run (and an uneven 3-way split: shards of 66667 /
+    66668 rows, the probe slices 1366 / 1365) on the one card: every rank's keys agree and
+    every planted probe finds its row across the shard boundaries."""
+    r = _run(["--gpus", str(ranks), "--backend", "gloo", "--gallery", str(gallery), "--no-cpu", "--no-fit",
+              "--no-image", "--no-c2", "--no-split", "--steps", "2", "--warmup", "1", "--repeats", "1",
+              "--launch-timeout", "240"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == ranks
+    assert rec["check"]["planted_match"] == 1.0
+    assert rec["check"]["ranks_agree"] is True
+    assert rec["config"]["rows_per_rank"] in (gallery // ranks, -(-gallery // ranks))
+
+
 def test_bench_rejects_gpus_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
