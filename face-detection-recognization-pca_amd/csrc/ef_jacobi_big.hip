@@ -125,7 +125,19 @@ __device__ __forceinline__ void bj_pair(int r, int t, int nb, int* I, int* J) {
   *J = q;
 }
 
-// rotation of LDS pair (p, q) of a 32 x 32 matrix (row stride 33), same rule as pair_rotation
+// 1/x and 1/sqrt(x) (x >= 1 for the latter) from v_rcp_f64 / v_rsq_f64 and two Newton steps
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = fma(y, fma(-x, y, 1.0), y);
+  return fma(y, fma(-x, y, 1.0), y);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
+  return fma(0.5 * y, fma(-x * y, y, 1.0), y);
+}
+
+// rotation of LDS pair (p, q) of a 32 x 32 matrix (row stride 33), the rule of pair_rotation
 __device__ __forceinline__ Rot lds_rotation(const double (*S)[33], int r, int t) {
   Rot R;
   int p = circle_pos(t, r, 2 * BJ), q = circle_pos(2 * BJ - 1 - t, r, 2 * BJ);
@@ -139,11 +151,20 @@ __device__ __forceinline__ Rot lds_rotation(const double (*S)[33], int r, int t)
     R.c = 1.0;
     R.s = 0.0;
   } else {
-    const double theta = (aqq - app) / (2.0 * apq);
-    double tt = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-    if (fabs(theta) > 1e150) tt = 0.5 / fabs(theta);
+    // the rule's quotients and roots from the hardware reciprocal / reciprocal square
+    // root, each refined by two Newton steps (~1 ulp): the 16 rotations of an inner round
+    // are its serial latency (a chain of three IEEE divisions and two square roots before)
+    const double theta = (aqq - app) * rcp_nr(2.0 * apq);
+    const double at = fabs(theta);
+    double tt;
+    if (at > 1e150) {
+      tt = 0.5 * rcp_nr(at);
+    } else {
+      const double u = fma(theta, theta, 1.0);
+      tt = rcp_nr(at + u * rsq_nr(u));
+    }
     if (theta < 0.0) tt = -tt;
-    R.c = 1.0 / sqrt(tt * tt + 1.0);
+    R.c = rsq_nr(fma(tt, tt, 1.0));
     R.s = tt * R.c;
     R.on = true;
   }
@@ -189,7 +210,8 @@ __device__ __forceinline__ void bj_locate(int r, int nb, int blk, int* pair, int
 __device__ __forceinline__ void bj_solve_part(const double* __restrict__ Gprev, const double* Gcur,
                                               double* __restrict__ Gnext, int mp, int r, int rp,
                                               const double* __restrict__ Zprev, double* __restrict__ Zcur,
-                                              int* __restrict__ flag, int pair, Tile* sm) {
+                                              int* __restrict__ flag, const double* __restrict__ tolp, int pair,
+                                              Tile* sm) {
   const int nb = mp / BJ;
   int I, J;
   bj_pair(r, pair, nb, &I, &J);
@@ -237,10 +259,12 @@ __device__ __forceinline__ void bj_solve_part(const double* __restrict__ Gprev, 
     }
   }
   __syncthreads();
-  // outer convergence: any off-diagonal entry above 1e-12 of its diagonal scale
+  // outer convergence: any off-diagonal entry above tol (1e-12, or the looser tolerance
+  // of a coarse-phase Rayleigh-Ritz solve) of its diagonal scale
+  const double tol = *tolp;
   for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
-    if (a != b && fabs(S[0][a][b]) > 1e-12 * sqrt(fabs(S[0][a][a] * S[0][b][b]))) any = 1;
+    if (a != b && fabs(S[0][a][b]) > tol * sqrt(fabs(S[0][a][a] * S[0][b][b]))) any = 1;
   }
   __syncthreads();
   if (any) *flag = 1;
@@ -352,16 +376,19 @@ __device__ __forceinline__ void bj_apply_part(const double* __restrict__ Gin, do
 __global__ __launch_bounds__(256) void bj_round_kernel(const double* __restrict__ Gprev, double* Gcur,
                                                        double* __restrict__ Gnext, double* __restrict__ V, int mp,
                                                        int r, int rp, int nsolve, const double* __restrict__ Zprev,
-                                                       double* __restrict__ Zcur, int* __restrict__ flag) {
+                                                       double* __restrict__ Zcur, int* __restrict__ flag,
+                                                       const double* __restrict__ tolp) {
   __shared__ Tile sm[7];
   const int b = blockIdx.x;
   if (b < nsolve) {
-    bj_solve_part(Gprev, Gcur, Gnext, mp, r, rp, Zprev, Zcur, flag, b, sm);
+    bj_solve_part(Gprev, Gcur, Gnext, mp, r, rp, Zprev, Zcur, flag, tolp, b, sm);
     return;
   }
   const int npair = mp / BS, a = b - nsolve;
   bj_apply_part(Gprev, Gcur, V, mp, rp, Zprev, a % npair, a / npair, sm);
 }
+
+__global__ void set_scalar_kernel(double* p, double v) { *p = v; }
 
 // G^(-1) = G^(0) = the symmetrised input in buffers 2 and 0, V = I, Z^(-1) = I: the first
 // round's pending apply is an exact identity
@@ -405,7 +432,7 @@ static int padded_order(int m) { return m >= kBlockJacobiMin ? (m + 2 * BJ - 1) 
 size_t jacobi_big_work_elems(int m) {
   const int64_t mp = padded_order(m);
   // scalar: G ping-pong + V; block: G^(g-1), G^(g), G^(g+1), V, two sets of pair rotations
-  return (size_t)(4 * mp * mp + 4 * BJ * mp) + 64;
+  return (size_t)(4 * mp * mp + 4 * BJ * mp) + 64;  // + the tolerance scalar
 }
 
 static inline int mod_pos(int x, int n) { return ((x % n) + n) % n; }
@@ -469,6 +496,7 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
   double* G[3] = {work, work + mm, work + 2 * mm};
   double* V = work + 3 * mm;
   double* Z[2] = {work + 4 * mm, work + 4 * mm + (int64_t)BS * mp};
+  double* tolv = work + 4 * mm + 2 * (int64_t)BS * mp;  // the solve's tolerance (set per solve)
   const int npair = mp / BS;
   const unsigned napply = (unsigned)(npair * (npair + mp / BS));
   if (!fused) {
@@ -477,9 +505,9 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
         int cur = par;
         for (int r = 0; r < R; ++r) {
           hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair), dim3(256), 0, capture, G[cur], G[cur],
-                             G[cur ^ 1], V, mp, r, r, npair, nullptr, Z[0], flag);
+                             G[cur ^ 1], V, mp, r, r, npair, nullptr, Z[0], flag, tolv);
           hipLaunchKernelGGL(bj_round_kernel, dim3(napply), dim3(256), 0, capture, G[cur], G[cur ^ 1], G[cur ^ 1],
-                             V, mp, r, r, 0, Z[0], Z[1], flag);
+                             V, mp, r, r, 0, Z[0], Z[1], flag, tolv);
           cur ^= 1;
         }
       });
@@ -495,7 +523,7 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
         const int g = ph + r;
         hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair + napply), dim3(256), 0, capture,
                            G[mod_pos(g - 1, 3)], G[g % 3], G[(g + 1) % 3], V, mp, r, r == 0 ? R - 1 : r - 1, npair,
-                           Z[mod_pos(g - 1, 2)], Z[g % 2], flag);
+                           Z[mod_pos(g - 1, 2)], Z[g % 2], flag, tolv);
       }
     });
     if (e != hipSuccess) return e;
@@ -504,12 +532,14 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
 }
 
 int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv,
-                     int max_sweeps, int* sweeps_out, hipError_t* err) {
+                     int max_sweeps, int* sweeps_out, hipError_t* err, double tol) {
   const int64_t mm = (int64_t)mp * mp;
   const int R = rounds();
   double* G[3] = {work, work + mm, work + 2 * mm};
   double* V = work + (block ? 3 : 2) * mm;
   double* Z[2] = {work + 4 * mm, work + 4 * mm + (int64_t)BS * mp};
+  double* tolv = work + 4 * mm + 2 * (int64_t)BS * mp;
+  if (block) hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(1), 0, s, tolv, tol);
   if (block)
     hipLaunchKernelGGL(bj_init_kernel, dim3((unsigned)((mm + 255) / 256)), dim3(256), 0, s, A, m, lda, mp, G[0], G[2],
                        V, Z[1]);
@@ -536,7 +566,7 @@ int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals,
     // the last round's rotations still go to V (and to G's off-diagonal blocks)
     const int npair = mp / BS, gl = cur - 1;
     hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)(npair * (npair + mp / BS))), dim3(256), 0, s, G[gl % 3],
-                       G[cur % 3], G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag);
+                       G[cur % 3], G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag, tolv);
     Gfinal = G[cur % 3];
   }
   hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, Gfinal, V, m, mp, evals, evecs, ldv);

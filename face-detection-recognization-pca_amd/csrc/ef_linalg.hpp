@@ -127,8 +127,10 @@ struct JacobiBig {
   int* flag = nullptr;
   void* exec[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipError_t init(int m, double* work, int* flag, hipStream_t capture);
+  // tol: a sweep in which no off-diagonal entry exceeds tol of its diagonal scale ends the
+  // solve (block path; the scalar rounds always use 1e-12)
   int solve(hipStream_t s, const double* A, int64_t lda, double* evals, double* evecs, int64_t ldv, int max_sweeps,
-            int* sweeps_out, hipError_t* err);
+            int* sweeps_out, hipError_t* err, double tol = 1e-12);
   void destroy();
   ~JacobiBig() { destroy(); }
 };
