@@ -125,18 +125,6 @@ __device__ __forceinline__ void bj_pair(int r, int t, int nb, int* I, int* J) {
   *J = q;
 }
 
-// 1/x and 1/sqrt(x) (x >= 1 for the latter) from v_rcp_f64 / v_rsq_f64 and two Newton steps
-__device__ __forceinline__ double rcp_nr(double x) {
-  double y = __builtin_amdgcn_rcp(x);
-  y = fma(y, fma(-x, y, 1.0), y);
-  return fma(y, fma(-x, y, 1.0), y);
-}
-__device__ __forceinline__ double rsq_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
-  return fma(0.5 * y, fma(-x * y, y, 1.0), y);
-}
-
 // rotation of LDS pair (p, q) of a 32 x 32 matrix (row stride 33), the rule of pair_rotation
 __device__ __forceinline__ Rot lds_rotation(const double (*S)[33], int r, int t) {
   Rot R;

@@ -634,6 +634,7 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
                                                         int* __restrict__ info) {
   __shared__ double col[2][kCholInvMax];  // phase 1: column t; phase 2: row t of X
   __shared__ double sq[kCholInvMax];      // diag(L) = sqrt of the pivots
+  __shared__ double isq[kCholInvMax];     // and their reciprocals
   __shared__ __attribute__((aligned(16))) double lch[2][8][kCholInvMax];  // phase 2: 8 columns of L
   __shared__ double red[16];
   const int tid = threadIdx.x, p = tid >> 5, q = tid & 31;
@@ -692,7 +693,7 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
       // branch-free update: operands of entries that must not change are selected to 0
       // (columns l <= t are final; slots outside the triangle are never read); col holds
       // only finite values (zeroed at entry), so 0 * col stays 0
-      const double inv = 1.0 / d;
+      const double inv = rcp_nr(d);  // (the step's critical path: pivot read -> scale)
 #pragma unroll
       for (int y = Y; y < 8; ++y) cl[y] = (y > Y || q > tq) ? cl[y] * inv : 0.0;
 #pragma unroll
@@ -703,7 +704,10 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
   }
   if (pq && p == q) {
 #pragma unroll
-    for (int x = 0; x < 8; ++x) sq[p + 32 * x] = sqrt(a[cslot(x, x)]);
+    for (int x = 0; x < 8; ++x) {
+      sq[p + 32 * x] = sqrt(a[cslot(x, x)]);
+      isq[p + 32 * x] = 1.0 / sq[p + 32 * x];  // phase 2's row scale, off its serial path
+    }
   }
   __syncthreads();
   // L^T into Li: row l holds column l of L (L[i][l] = a / sqrt(d_l), sqrt(d_l) on the diagonal)
@@ -748,7 +752,7 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
         if ((t >> 3) + 1 < nch) issue_chunk((t >> 3) + 1);
       }
       if (p == tp) {  // row t of X: R[t][:] / L[t][t] (entries l <= t), published
-        const double f = 1.0 / sq[t];
+        const double f = isq[t];
 #pragma unroll
         for (int y = 0; y <= X; ++y)
           if (y < X || pq) {

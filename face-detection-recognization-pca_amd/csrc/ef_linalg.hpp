@@ -5,6 +5,20 @@
 
 namespace ef {
 
+// 1/x and 1/sqrt(x) (x > 0) from v_rcp_f64 / v_rsq_f64 refined by two Newton steps (~1 ulp;
+// a few dependent instructions instead of the IEEE division / square-root sequences) for
+// the serial chains of the small eigen- and Cholesky solvers
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = fma(y, fma(-x, y, 1.0), y);
+  return fma(y, fma(-x, y, 1.0), y);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
+  return fma(0.5 * y, fma(-x * y, y, 1.0), y);
+}
+
 // Loader semantics: L(r, c) = trans ? M[c][r] : M[r][c] for the stored row-major M.
 // A operands are read as A(m, k), B operands as B(k, n).  kfast tells the staging loop
 // which tile index is contiguous in memory so global reads coalesce.
