@@ -135,17 +135,20 @@ def scan_roofline(split, avg_ms, bsz, rows, k, split_opt=1):
     """Roofline of one gallery-scan launch.  fp32 scan: algorithmic 2 B N k flop against the
     fp32 MFMA peak; split-bf16 scan: its MFMA work (3 bf16 products per fp32 product, at
     the padded k) against the dense bf16 peak, plus the power-limited ceiling of a bare
-    LDS-fed loop of the same MFMA shape."""
+    LDS-fed loop of the same MFMA shape; the bf16 screen (split_opt 3, k > 128): one bf16
+    product per product, the same peak and ceiling."""
     flops_launch = 2.0 * bsz * rows * k
     kpad = next(p for p in (16, 32, 64, 128, 256, 512) if p >= k) if k <= 512 else (k + 127) // 128 * 128
     if split:
-        mflops = 3.0 * 2.0 * bsz * rows * kpad
+        screen = split_opt == 3 and k > 128
+        mflops = (1.0 if screen else 3.0) * 2.0 * bsz * rows * kpad
         a = mflops / (avg_ms * 1e-3) / 1e12
         shape16 = split_opt != 2 and k > 64
         kname = ("search16_kernel" if shape16 else "search_kernel<S3>") if k <= 128 else \
             ("search_wide16_kernel" if shape16 else "search_wide3_kernel")
-        rec = {"bound": "mfma", "kernel": kname + " (split-bf16: 3 x bf16 MFMA per fp32 "
-               "product + fused arg-best, fp64-resolved)", "achieved": round(a, 2),
+        what = (" (bf16 screen: 1 x bf16 MFMA per product, fp32 accumulation + fused arg-best, fp64-resolved)"
+                if screen else " (split-bf16: 3 x bf16 MFMA per fp32 product + fused arg-best, fp64-resolved)")
+        rec = {"bound": "mfma", "kernel": kname + ("<HI1>" if screen else "") + what, "achieved": round(a, 2),
                "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(a / PEAK_BF16_TFLOPS, 4),
                "avg_launch_ms": round(avg_ms, 4), "mfma_flops_per_launch": mflops,
                "algorithmic_flops_per_launch": flops_launch,
@@ -164,12 +167,13 @@ def scan_roofline(split, avg_ms, bsz, rows, k, split_opt=1):
 
 
 def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cpu_budget: float,
-             split_opt: int = 1):
+             split_opt: int = 3):
     """BASELINE.json configs[4] on one GPU, as a sub-record of the default run: 1M-row
-    gallery, 256x256 uint8 probes, k = 512, bf16 projection, fp32-accumulated distances (the
-    split-bf16 scan: bf16 MFMA products, fp32 accumulation, fp64-resolved identities); the
-    fp32 scan on the same step as a side leg whose keys must be identical; the bf16
-    projection's tolerance vs fp32; planted-match check; the CPU fp32 restatement."""
+    gallery, 256x256 uint8 probes, k = 512, bf16 projection, bf16-MFMA distances with fp32
+    accumulation (split_opt 3, the default: the single-bf16 screen, one bf16 MFMA per
+    product; 1: the split-bf16 scan, three), identities fp64-resolved either way; the
+    split-bf16 and fp32 scans on the same step as side legs whose keys must be identical;
+    the bf16 projection's tolerance vs fp32; planted-match check; the CPU fp32 restatement."""
     import torch
     from eigenface import decode_keys, synth
     n, side, k, bsz, precision = CONFIGS["c5"]
@@ -186,11 +190,12 @@ def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cp
     eng.set_model(mean, W, precision=precision)
     eng.set_gallery(G)
     P_dev = torch.from_numpy(P).to(dev)
-    keys = {o: torch.empty(bsz, dtype=torch.int64, device=dev) for o in (split_opt, 0)}
+    opts = [split_opt] + ([1] if split_opt != 1 else []) + [0]
+    keys = {o: torch.empty(bsz, dtype=torch.int64, device=dev) for o in opts}
     torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
     legs = {}
-    for opt in (split_opt, 0):  # headline: split-bf16 scan; side leg: fp32 scan
+    for opt in opts:  # headline: the bf16 scan of split_opt; side legs: split-bf16, fp32
         eng.set_option("search_split_bf16", opt)
         for _ in range(warmup):
             eng.recognize_keys(P_dev, "l2", keys=keys[opt])
@@ -211,15 +216,24 @@ def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cp
     reps, s_avg, s_n = legs[split_opt]
     el = float(np.median(reps))
     idx, _ = decode_keys(keys[split_opt].cpu().numpy(), "l2")
-    traffic, traffic_src = pmc_traffic("c5s3")
+    traffic, traffic_src = pmc_traffic("c5hi" if split_opt == 3 else "c5s3")
+    scan_name = ("bf16 distance screen (one bf16 MFMA per product, fp32 accumulate, fp64-resolved)"
+                 if split_opt == 3 else "split-bf16 distance scan (fp32 accumulate, fp64-resolved)")
     out = {"config": f"C5: gallery {n} x k={k}, {side}x{side} uint8 faces, probe batch {bsz}, metric l2, "
-                     "bf16 projection, split-bf16 distance scan (fp32 accumulate, fp64-resolved)",
+                     f"bf16 projection, {scan_name}",
            "value": round(bsz * steps / el, 1), "unit": "faces/s", "steps": steps, "warmup": warmup,
            "ms_per_step": round(el / steps * 1e3, 4),
            "repeats_ms_per_step": [round(r / steps * 1e3, 4) for r in reps],
            "roofline": dict(scan_roofline(True, s_avg, bsz, n, k, split_opt), traffic=traffic,
                             traffic_source=traffic_src, launches=s_n),
            "setup_s": round(setup_s, 1)}
+    if split_opt != 1:
+        reps1, s1_avg, s1_n = legs[1]
+        el1 = float(np.median(reps1))
+        out["scan_split_bf16"] = {"value": round(bsz * steps / el1, 1), "unit": "faces/s",
+                                  "ms_per_step": round(el1 / steps * 1e3, 4),
+                                  "keys_identical_to_headline": bool(torch.equal(keys[1], keys[split_opt])),
+                                  "roofline": dict(scan_roofline(True, s1_avg, bsz, n, k, 1), launches=s1_n)}
     reps32, s32_avg, s32_n = legs[0]
     el32 = float(np.median(reps32))
     traffic32, src32 = pmc_traffic("c5")
@@ -760,8 +774,12 @@ def main():
                          "config 5, whose bf16-MFMA + fp32-accumulate arithmetic it is); the other one is timed "
                          "as a side leg")
     ap.add_argument("--no-split", action="store_true", help="skip the side leg of the other scan arithmetic")
-    ap.add_argument("--split-opt", type=int, default=1, choices=[1, 2],
-                    help="EF_OPT_SEARCH_SPLIT_BF16 value of the split scan (2: the 32x32x16 kernel at k = 128)")
+    ap.add_argument("--split-opt", type=int, default=1, choices=[1, 2, 3],
+                    help="EF_OPT_SEARCH_SPLIT_BF16 value of the split scan (2: the 32x32x16 kernel at k = 128; "
+                         "3: the single-bf16 screen at k > 128)")
+    ap.add_argument("--c5-opt", type=int, default=3, choices=[1, 3],
+                    help="EF_OPT_SEARCH_SPLIT_BF16 value of the c5 sub-record's headline scan (3: the bf16 "
+                         "screen; 1: the split-bf16 scan)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -937,8 +955,12 @@ def main():
         def roof(split, avg_ms):
             return scan_roofline(split, avg_ms, bsz, hi - lo, k, args.split_opt)
 
-        traffic, traffic_src = (pmc_traffic(args.config + ("s3" if split_main else "")) if world == 1
-                                else (None, None))
+        def traffic_key(split):  # the committed PMC summary of this scan (pmc_summary.py configs)
+            if not split:
+                return args.config
+            return args.config + ("hi" if args.split_opt == 3 and k > 128 else "s3")
+
+        traffic, traffic_src = pmc_traffic(traffic_key(split_main)) if world == 1 else (None, None)
         rec = {
             "metric": "faces/sec recognized (projection+NN) @1M-gallery k=128" if args.config == "c3"
                       else f"faces/sec recognized (projection+NN) @{n_total}-gallery k={k}",
@@ -986,7 +1008,7 @@ def main():
                 "roofline": dict(roof(split_leg["scan"] == "split_bf16", split_leg["search_avg_ms"]),
                                  launches=split_leg["launches"],
                                  **dict(zip(("traffic", "traffic_source"),
-                                            pmc_traffic(args.config + ("s3" if not split_main else ""))))),
+                                            pmc_traffic(traffic_key(not split_main))))),
             }
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(P, mean, W, G, targets, args.cpu_budget)
@@ -998,7 +1020,7 @@ def main():
             rec["c2"] = c2_bench(eng, not args.no_cpu)
         if world == 1 and args.config == "c3" and not args.no_c5:
             rec["c5"] = c5_bench(eng, dev, not args.no_cpu, args.steps, args.warmup, args.repeats,
-                                 min(args.cpu_budget, 8.0), args.split_opt)
+                                 min(args.cpu_budget, 8.0), args.c5_opt)
         if world == 1 and not args.no_fit:
             rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu), "c2": fit_bench(eng, not args.no_cpu)}
         if world == 1 and not args.no_image:

@@ -131,11 +131,17 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
       EF_TRY(ensure(c, c->q3, (size_t)bpad_max * c->g_kp * sizeof(float)));
       Q3 = static_cast<float*>(c->q3.p);
     }
-    if (!c->g3_valid) {
+    // the bf16 screen (3) runs on single-bf16 rows (wide kernels, k > 128); every other split
+    // scan on the split (hi + lo) rows
+    const int layout = c->opt_search_split_bf16 == 3 && c->g_kp > 128 ? 3 : 1;
+    if (!c->g3_valid || c->g3_layout != layout) {
       EF_TRY(ensure(c, c->G3, (size_t)c->n_gallery * c->g_kp * sizeof(float)));
-      EF_HIP(c, launch_split_rows(c->stream, static_cast<const float*>(c->G.p), c->n_gallery, c->g_kp, c->G3.p),
+      const float* Gp = static_cast<const float*>(c->G.p);
+      EF_HIP(c, layout == 3 ? launch_hi_rows(c->stream, Gp, c->n_gallery, c->g_kp, c->G3.p)
+                            : launch_split_rows(c->stream, Gp, c->n_gallery, c->g_kp, c->G3.p),
              "split gallery");
       c->g3_valid = true;
+      c->g3_layout = layout;
     }
     G3 = static_cast<const float*>(c->G3.p);
   }
@@ -696,7 +702,7 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
       c->opt_fit_chebyshev = value != 0;
       return EF_OK;
     case EF_OPT_SEARCH_SPLIT_BF16:
-      if (value < 0 || value > 2) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1 or 2");
+      if (value < 0 || value > 3) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1, 2 or 3");
       c->opt_search_split_bf16 = value;
       return EF_OK;
     default:

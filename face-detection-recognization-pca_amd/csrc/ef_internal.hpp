@@ -83,6 +83,7 @@ struct ef_ctx {
   int64_t opt_haar_ordered = 0;
   int64_t opt_jpeg_chunk_bits = 0;
   int64_t opt_search_split_bf16 = 0;
+  int g3_layout = 0;  // what G3 holds: 1 split (hi + lo) rows, 3 single-bf16 rows
   int64_t opt_jpeg_part_files = 8192;
   int64_t opt_fit_chebyshev = 1;
   hipStream_t own_stream = nullptr;
@@ -178,6 +179,8 @@ hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl
                          int64_t bpad, int64_t b, const float* G, const float* G3, const float* aux, int64_t n,
                          int64_t g_offset, float gmax2, const SearchWs& ws, long long* keys, ef_ctx* c);
 hipError_t launch_split_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out);
+// single-bf16 copy for the bf16 screen (EF_OPT_SEARCH_SPLIT_BF16 = 3), kp % 64 == 0
+hipError_t launch_hi_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out);
 hipError_t launch_keys_none(hipStream_t s, long long* keys, int64_t b, ef_match* match);
 // keys[b] (+ merged[b]) <- exact arg-best over parts x b match records (ef_comm.hip)
 hipError_t launch_matches_merge(hipStream_t s, const ef_match* parts, int nparts, int64_t b, long long* keys,

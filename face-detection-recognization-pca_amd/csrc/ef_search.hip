@@ -689,7 +689,9 @@ __global__ __launch_bounds__(512, 4) void search16_kernel(
 
 // One wave per probe: winner over chunks, global runner-up, fp64 re-score, ambiguity test.
 // KP = 0: row length kp_rt at run time (k > 512).
-template <int KP, int METRIC, bool S3 = false>
+// S3: the scan's arithmetic — 0 fp32, 1 split bf16 (hi + lo), 2 single bf16 (the screen of
+// EF_OPT_SEARCH_SPLIT_BF16 = 3) — which sets the bound below.
+template <int KP, int METRIC, int S3 = 0>
 __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ qpad, int64_t b, int64_t bpad,
                                                      int nchunks, const float* __restrict__ G, int64_t n,
                                                      int64_t g_offset, float gmax2, SearchWs ws,
@@ -737,7 +739,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ q
   const float u = 5.9604645e-08f;  // 2^-24
   const float qn = sqrtf(qq);
   float delta;
-  if constexpr (S3) {
+  if constexpr (S3 == 2) {
+    // single-bf16 chain: |x - bf16(x)| <= 2^-8 |x| for both operands, so each product is
+    // within (2 + 2^-8) 2^-8 |q||g| of the exact one (2.01 2^-8 taken); KP exact products +
+    // the start value summed in fp32 (2u per add allowed), ||g||^2 itself to KP u
+    const float es = 2.01f * 3.90625e-03f;  // 2.01 * 2^-8
+    if constexpr (METRIC == EF_METRIC_L2) {
+      const float gm = sqrtf(gmax2);
+      delta = 2.f * (2.f * es * qn * gm + (kpv + 4) * 2.f * u * 1.01f * (2.02f * qn * gm + gmax2) +
+                     kpv * u * gmax2 + 4.f * u * fabsf(b1)) + 1e-30f;
+    } else {
+      delta = 2.f * ((es + (kpv + 8) * 2.f * u) * 1.01f * qn) + 1e-30f;
+    }
+  } else if constexpr (S3 == 1) {
     // split-bf16 chain: dropped terms (lo.lo', hi.e', lo.e', e.q) <= 3.02 * 2^-16 |q||g| per
     // element, 3 KP exact products + the start value summed in fp32 (2u per add allowed, in
     // case the matrix core's adds do not round to nearest), ||g||^2 itself to KP u
@@ -868,6 +882,23 @@ __global__ void split_rows_kernel(const float* __restrict__ G, int64_t groups, u
   out[2 * i + 1] = make_uint4(lo[0] | lo[1] << 16, lo[2] | lo[3] << 16, lo[4] | lo[5] << 16, lo[6] | lo[7] << 16);
 }
 
+// Single-bf16 copy (the bf16 screen, EF_OPT_SEARCH_SPLIT_BF16 = 3; wide kernels): per 64
+// fp32 elements, 128 B = eight 16-B chunks, chunk 2q = bf16(x[8q .. 8q + 7]) and chunk
+// 2q + 1 = bf16(x[32 + 8q .. 32 + 8q + 7]) — the split copy's slice row bytes and fragment
+// order, so search_wide16_kernel<.., HI1> reads it with the split code (half the bytes).
+__global__ void hi_rows_kernel(const float* __restrict__ G, int64_t blocks, uint4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= blocks) return;
+  const float4* x = reinterpret_cast<const float4*>(G) + 16 * i;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int e0 = (c & 1) * 32 + (c >> 1) * 8;  // first element of chunk c
+    const float4 a = x[e0 / 4], b = x[e0 / 4 + 1];
+    out[8 * i + c] = make_uint4(bf16_bits(a.x) | bf16_bits(a.y) << 16, bf16_bits(a.z) | bf16_bits(a.w) << 16,
+                                bf16_bits(b.x) | bf16_bits(b.y) << 16, bf16_bits(b.z) | bf16_bits(b.w) << 16);
+  }
+}
+
 // max ||g||^2 (one atomic per block; non-negative floats order as their bit patterns)
 __global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out) {
   __shared__ float red[4];
@@ -947,18 +978,23 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
                               ef_ctx* c, int kp) {
   if constexpr (KP > 128 || KP == 0) {
     if (!Q3) return hipErrorInvalidValue;
-    hipError_t e = launch_split_rows(s, qpad, bpad, kp, Q3);
+    // 16x16x32 split kernel unless the 32x32x16 one (2) or the single-bf16 screen (3) is asked for
+    const int variant = c->opt_search_split_bf16 == 2 || c->opt_search_split_bf16 == 3 ? (int)c->opt_search_split_bf16 : 1;
+    hipError_t e = variant == 3 ? launch_hi_rows(s, qpad, bpad, kp, Q3) : launch_split_rows(s, qpad, bpad, kp, Q3);
     if (e != hipSuccess) return e;
     timer_begin(c, EF_KERNEL_SEARCH, tev);
-    const int variant = c->opt_search_split_bf16 == 2 ? 2 : 1;  // 16x16x32 unless the 32x32x16 kernel is asked for
     e = launch_search_wide(s, kp, M, false, variant, pl, Q3, G3, aux, n, bpad, ws);
     timer_end(c, tev);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     const dim3 pgrid((unsigned)((b + 3) / 4));
-    hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
-                       g_offset, gmax2, ws, keys, kp);
+    if (variant == 3)
+      hipLaunchKernelGGL((reduce_kernel<KP, M, 2>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
+                         g_offset, gmax2, ws, keys, kp);
+    else
+      hipLaunchKernelGGL((reduce_kernel<KP, M, 1>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
+                         g_offset, gmax2, ws, keys, kp);
     e = launch_search_wide(s, kp, M, true, variant, pl, Q3, G3, aux, n, bpad, ws);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((resolve_kernel<KP, M>), pgrid, dim3(256), 0, s, qpad, G, n, g_offset, gmax2, ws, keys, kp);
@@ -981,7 +1017,7 @@ static hipError_t search_s3_t(hipStream_t s, const SearchPlan& pl, const float* 
     e = hipMemsetAsync(ws.amb_count, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     const dim3 pgrid((unsigned)((b + 3) / 4));
-    hipLaunchKernelGGL((reduce_kernel<KP, M, true>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
+    hipLaunchKernelGGL((reduce_kernel<KP, M, 1>), pgrid, dim3(256), 0, s, qpad, b, bpad, pl.nchunks, G, n,
                        g_offset, gmax2, ws, keys, kp);
     if (k16)
       hipLaunchKernelGGL((search16_kernel<M, true>), dim3((unsigned)pl.c_grid), block, 0, s, qpad, G3, aux, n,
@@ -1097,6 +1133,14 @@ hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k,
 hipError_t launch_split_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out) {
   const int64_t groups = n * kp / 8;
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, G, groups,
+                     static_cast<uint4*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_hi_rows(hipStream_t s, const float* G, int64_t n, int kp, void* out) {
+  if (kp % 64 != 0) return hipErrorInvalidValue;
+  const int64_t blocks = n * kp / 64;
+  hipLaunchKernelGGL(hi_rows_kernel, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, s, G, blocks,
                      static_cast<uint4*>(out));
   return hipGetLastError();
 }

@@ -637,7 +637,14 @@ __global__ __launch_bounds__(512, 1) void search_wide3_kernel(
 // pairs 2m, 2m + 1 fill both 32-bank halves): every group covers all 64 banks.  The wide3
 // swizzle (row >> 1) & 7 would be 2-way conflicted here.
 // Accumulator layout: acc[rb][pb][r] = row 16 rb + 4 qd + r of probe 16 pb + r16.
-template <int KP, int METRIC, bool COLLECT>
+// HI1 (EF_OPT_SEARCH_SPLIT_BF16 = 3, the bf16 screen): the operands are the single-bf16
+// copies of hi_rows_kernel (ef_search.hip) — per 64-element k slice, chunk 2q = elements
+// 8q .. 8q + 7 and chunk 2q + 1 = elements 32 + 8q .. 32 + 8q + 7, so a slice row is the same
+// 128 B, read by the same fragment code and swizzle: "hi" is the slice's first 32-k step,
+// "lo" its second, two MFMAs per 64 k instead of three per 32 k.  Launched with the row
+// length in 4-byte units (kp / 2); scores carry bf16 rounding of both operands, which the
+// screen's bound (reduce_kernel<.., 2>) covers.
+template <int KP, int METRIC, bool COLLECT, bool HI1 = false>
 __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     const float* __restrict__ q3, const float* __restrict__ G3, const float* __restrict__ aux, int64_t n,
     int n_ptiles, int tiles_per_chunk, int pblk, int cblk, int64_t bpad, SearchWs ws, int kp_rt) {
@@ -833,9 +840,14 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
       const bf16x8w al = as_bf16x8w(*reinterpret_cast<const float4*>(sg + 16 * rb * WBK + pl));
 #pragma unroll
       for (int pb = 0; pb < 4; ++pb) {
-        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[pb], acc[rb][pb], 0, 0, 0);
-        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[pb], acc[rb][pb], 0, 0, 0);
-        acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[pb], acc[rb][pb], 0, 0, 0);
+        if constexpr (HI1) {  // k steps 0 and 1 of the 64-k slice
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[pb], acc[rb][pb], 0, 0, 0);
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bl[pb], acc[rb][pb], 0, 0, 0);
+        } else {  // hi.hi' + hi.lo' + lo.hi'
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[pb], acc[rb][pb], 0, 0, 0);
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[pb], acc[rb][pb], 0, 0, 0);
+          acc[rb][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[pb], acc[rb][pb], 0, 0, 0);
+        }
       }
 #if EF_WIDE_STAGGER
       if (rb == EF_WIDE_STAGGER - 1 && more && wave >= 4) issue(it + 1, buf ^ 1);
@@ -943,19 +955,19 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
   }
 }
 
-template <int KP, int M>
+template <int KP, int M, bool HI1 = false>
 static hipError_t wide3_t(hipStream_t s, bool collect, bool w16, const SearchPlan& pl, const float* q3,
                           const float* G3, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws, int kp) {
   const dim3 grid((unsigned)(pl.nchunks * pl.n_ptiles)), block(512);
   if (pl.n_ptiles % pl.pblk != 0 || pl.nchunks % pl.cblk != 0 || (pl.nchunks * pl.n_ptiles) % 8 != 0 ||
       (pl.nchunks * pl.n_ptiles / 8) % (pl.cblk * pl.pblk) != 0 || bpad % W3P != 0)
     return hipErrorInvalidValue;  // the block deal would not be a bijection
-  if (w16) {
+  if (w16 || HI1) {
     if (collect)
-      hipLaunchKernelGGL((search_wide16_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux,
-                         n, pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws, kp);
+      hipLaunchKernelGGL((search_wide16_kernel<KP, M, true, HI1>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3,
+                         aux, n, pl.c_chunks, pl.c_tpc, pl.pblk, pl.cblk, bpad, ws, kp);
     else
-      hipLaunchKernelGGL((search_wide16_kernel<KP, M, false>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
+      hipLaunchKernelGGL((search_wide16_kernel<KP, M, false, HI1>), grid, block, 0, s, q3, G3, aux, n, pl.n_ptiles,
                          pl.tiles_per_chunk, pl.pblk, pl.cblk, bpad, ws, kp);
   } else if (collect) {
     hipLaunchKernelGGL((search_wide3_kernel<KP, M, true>), dim3((unsigned)pl.c_grid), block, 0, s, q3, G3, aux, n,
@@ -995,6 +1007,25 @@ hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, i
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
                               const SearchWs& ws) {
   const bool l2 = metric == EF_METRIC_L2;
+  if (s3 == 3) {  // the bf16 screen on single-bf16 copies: rows of kp / 2 four-byte units
+    const int kh = kp / 2;
+    const int64_t ns = kh / WBK;
+    if (kp % 128 != 0 || bpad * (int64_t)kh * 4 >= ((int64_t)1 << 31) ||
+        (int64_t)std::max(pl.tiles_per_chunk, pl.c_tpc) * ns >= ((int64_t)1 << 31))
+      return hipErrorInvalidValue;
+    switch (kp) {
+      case 256:
+        return l2 ? wide3_t<128, EF_METRIC_L2, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh)
+                  : wide3_t<128, EF_METRIC_COSINE, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh);
+      case 512:
+        return l2 ? wide3_t<256, EF_METRIC_L2, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh)
+                  : wide3_t<256, EF_METRIC_COSINE, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh);
+      default:
+        if (kp <= 512) return hipErrorInvalidValue;
+        return l2 ? wide3_t<0, EF_METRIC_L2, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh)
+                  : wide3_t<0, EF_METRIC_COSINE, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh);
+    }
+  }
   switch (kp) {
     case 256:
       return l2 ? wide_t<256, EF_METRIC_L2>(s, collect, s3, pl, qpad, G, aux, n, bpad, ws, kp)

@@ -220,7 +220,11 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
 #define EF_OPT_SEARCH_SPLIT_BF16 7 /* 1: gallery scans on bf16 MFMA with split (hi + lo) fp32 operands
                                       and a widened error bound; identities and scores are still
                                       fp64-resolved, so results equal the fp32 scan's [0]; 2: the same
-                                      with the 32x32x16 kernel at k in (64, 128] (comparison) */
+                                      with the 32x32x16 kernel at k in (64, 128] (comparison); 3: at
+                                      k > 128 a single-bf16 screen (one bf16 MFMA per product, fp32
+                                      accumulation, a bf16-wide bound) — still fp64-resolved, same
+                                      results, fewer MFMAs; more probes reach the resolution when
+                                      the best two rows are within ~2% (k <= 128: as 1) */
 #define EF_OPT_JPEG_PART_FILES 8   /* ef_jpeg_ingest decodes in parts of this many files, staging
                                       part i + 1 on a host thread while part i decodes [8192] */
 #define EF_OPT_FIT_CHEBYSHEV 9     /* 1 [default]: the subspace iteration advances a Chebyshev

@@ -2,11 +2,11 @@
 1M x 512 gallery, 4096 planted 256x256 uint8 probes, the bf16 projection
 (EF_MODEL_BF16) — the bench's exact workload (eigenface.synth).  Covers the wide plans at
 N = 1M and KP = 512 (chunk counts, the blocked XCD deal with its serpentine k order, the
-collect-pass grid) for the fp32 wide scan and the split-bf16 one (search_wide16_kernel),
-L2 and cosine:
+collect-pass grid) for the fp32 wide scan, the split-bf16 one (search_wide16_kernel) and
+the single-bf16 screen (option 3, search_wide16_kernel<.., HI1>), L2 and cosine:
 
 * L2: every probe finds its planted row;
-* split-bf16 keys == fp32-scan keys bit for bit; fused recognise == project + search;
+* split-bf16 and bf16-screen keys == fp32-scan keys bit for bit; fused recognise == project + search;
 * a fixed 256-probe subset against the fp64 oracle over the whole gallery on the GPU's
   (bf16-projected) features: identical rows wherever the fp64 runner-up is outside fp32
   rounding, and the chosen row's score within it everywhere.
@@ -36,7 +36,7 @@ def c5():
     return dict(mean=mean, W=W, G=G, targets=targets, P_dev=torch.from_numpy(P).cuda())
 
 
-@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("split", [0, 1, 3])
 def test_c5_full_size(eng, c5, split):
     import torch
     from eigenface import decode_keys

@@ -239,3 +239,102 @@ def test_split_match_records_equal_fp32(split, k):
         for a, b in zip(recs[0], recs[1]):
             for f in ("score", "scale", "key"):
                 np.testing.assert_array_equal(a[f], b[f])
+
+
+# ---- the single-bf16 screen (option 3, k > 128): one bf16 MFMA per product, a bound 2^8
+# times wider than the split scan's; probes whose best rows are within it are collected and
+# fp64-resolved, so the keys still equal the fp32 scan's bit for bit.
+
+def _keys_screen(eng, g, q, metric, offset=0):
+    eng.set_option("search_split_bf16", 0)
+    eng.set_gallery(g, global_offset=offset)
+    k32 = eng.search_keys(q, metric)
+    eng.set_option("search_split_bf16", 3)
+    try:
+        k1 = eng.search_keys(q, metric)  # the single-bf16 copy is built on this first search
+    finally:
+        eng.set_option("search_split_bf16", 0)
+    return k32, k1
+
+
+def test_screen_option_roundtrip(eng):
+    eng.set_option("search_split_bf16", 3)
+    try:
+        assert eng.get_option("search_split_bf16") == 3
+    finally:
+        eng.set_option("search_split_bf16", 0)
+    with pytest.raises(Exception):
+        eng.set_option("search_split_bf16", 4)
+
+
+@pytest.mark.parametrize("k", [256, 300, 512, 640, 1024])
+def test_screen_keys_equal_fp32(eng, k):
+    """Random Gaussian rows: the best two rows of a probe are often within the bf16 bound
+    (many probes take the collect pass, some overflow its 32 candidates and are re-scored
+    over the whole gallery) — keys identical to the fp32 scan either way."""
+    rng = np.random.default_rng(31 + k)
+    g = rng.standard_normal((3001, k)).astype(np.float32)
+    q = rng.standard_normal((1100, k)).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        k32, k1 = _keys_screen(eng, g, q, metric)
+        np.testing.assert_array_equal(k1, k32)
+
+
+@pytest.mark.parametrize("k", [256, 512])
+def test_screen_near_ties_and_planted(eng, k):
+    """Sub-bf16 near-ties (the later row closer by ~4e-6 relative) and planted probes in
+    one batch: exact fp64 winners."""
+    rng = np.random.default_rng(71 + k)
+    n, b = 6000, 512
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    q = rng.standard_normal((b, k)).astype(np.float32)
+    for i in range(0, b, 2):
+        d = rng.standard_normal(k).astype(np.float32) * 0.5
+        lo, hi = sorted(rng.choice(n, 2, replace=False))
+        g[lo] = q[i] + d
+        g[hi] = q[i] + d * np.float32(1 - 2e-6)
+    t = rng.integers(0, n, b)
+    q[1::2] = g[t[1::2]] + rng.standard_normal((b // 2, k)).astype(np.float32) * 0.1
+    want = orc.l2_argmin(q, g)[0]
+    k32, k1 = _keys_screen(eng, g, q, "l2")
+    np.testing.assert_array_equal(k1, k32)
+    np.testing.assert_array_equal((k1 & 0xFFFFFFFF).astype(np.int64), want)
+
+
+@pytest.mark.parametrize("b", [1024, 4096])
+def test_screen_xcd_deal_and_ragged_tile(eng, b):
+    rng = np.random.default_rng(b + 3)
+    g = rng.standard_normal((5003, 512)).astype(np.float32)
+    t = rng.integers(0, 5003, b)
+    q = (g[t] + rng.standard_normal((b, 512)).astype(np.float32) * 0.3).astype(np.float32)
+    for metric in ("l2", "cosine"):
+        k32, k1 = _keys_screen(eng, g, q, metric)
+        np.testing.assert_array_equal(k1, k32)
+        np.testing.assert_array_equal((k1 & 0xFFFFFFFF).astype(np.int64), t)
+
+
+def test_screen_cluster_overflow_and_records(eng):
+    """A 200-row cluster inside 1e-6 (candidate overflow -> whole-gallery fp64 re-score) and
+    the match records of two shards: field for field equal to the fp32 scan's."""
+    rng = np.random.default_rng(515)
+    k, n, b = 512, 3000, 64
+    g = rng.standard_normal((n, k)).astype(np.float32)
+    base = rng.standard_normal(k).astype(np.float32)
+    g[100:300] = base + (rng.standard_normal((200, k)) * 1e-6).astype(np.float32)
+    q = (base + rng.standard_normal((b, k)).astype(np.float32) * 0.01).astype(np.float32)
+    k32, k1 = _keys_screen(eng, g, q, "l2")
+    np.testing.assert_array_equal((k32 & 0xFFFFFFFF).astype(np.int64), orc.l2_argmin(q, g)[0])
+    np.testing.assert_array_equal(k1, k32)
+    recs = {}
+    for opt in (0, 3):
+        eng.set_option("search_split_bf16", opt)
+        try:
+            recs[opt] = [None, None]
+            for j, (lo, hi) in enumerate([(0, 1500), (1500, 3000)]):
+                eng.set_gallery(g[lo:hi], global_offset=lo)
+                recs[opt][j] = eng.search_matches(q, "cosine")
+        finally:
+            eng.set_option("search_split_bf16", 0)
+    for a, c in zip(recs[0], recs[3]):
+        for f in ("score", "scale", "key"):
+            np.testing.assert_array_equal(a[f], c[f])

@@ -20,7 +20,10 @@ CONFIGS = {
     "c3": ("search_kernel<128, 0, false, false, 0>", 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4),
     # split-bf16 scan: the split gallery copy has the fp32 gallery's bytes
     "c3s3": ("search16_kernel<0, false>", 1_000_000 * 128 * 4 + 1_000_000 * 4 + 4096 * 128 * 4),
-    "c5s3": ("search_wide16_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
+    "c5s3": ("search_wide16_kernel<512, 0, false, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
+    # the single-bf16 screen (EF_OPT_SEARCH_SPLIT_BF16 = 3): 2-byte gallery and probe copies,
+    # launched with the row length in 4-byte units (KP = 512 / 2)
+    "c5hi": ("search_wide16_kernel<256, 0, false, true>", 1_000_000 * 512 * 2 + 1_000_000 * 4 + 4096 * 512 * 2),
     # the 32x32x16 split wide kernel (EF_OPT_SEARCH_SPLIT_BF16 = 2)
     "c5s3w3": ("search_wide3_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
     "c5": ("search_wide_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
