@@ -777,6 +777,10 @@ def main():
     ap.add_argument("--split-opt", type=int, default=1, choices=[1, 2, 3],
                     help="EF_OPT_SEARCH_SPLIT_BF16 value of the split scan (2: the 32x32x16 kernel at k = 128; "
                          "3: the single-bf16 screen at k > 128)")
+    ap.add_argument("--merge", default="exact", choices=["exact", "min"],
+                    help="N > 1 exchange: 'exact' = all-gather of fp64 match records + exact merge (default); "
+                         "'min' = one all-reduce(MIN) of packed fp32 keys (SURVEY 8e; differs only on sub-ulp "
+                         "cross-shard near-ties); the other one is timed on the same step as a side record")
     ap.add_argument("--c5-opt", type=int, default=3, choices=[1, 3],
                     help="EF_OPT_SEARCH_SPLIT_BF16 value of the c5 sub-record's headline scan (3: the bf16 "
                          "screen; 1: the split-bf16 scan)")
@@ -840,7 +844,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     eng.set_model(mean, W, precision=precision)
-    shard = ShardedGallery(eng, G, n_total, rank, world)
+    shard = ShardedGallery(eng, G, n_total, rank, world, merge=args.merge)
     P_dev = torch.from_numpy(P).to(dev)
     keys = torch.empty(bsz, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
@@ -891,6 +895,19 @@ def main():
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         exchange_ms = float(t.item())
+    other_merge = None
+    if world > 1:  # the other exchange on the same step: exact record merge <-> one all-reduce(MIN)
+        main_keys = keys.clone()
+        shard.merge = "min" if args.merge == "exact" else "exact"
+        reps_o, _, _ = timed(step)
+        xo = torch.tensor([shard.exchange_ms(bsz, k, dev)], dtype=torch.float64,
+                          device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(xo, op=dist.ReduceOp.MAX)
+        other_merge = {"merge": shard.merge, "ms_per_step": round(float(np.median(reps_o)) / args.steps * 1e3, 4),
+                       "exchange_ms_per_step": round(float(xo.item()), 4),
+                       "keys_identical": bool(torch.equal(keys, main_keys))}
+        shard.merge = args.merge
+        keys.copy_(main_keys)
     ranks_agree = None
     if world > 1:  # every rank must hold the same merged keys
         h = torch.tensor([int(np.bitwise_xor.reduce(keys.cpu().numpy() * np.int64(0x9E3779B1)))
@@ -993,6 +1010,8 @@ def main():
             "project_avg_ms": round(p_ms / max(p_n, 1), 4),
             "exchange_ms_per_step": round(exchange_ms, 4) if exchange_ms is not None else None,
             "exchange_share_of_step": round(exchange_ms / ms_step, 4) if exchange_ms is not None else None,
+            "merge": args.merge if world > 1 else None,
+            "other_merge": other_merge,
             "host_buffer_faces_per_s": round(host_rate, 1) if host_rate else None,
             "check": {"planted_match": match, "ranks_agree": ranks_agree, "host_buffer_keys_identical": host_same},
         }

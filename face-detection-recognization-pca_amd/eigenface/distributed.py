@@ -16,6 +16,12 @@ The projection model is replicated; the probe batch's projection is split by row
 ranks and the (B x k) fp32 features are all-gathered (2 MiB at B = 4096, k = 128), so no
 rank repeats another's projection work.
 
+``merge="min"`` is the north star's exchange instead: each rank's packed
+fp32 key per probe and ONE all-reduce(MIN) of B x 8 B — no record gather, no merge launch.
+It equals the exact merge except where two ranks' winners tie in fp32 but not in fp64 (a
+sub-ulp difference: the MIN then keeps the lower index; tests/test_distributed_cpu.py
+shows both cases), so "exact" stays the default.
+
 The same exchange also exists inside the library (``Engine.comm_init`` /
 ``ef_comm_init``: RCCL driven from C, for callers of the C ABI); this module is the
 torch.distributed form.
@@ -73,7 +79,10 @@ class ShardedGallery:
     :class:`eigenface.Engine` (device tensors in, a (b, 3) int64 device tensor out)."""
 
     def __init__(self, engine, gallery_local, n_total: int, rank: int, world: int, group=None,
-                 local_matches=None, local_project=None):
+                 local_matches=None, local_project=None, merge: str = "exact"):
+        if merge not in ("exact", "min"):
+            raise ValueError(f"merge must be 'exact' or 'min', not {merge!r}")
+        self.merge = merge
         self.rank, self.world, self.n_total, self.group = rank, world, n_total, group
         self.lo, self.hi = shard_range(n_total, rank, world)
         if gallery_local is not None and len(gallery_local) != self.hi - self.lo:
@@ -84,6 +93,7 @@ class ShardedGallery:
         # one rank with the engine's own search: its keys are already global (no records,
         # no merge launch)
         self._direct = world == 1 and engine is not None and local_matches is None and local_project is None
+        self._local_is_engine = local_matches is None
         self._local = local_matches or (lambda q, m: engine.search_matches(q, m))
         self._project = local_project or (lambda p, out=None: engine.project(p, out=out))
         self._fbuf = {}
@@ -120,10 +130,40 @@ class ShardedGallery:
             return keys
         return out
 
+    def _min_reduce(self, local_keys, keys=None):
+        """merge="min": one all-reduce(MIN) of the ranks' packed keys -> int64 keys[b]."""
+        import torch
+        import torch.distributed as dist
+
+        k = local_keys if isinstance(local_keys, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(local_keys, dtype=np.int64))
+        if self.world > 1:
+            if k.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: reduce on host
+                t = k.cpu()
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+                k.copy_(t)
+            else:  # RCCL over xGMI, stream-ordered on torch's current stream (or gloo, CPU)
+                dist.all_reduce(k, op=dist.ReduceOp.MIN, group=self.group)
+        if keys is not None:
+            keys.copy_(k)
+            return keys
+        return k
+
+    def _local_keys(self, Q, metric):
+        """This rank's packed keys (global row indices) of its best row per probe."""
+        if self.engine is not None and self._local_is_engine:
+            return self.engine.search_keys(Q, metric)
+        rec = self._local(Q, metric)
+        if isinstance(rec, np.ndarray) and rec.dtype.names:
+            return np.ascontiguousarray(rec["key"], dtype=np.int64).copy()
+        return _as_records_tensor(rec)[:, 2].contiguous()
+
     def search_keys(self, Q, metric="l2", keys=None):
         """Global packed keys of the best row per probe (all ranks get the same keys)."""
         if self._direct:
             return self.engine.search_keys(Q, metric, keys=keys)
+        if self.merge == "min":
+            return self._min_reduce(self._local_keys(Q, metric), keys)
         b = int(Q.shape[0])
         return self._gather_merge(self._local(Q, metric), b, keys)
 
@@ -182,6 +222,10 @@ class ShardedGallery:
         if self._direct:
             return self.engine.recognize_keys(P, metric, keys=keys)
         b = int(P.shape[0])
+        if self.merge == "min":
+            if self.world > 1 and shard_projection and isinstance(P, torch.Tensor):
+                return self._min_reduce(self._local_keys(self.project_sharded(P), metric), keys)
+            return self._min_reduce(self.engine.recognize_keys(P, metric), keys)  # replicated projection
         if self.world == 1 or not shard_projection or not isinstance(P, torch.Tensor):
             return self._gather_merge(self.engine.recognize_matches(P, metric), b, keys)
         q = self.project_sharded(P)
@@ -189,7 +233,8 @@ class ShardedGallery:
 
     def exchange_ms(self, b: int, k: int, device, reps: int = 20) -> float:
         """Milliseconds per step of this rank's collectives alone — the feature all-gather of
-        ceil(b / world) x k fp32 rows per rank and the all-gather of b fp64 match records —
+        ceil(b / world) x k fp32 rows per rank and the all-gather of b fp64 match records
+        (merge="min": the all-reduce of b packed keys instead) —
         on the same transport as recognize_keys (RCCL stream-ordered, or gloo through the
         host), averaged over `reps` after one warm-up.  The caller takes the max over ranks."""
         import time
@@ -204,9 +249,13 @@ class ShardedGallery:
         gloo = dist.get_backend(self.group) != "nccl"
         parts = torch.empty((self.world * b, 3), dtype=torch.int64, device=device)
 
+        kmin = torch.zeros(b, dtype=torch.int64, device=device)
+
         def one():
             self._allgather_rows(loc, full)
-            if gloo:
+            if self.merge == "min":
+                self._min_reduce(kmin)
+            elif gloo:
                 chunks = [torch.empty((b, 3), dtype=torch.int64) for _ in range(self.world)]
                 dist.all_gather(chunks, rec.cpu(), group=self.group)
                 parts.copy_(torch.cat(chunks))

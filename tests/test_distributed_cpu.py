@@ -66,7 +66,7 @@ def _oracle_keys(q, g, metric):
     return _oracle_matches(q, g, 0, metric)["key"]
 
 
-def _worker(rank, world, port, g, q, metric, out):
+def _worker(rank, world, port, g, q, metric, out, merge="exact"):
     import sys
     for p in (ROOT, PKG):
         if p not in sys.path:
@@ -77,7 +77,7 @@ def _worker(rank, world, port, g, q, metric, out):
     from eigenface.distributed import ShardedGallery, shard_range
     lo, hi = shard_range(len(g), rank, world)
     sg = ShardedGallery(None, g[lo:hi], len(g), rank, world,
-                        local_matches=lambda qq, m: _oracle_matches(qq, g[lo:hi], lo, m))
+                        local_matches=lambda qq, m: _oracle_matches(qq, g[lo:hi], lo, m), merge=merge)
     keys = sg.search_keys(q, metric)
     out[rank] = keys.numpy().copy()
     dist.destroy_process_group()
@@ -268,3 +268,58 @@ def test_sharded_merge_is_fp64_exact_across_shards(world):
         for r in range(world):
             idx, _ = decode_keys(res[metric][r], metric)
             np.testing.assert_array_equal(idx, want)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_min_allreduce_merge(world):
+    """merge="min" (the north star's single all-reduce(MIN) of packed keys): equal to the
+    exact merge on duplicates and cosine ties across shards; on the sub-ulp case (winners
+    of different shards tied in fp32, not in fp64) it keeps the lower index, where the
+    exact merge returns the fp64 winner."""
+    rng = np.random.default_rng(40 + world)
+    g = rng.standard_normal((1001, 24)).astype(np.float32)
+    g[600] = g[17]
+    g[999] = 3.0 * g[40]
+    q = rng.standard_normal((64, 24)).astype(np.float32)
+    q[0] = g[17]
+    q[1] = g[40]
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    for metric in ("l2", "cosine"):
+        out = mgr.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, g, q, metric, out, "min")) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+        full = _oracle_keys(q, g, metric)
+        for r in range(world):
+            np.testing.assert_array_equal(out[r], full)
+    gs, qs, ra, rb = sub_ulp_case()
+    from eigenface import decode_keys
+    from eigenface.distributed import shard_range
+    shard = [next(r for r in range(world) if shard_range(len(gs), r, world)[0] <= i < shard_range(len(gs), r, world)[1])
+             for i in range(len(gs))]
+    # across shards the fp32 tie keeps the lower index; inside one shard its fp64 resolution holds
+    want_all = [a if shard[a] != shard[b] else b for a, b in zip(ra, rb)]
+    for metric, qq, want in (("l2", qs[:2], want_all[:2]), ("cosine", qs[2:], want_all[2:])):
+        out = mgr.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, gs, qq, metric, out, "min")) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+        for r in range(world):
+            idx, _ = decode_keys(out[r], metric)
+            np.testing.assert_array_equal(idx, want)
+
+
+def test_merge_mode_is_checked():
+    _paths()
+    from eigenface.distributed import ShardedGallery
+    with pytest.raises(ValueError):
+        ShardedGallery(None, None, 10, 0, 1, merge="sum")

@@ -45,8 +45,13 @@ def test_bench_two_ranks_one_gpu(metric):
     assert rec["value"] > 0 and rec["cpu_baseline"] is None
     # the collectives alone (gloo through the host here: an upper bound of RCCL's share)
     assert rec["exchange_ms_per_step"] > 0 and 0 < rec["exchange_share_of_step"]
+    # the north star's single all-reduce(MIN) on the same step: same keys on this data
+    om = rec["other_merge"]
+    assert om["merge"] == "min" and om["keys_identical"] is True and om["ms_per_step"] > 0
+    assert om["exchange_ms_per_step"] > 0
     print(f"2 ranks / one GPU, gloo: step {rec['ms_per_step']} ms, exchange {rec['exchange_ms_per_step']} ms "
-          f"({100 * rec['exchange_share_of_step']:.1f} %)")
+          f"({100 * rec['exchange_share_of_step']:.1f} %); merge=min: step {om['ms_per_step']} ms, "
+          f"exchange {om['exchange_ms_per_step']} ms")
 
 
 @pytest.mark.parametrize("ranks,gallery", [(4, 200_000), (3, 200_003)])
