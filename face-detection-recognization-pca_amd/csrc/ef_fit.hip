@@ -65,6 +65,19 @@ hipError_t dense_gemm(ef_ctx* c, hipStream_t s, const Operand& A, const Operand&
                       double* bt_scratch = nullptr) {
   (void)c;
   const bool small_out = M * N <= (int64_t)512 * 512 && K >= 4096;
+  // Y^T.Y, Q^T.Y (small output, long K, A given transposed): B transposed once into
+  // bt_scratch, then the register-direct tall kernel walking down A's rows with split-K —
+  // the LDS-staged split-K gemm64 is latency-bound here (C3: 79 + 18 us per product)
+  bool tn_tall = true;
+#ifdef EF_DIAGNOSTICS
+  if (const char* e = getenv("EF_FIT_TN_TALL")) tn_tall = atoi(e) != 0;
+#endif
+  if (tn_tall && bt_scratch && small_out && A.trans && !B.trans && !A.u8 && !B.u8 && tall_gemm_supported(A.ld, A.p, 8) &&
+      tall_gemm_supported(K, bt_scratch, 8)) {
+    hipError_t e = launch_transpose_f64(s, B.p, B.ld, K, N, bt_scratch, K);
+    if (e != hipSuccess) return e;
+    return tall_gemm_f64(s, A.p, A.ld, true, bt_scratch, K, C, ldc, M, N, K, alpha, work, work_elems);
+  }
   if (bt_scratch && !A.u8 && !B.u8 && !A.trans && !B.trans && !small_out && tall_gemm_supported(A.ld, A.p, 8) &&
       tall_gemm_supported(K, bt_scratch, 8)) {
     hipError_t e = launch_transpose_f64(s, B.p, B.ld, K, N, bt_scratch, K);
@@ -194,7 +207,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     carried = false;
     if (carry) std::swap(Q, Qold);
     EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
-                         kWorkElems),
+                         kWorkElems, Bt),
            "G = Y^T.Y");
     int hinfo = -1;
     const bool fused = chol_inv_supported(m);  // Cholesky + L^-1 in one register-resident workgroup
@@ -228,7 +241,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     }
     // rank-deficient block: eigen-orthonormalisation with a floored spectrum
     EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m, work,
-                         kWorkElems),
+                         kWorkElems, Bt),
            "G = Y^T.Y");
     EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(G)"));
     EF_HIP(c, launch_scale_cols_rsqrt(s, V, m, m, lam, W2), "W.L^-1/2");
@@ -323,7 +336,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     const bool rr = early || it == next_rr || it == max_iters;
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
-                           work, kWorkElems),
+                           work, kWorkElems, Bt),
              "H = Q^T.C.Q");
       // A Rayleigh-Ritz step after reduced-precision products can never be the converged
       // one (that needs two steps after fp64 products), and its Ritz values only steer the
