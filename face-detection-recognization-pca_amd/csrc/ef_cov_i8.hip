@@ -752,11 +752,12 @@ static int syrk_tile_cols(int64_t dim) {
 }
 
 // Tiles (256 rows x tj columns) that hold an upper-triangle element, in blocks of 8 row
-// tiles x (2048 / tj) column tiles: consecutive list entries run together on one XCD and
-// share their panels in its L2.
+// tiles x bw column tiles: consecutive list entries run together on one XCD and share their
+// panels in its L2.  bw = 3 on the 384-column tiles measured 1% faster than 5 or 4
+// (profiles/r04/syrk_block_width_ab.txt).
 static std::vector<int2> syrk_tiles(int64_t dim, int tj) {
   const int nti = (int)((dim + YT - 1) / YT), ntj = (int)((dim + tj - 1) / tj);
-  const int bw = 2048 / tj;
+  const int bw = tj == 384 ? 3 : 2048 / tj;
   std::vector<int2> order;
   for (int bi = 0; bi < nti; bi += 8)
     for (int bj = 0; bj < ntj; bj += bw)
