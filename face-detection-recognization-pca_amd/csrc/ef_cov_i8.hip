@@ -757,11 +757,15 @@ static int syrk_tile_cols(int64_t dim) {
 // (profiles/r04/syrk_block_width_ab.txt).
 static std::vector<int2> syrk_tiles(int64_t dim, int tj) {
   const int nti = (int)((dim + YT - 1) / YT), ntj = (int)((dim + tj - 1) / tj);
-  const int bw = tj == 384 ? 3 : 2048 / tj;
+#ifndef EF_SYRK_BH  // block shape override (variant builds: experiments)
+  const int bw = tj == 384 ? 3 : 2048 / tj, bh = 8;
+#else
+  const int bw = EF_SYRK_BW, bh = EF_SYRK_BH;
+#endif
   std::vector<int2> order;
-  for (int bi = 0; bi < nti; bi += 8)
+  for (int bi = 0; bi < nti; bi += bh)
     for (int bj = 0; bj < ntj; bj += bw)
-      for (int ti = bi; ti < bi + 8 && ti < nti; ++ti)
+      for (int ti = bi; ti < bi + bh && ti < nti; ++ti)
         for (int tj_ = bj; tj_ < bj + bw && tj_ < ntj; ++tj_)
           if (std::min<int64_t>((int64_t)tj_ * tj + tj - 1, dim - 1) >= (int64_t)ti * YT) order.push_back(make_int2(ti, tj_));
   return order;
