@@ -13,8 +13,12 @@ cp $C/pmc_sq/run_counter_collection.csv $P/c5_pmc_sq_counters.csv
 cp $C/proj_fetch/run_counter_collection.csv $P/c5proj_pmc_fetch_counters.csv
 cp $C/proj_write/run_counter_collection.csv $P/c5proj_pmc_write_counters.csv
 cp $C/proj_sq/run_counter_collection.csv $P/c5proj_pmc_sq_counters.csv
-cp $C/pmc_summary_c5s3.json $C/pmc_summary_c5proj.json $P/
-cp $C/l2.txt $P/c5_l2_counters.txt
+cp $C/pmc_summary_c5proj.json $P/
+if [ -f $C/pmc_summary_c5hi.json ]; then  # c5_pmc.sh default: the single-bf16 screen
+  cp $C/pmc_summary_c5hi.json $P/ && cp $C/l2.txt $P/c5hi_l2_counters.txt
+else
+  cp $C/pmc_summary_c5s3.json $P/ && cp $C/l2.txt $P/c5_l2_counters.txt
+fi
 cp gpurun_out/${T}_fit/breakdown.txt $P/fit_c3_breakdown.txt
 cp gpurun_out/${T}_fit/kernel_stats.csv $P/fit_c3_kernel_stats.csv
 cp gpurun_out/${T}_img/kernel_stats.csv $P/image_kernel_stats.csv
