@@ -62,13 +62,27 @@ static void time_it(K k, const T* in, T* out, int iters, double flop_per_iter_wa
   printf("%-24s %.3f ms  %.1f TF/s\n", name, ms, tf);
 }
 
-int main() {
+int main(int argc, char** argv) {
   double* in;
   double* out;
   (void)hipMalloc(&in, 4096 * 8);
   (void)hipMalloc(&out, 1 << 22);
   (void)hipMemset(in, 0, 4096 * 8);
   const int it = 20000;
+  if (argc > 1) {  // "rand": fp64 shapes on random operands in [-1, 1) (the power-limited rate)
+    double h[4096];
+    unsigned long long st = 1;
+    for (double& v : h) {
+      st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+      v = (double)(st >> 11) / 4503599627370496.0 - 1.0;
+    }
+    (void)hipMemcpy(in, h, sizeof h, hipMemcpyHostToDevice);
+    for (int rep = 0; rep < 3; ++rep) {
+      time_it(f64_rate<16>, in, out, it, 4.0 * 16 * 2048, "rand f64 16x16x4, 16 acc");
+      time_it(f64_rate<8>, in, out, it, 4.0 * 8 * 2048, "rand f64 16x16x4, 8 acc, 2 w/SIMD", 512);
+    }
+    return 0;
+  }
   time_it(f64_rate<16>, in, out, it, 4.0 * 16 * 2048, "f64 16x16x4, 16 acc");
   time_it(f64_rate<4>, in, out, it, 4.0 * 4 * 2048, "f64 16x16x4, 4 acc");
   time_it(f64_rate<8>, in, out, it, 4.0 * 8 * 2048, "f64 16x16x4, 8 acc, 2 w/SIMD", 512);
