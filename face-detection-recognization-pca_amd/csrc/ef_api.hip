@@ -85,23 +85,44 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
     if (_e != hipSuccess) return hip_err(ctx, _e, what);  \
   } while (0)
 
-// Search the probes already in ctx->q_pad (bpad rows, kp = ctx->g_kp) of this rank's
-// gallery: keys_dev[b] and, when match_dev is non-null, the fp64 match records.  The search
-// kernels address probe rows with 32-bit byte offsets, so a batch with bpad x kp x 4 >= 2^31
-// (wide features, k > 512) is searched in pieces of whole 256-probe tiles.
+// The pieces search_local launches for b probes of kp floats: whole 256-probe tiles, at
+// most as many per piece as keep a probe row's byte offset below 2^31 (the kernels' 32-bit
+// offsets).  Piece i covers probes [off, off + b) and is launched with bpad =
+// round_up(b, 256) rows, and its plan is built from that same bpad — never from the
+// caller's q_pad row count, which can be larger (the sharded projection pads
+// R * ceil(b / R) rows): a plan whose probe-tile count differs from the launch's row count
+// makes the kernels' part_key stride disagree between chunks.
+std::vector<SearchPiece> search_pieces(int64_t b, int kp) {
+  std::vector<SearchPiece> v;
+  const int64_t row_bytes = (int64_t)kp * 4;
+  const int64_t piece = std::max<int64_t>(kSearchProbeTile, ((int64_t)INT_MAX / row_bytes) / kSearchProbeTile * kSearchProbeTile);
+  for (int64_t off = 0; off < b; off += piece) {
+    const int64_t bi = std::min(piece, b - off);
+    v.push_back(SearchPiece{off, bi, round_up(bi, kSearchProbeTile)});
+  }
+  return v;
+}
+
+// Search the probes already in ctx->q_pad (at least round_up(b, 256) rows, kp = ctx->g_kp)
+// of this rank's gallery: keys_dev[b] and, when match_dev is non-null, the fp64 match
+// records, piece by piece (search_pieces).
 static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long long* keys_dev, ef_match* match_dev) {
   if (c->n_gallery == 0) {
     EF_HIP(c, launch_keys_none(c->stream, keys_dev, b, match_dev), "keys");
     return EF_OK;
   }
-  const int64_t row_bytes = (int64_t)c->g_kp * 4;
-  const int64_t piece = std::max<int64_t>(kSearchProbeTile, ((int64_t)INT_MAX / row_bytes) / kSearchProbeTile * kSearchProbeTile);
-  const int64_t bpad_max = std::min(bpad, piece);
-  const SearchPlan pl_max = search_plan(bpad_max, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
-  // the last piece may be shorter, and a shorter piece's plan may have more chunks
-  const int64_t bpad_last = b > piece ? round_up(b - (b - 1) / piece * piece, kSearchProbeTile) : bpad_max;
-  const SearchPlan pl_last = search_plan(bpad_last, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0);
-  const size_t parts = (size_t)std::max<int64_t>(pl_max.nchunks * bpad_max, pl_last.nchunks * bpad_last);
+  if (bpad < round_up(b, kSearchProbeTile))
+    return set_err(c, EF_E_INVALID, "search: probe buffer shorter than the batch");
+  const std::vector<SearchPiece> pieces = search_pieces(b, c->g_kp);
+  std::vector<SearchPlan> plans;
+  int64_t bpad_max = 0;
+  size_t parts = 0;
+  for (const SearchPiece& p : pieces) {
+    // a shorter last piece's plan may have more chunks
+    plans.push_back(search_plan(p.bpad, c->n_gallery, c->g_kp, c->opt_search_split_bf16 != 0));
+    bpad_max = std::max(bpad_max, p.bpad);
+    parts = std::max(parts, (size_t)plans.back().nchunks * (size_t)p.bpad);
+  }
   // workspace carve-out (16-byte aligned pieces), sized for the largest piece
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t nkb = al(parts * 8), nb2 = al(parts * 4);
@@ -145,14 +166,13 @@ static int search_local(ef_ctx* c, int64_t bpad, int64_t b, int metric, long lon
     }
     G3 = static_cast<const float*>(c->G3.p);
   }
-  for (int64_t off = 0; off < b; off += piece) {
-    const int64_t bi = std::min(piece, b - off), bpad_i = round_up(bi, kSearchProbeTile);
-    const SearchPlan& pl = bpad_i == bpad_max ? pl_max : pl_last;
-    ws.match = match_dev ? match_dev + off : nullptr;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    const SearchPiece& p = pieces[i];
+    ws.match = match_dev ? match_dev + p.off : nullptr;
     EF_HIP(c,
-           launch_search(c->stream, c->g_kp, metric, pl, static_cast<const float*>(c->q_pad.p) + off * c->g_kp, Q3,
-                         bpad_i, bi, static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset,
-                         c->gmax2_host, ws, keys_dev + off, c),
+           launch_search(c->stream, c->g_kp, metric, plans[i], static_cast<const float*>(c->q_pad.p) + p.off * c->g_kp,
+                         Q3, p.bpad, p.b, static_cast<const float*>(c->G.p), G3, aux, c->n_gallery, c->g_offset,
+                         c->gmax2_host, ws, keys_dev + p.off, c),
            "search");
   }
   return EF_OK;
@@ -328,6 +348,26 @@ using namespace ef;
 extern "C" {
 
 int ef_api_version(void) { return EF_API_VERSION; }
+
+int ef_search_schedule(int64_t b, int32_t k, int64_t n, int32_t split_bf16, int64_t* pieces_out, int32_t max_pieces,
+                       int32_t* n_pieces) {
+  if (b < 0 || k < 1 || k > 65536 || n < 1 || !n_pieces || max_pieces < 0 || (max_pieces > 0 && !pieces_out))
+    return EF_E_INVALID;
+  const int kp = feature_pad(k);
+  const std::vector<SearchPiece> pieces = search_pieces(b, kp);
+  *n_pieces = (int32_t)pieces.size();
+  for (size_t i = 0; i < pieces.size() && (int64_t)i < max_pieces; ++i) {
+    const SearchPlan pl = search_plan(pieces[i].bpad, n, kp, split_bf16 != 0);
+    int64_t* o = pieces_out + 6 * i;
+    o[0] = pieces[i].off;
+    o[1] = pieces[i].b;
+    o[2] = pieces[i].bpad;
+    o[3] = pl.n_ptiles;
+    o[4] = pl.nchunks;
+    o[5] = (int64_t)pl.tiles_per_chunk;
+  }
+  return EF_OK;
+}
 
 int ef_device_count(int* out) {
   if (!out) return EF_E_INVALID;

@@ -60,6 +60,12 @@ struct SearchPlan {
   int c_chunks = 1, c_tpc = 1, c_grid = 8;
 };
 
+// one launch of a (possibly piecewise) search: probes [off, off + b), launched and planned
+// with bpad = round_up(b, 256) rows (ef_api.hip search_pieces)
+struct SearchPiece {
+  int64_t off, b, bpad;
+};
+
 // ---- device buffer ------------------------------------------------------------------
 struct DevBuf {
   void* p = nullptr;
@@ -173,6 +179,7 @@ void timer_commit(ef_ctx* c, TimerEvt* t);
 
 // ---- launchers (defined in the .hip files) -------------------------------------------
 SearchPlan search_plan(int64_t bpad, int64_t n, int kp, bool s3);
+std::vector<SearchPiece> search_pieces(int64_t b, int kp);
 // G3: split-bf16 copy of G (EF_OPT_SEARCH_SPLIT_BF16) or null for the fp32 kernels; Q3: scratch
 // [bpad][kp] for the split probes (kp > 128 with G3 only)
 hipError_t launch_search(hipStream_t s, int kp, int metric, const SearchPlan& pl, const float* qpad, float* Q3,

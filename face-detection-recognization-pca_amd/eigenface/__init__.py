@@ -11,6 +11,7 @@ from .pca import (  # noqa: F401
     EigenfacePCA,
     get_engine,
     invalidate_uploads,
+    set_resident_check,
     load_gallery_cache,
     manual_pca,
     recognize_face,
@@ -23,7 +24,7 @@ from .pca import (  # noqa: F401
 
 __all__ = [
     "Engine", "FitResult", "decode_keys", "device_count", "EigenfacePCA", "get_engine",
-    "invalidate_uploads", "manual_pca", "recognize_face", "recognize_face_with_model", "recognize_faces",
+    "invalidate_uploads", "set_resident_check", "manual_pca", "recognize_face", "recognize_face_with_model", "recognize_faces",
     "recognize_face_dual_model", "recognize_faces_dual_model", "merge_matches_host", "EigenfaceError",
     "NativeLibraryError", "LIB_PATH", "save_gallery_cache", "load_gallery_cache", "ManualPCA",
     "ManualStandardScaler", "project_face_to_eigenspace", "cosine_similarity",

@@ -83,6 +83,7 @@ _SIGS = {
     "ef_search": ([vp, vp, i64, i32, vp, u32], C.c_int),
     "ef_recognize": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
     "ef_keys_decode": ([vp, i64, i32, vp, vp], None),
+    "ef_search_schedule": ([i64, i32, i64, i32, vp, i32, C.POINTER(i32)], C.c_int),
     "ef_search_matches": ([vp, vp, i64, i32, vp, u32], C.c_int),
     "ef_recognize_matches": ([vp, vp, i32, i64, i32, vp, vp, u32], C.c_int),
     "ef_matches_merge": ([vp, vp, i32, i64, vp, vp, u32], C.c_int),
@@ -146,7 +147,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 5:
+        if h.ef_api_version() != 6:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

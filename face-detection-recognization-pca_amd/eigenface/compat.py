@@ -377,8 +377,12 @@ def visualize_eigenfaces(eigenfaces, mean_face, output_dir, person_name, n_displ
 
 # ------------------------------------------------------------------ scanner
 def _model_projection(md):
-    """Fold a face_model.pkl's scaler + pca into (mean, W) for the GPU projection."""
-    pca = md.get("pca", md.get("pca_model"))
+    """Fold a face_model.pkl's scaler + pca into (mean, W) for the GPU projection.  The
+    estimator is read from ``md['pca']`` only, as scan-template-v4.py:266 does: a model
+    dict without that key (the reference's own faces/lock_version/Joseph_Lai/face_model.pkl
+    is keyed ``pca_model``) raises ``KeyError('pca')``, which the per-model ``try`` of
+    recognize_faces_all_models reports and skips, exactly as the reference (:312-314)."""
+    pca = md["pca"]
     sc = md["scaler"]
     comp = np.asarray(pca.components_, dtype=np.float64)
     scale = np.asarray(sc.scale_, dtype=np.float64)
@@ -393,7 +397,7 @@ _fold_cache: dict = {}
 def _folded(md):
     """(mean, W) of a model dict, folded once per model (the cache keeps the dict and the
     estimator arrays it was folded from, so a replaced or refitted estimator re-folds)."""
-    pca = md.get("pca", md.get("pca_model"))
+    pca = md["pca"]  # no fallback key: see _model_projection
     sc = md["scaler"]
     src = (pca.components_, pca.mean_, sc.mean_, sc.scale_)
     hit = _fold_cache.get(id(md))

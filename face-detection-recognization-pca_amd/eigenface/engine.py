@@ -152,13 +152,15 @@ class Engine:
         return int(s.value or 0)
 
     @contextlib.contextmanager
-    def _torch_order(self, *outs):
+    def _torch_order(self, *tensors):
         """Stream order of a call on device tensors when the engine runs on its own stream:
         the engine's stream first waits for torch's current stream (the inputs' producers),
-        then torch's current stream waits for the engine's (the outputs' consumers), and the
-        output tensors are marked as used on the engine's stream (so the caching allocator
-        does not hand their memory out before the engine's kernels are done).  No host
-        wait either way; a no-op when the engine already runs on torch's stream."""
+        then torch's current stream waits for the engine's (the outputs' consumers), and
+        every tensor the call reads or writes — inputs included, e.g. a dtype-converted
+        temporary that dies when the wrapper returns — is marked as used on the engine's
+        stream, so the caching allocator hands its memory to no other stream before the
+        engine's kernels are done.  No host wait either way; a no-op when the engine
+        already runs on torch's stream."""
         import torch
         h = self.stream_handle()
         cur = torch.cuda.current_stream(self.device)
@@ -169,7 +171,7 @@ class Engine:
         ext.wait_stream(cur)
         yield
         cur.wait_stream(ext)
-        for t in outs:
+        for t in tensors:
             if t is not None:
                 t.record_stream(ext)
 
@@ -270,7 +272,7 @@ class Engine:
         k_out = C.c_int32(0)
         it = C.c_int32(0)
         flags = (N.EF_FIT_STANDARDIZE if standardize else 0) | (N.EF_MEM_DEVICE if dev else 0)
-        with (self._torch_order() if dev else contextlib.nullcontext()):
+        with (self._torch_order(x, mean, var, scale, comps, eig, proj, tv) if dev else contextlib.nullcontext()):
             self._chk(self._lib.ef_fit_ex(
                 self._h, xp, xdt, n, d, k, flags, ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig),
                 ptr(proj) if proj is not None else None, ptr(tv), C.byref(k_out), C.byref(it)))
@@ -290,7 +292,7 @@ class Engine:
             import torch
             mean = torch.empty(d, dtype=torch.float64, device=x.device)
             var = torch.empty(d, dtype=torch.float64, device=x.device)
-            with self._torch_order(mean, var):
+            with self._torch_order(x, mean, var):
                 self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, N.EF_MEM_DEVICE, mean.data_ptr(),
                                                 var.data_ptr()))
             self.synchronize()
@@ -355,7 +357,7 @@ class Engine:
             if out is None:
                 out = torch.empty((b, self.model_k), dtype=torch.float32, device=p.device)
             self._dev_out(out, (b, self.model_k), torch.float32, "out")
-            with self._torch_order(out):
+            with self._torch_order(p, out):
                 self._chk(self._lib.ef_project(self._h, pp, dtype, b, out.data_ptr(), N.EF_MEM_DEVICE))
             return out
         p = np.asarray(P)
@@ -399,7 +401,7 @@ class Engine:
             if keys is None:
                 keys = torch.empty(b, dtype=torch.int64, device=q.device)
             self._dev_out(keys, (b,), torch.int64, "keys")
-            with self._torch_order(keys):
+            with self._torch_order(q, keys):
                 self._chk(self._lib.ef_search(self._h, qp, b, mt, keys.data_ptr(), N.EF_MEM_DEVICE))
             return keys
         q, qp = _host(Q, np.float32)
@@ -432,7 +434,7 @@ class Engine:
             fp = None
             if feats is not None:
                 fp = self._dev_out(feats, (b, self.model_k), torch.float32, "feats").data_ptr()
-            with self._torch_order(keys, feats):
+            with self._torch_order(p, keys, feats):
                 self._chk(self._lib.ef_recognize(self._h, pp, dtype, b, mt, keys.data_ptr(), fp, N.EF_MEM_DEVICE))
             return keys
         p = np.asarray(P)
@@ -479,7 +481,7 @@ class Engine:
             if out is None:
                 out = torch.empty((b, 3), dtype=torch.int64, device=x.device)
             self._dev_out(out, (b, 3), torch.int64, "out")
-            with self._torch_order(out):
+            with self._torch_order(x, out):
                 if search:
                     self._chk(self._lib.ef_search_matches(self._h, xp, b, mt, out.data_ptr(), N.EF_MEM_DEVICE))
                 else:
@@ -525,7 +527,7 @@ class Engine:
                   and keys.device == parts.device):
             raise ValueError(f"keys must be a contiguous int64 tensor of shape ({b},) on {parts.device}")
         if b:
-            with self._torch_order(keys):
+            with self._torch_order(parts, keys):
                 self._chk(self._lib.ef_matches_merge(self._h, parts.data_ptr(), nparts, b, keys.data_ptr(), None,
                                                      N.EF_MEM_DEVICE))
         return keys

@@ -194,17 +194,44 @@ class _ArrayToken:
     so an in-place edit anywhere (re-enrolling one person's row of a large gallery) makes
     the next call re-upload — the reference reads the array it is given on every call.
     The digest is xxh3-128 (~20 GB/s on one host core: a 1M x 128 fp32 gallery costs
-    ~25 ms, half of what its re-upload over PCIe would), blake2b where xxhash is absent."""
+    ~25 ms, half of what its re-upload over PCIe would; the 2 GB C5 gallery ~100 ms),
+    blake2b (seconds per GB) where xxhash is absent.  It is paid on EVERY recognise call,
+    which dominates single-face calls on large galleries: a caller that never edits its
+    arrays in place can switch it off with ``set_resident_check("identity")`` (same
+    object, pointer, shape and dtype only) and call :func:`invalidate_uploads` after any
+    edit."""
 
     def __init__(self, a):
         self.a = a
         self.ptr = a.__array_interface__["data"][0]
         self.shape, self.dtype = a.shape, a.dtype
-        self.digest = _digest(a)
+        self.digest = _digest(a) if _RESIDENT_CHECK == "digest" else None
 
     def matches(self, a):
-        return (a is self.a and a.shape == self.shape and a.dtype == self.dtype
-                and a.__array_interface__["data"][0] == self.ptr and _digest(a) == self.digest)
+        if not (a is self.a and a.shape == self.shape and a.dtype == self.dtype
+                and a.__array_interface__["data"][0] == self.ptr):
+            return False
+        if _RESIDENT_CHECK != "digest":
+            return True
+        if self.digest is None:  # token made while the check was off: digest it now
+            self.digest = _digest(a)
+            return False
+        return _digest(a) == self.digest
+
+
+_RESIDENT_CHECK = "digest"
+
+
+def set_resident_check(mode: str):
+    """How the recognise helpers decide that a resident gallery / model is still the host
+    array they are given: "digest" (default: a full xxh3-128 hash of its bytes per call,
+    so in-place edits re-upload) or "identity" (the same array object, pointer, shape and
+    dtype — no per-call hashing; the caller promises not to edit resident arrays in place
+    or calls invalidate_uploads after doing so)."""
+    global _RESIDENT_CHECK
+    if mode not in ("digest", "identity"):
+        raise ValueError("mode must be 'digest' or 'identity'")
+    _RESIDENT_CHECK = mode
 
 
 try:
@@ -279,7 +306,9 @@ def recognize_face(face_vector, model_data, similarity_threshold=0.7, device=0):
 
 def recognize_faces(face_vectors, model_data, similarity_threshold=0.7, device=0):
     """Batched ``recognize_face``: one GPU projection + cosine arg-best for all rows of
-    ``face_vectors`` (b, d) — the loop useless/scan.py:168-215 runs per detection."""
+    ``face_vectors`` (b, d) — the loop useless/scan.py:168-215 runs per detection.
+    Each call hashes the model's and gallery's host arrays to decide whether the resident
+    copies are current (``_ArrayToken``; ~25 ms per 512 MB): see set_resident_check."""
     mean, ef = _as_array(model_data["mean_face"]), _as_array(model_data["eigenfaces"])
     eng = _model_engine(mean, ef, device)
     _gallery_engine(_as_array(model_data["projected_data"]), device)

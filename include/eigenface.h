@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 5
+#define EF_API_VERSION 6
 
 /* status codes */
 #define EF_OK 0
@@ -160,6 +160,14 @@ int ef_recognize(ef_ctx* ctx, const void* P, int32_t p_dtype, int64_t b, int32_t
 /* Host-side key decoding: L2 -> squared distance, COSINE -> similarity;
  * EF_KEY_NONE -> idx -1, best NaN. */
 void ef_keys_decode(const int64_t* keys, int64_t b, int32_t metric, float* best, int64_t* idx);
+/* Host-side introspection (no ctx, no GPU): the launches a search of b probes of k features
+ * over an n-row gallery makes.  A batch whose padded probe block would pass 2 GiB (k > 512)
+ * is searched in pieces of whole 256-probe tiles.  *n_pieces = the piece count; for the
+ * first max_pieces pieces, pieces_out[6*i ..] = {first probe, probes, padded rows the
+ * piece is launched with, probe tiles of its plan, gallery chunks, row tiles per chunk}.
+ * split_bf16 as EF_OPT_SEARCH_SPLIT_BF16.  (API v6) */
+int ef_search_schedule(int64_t b, int32_t k, int64_t n, int32_t split_bf16, int64_t* pieces_out, int32_t max_pieces,
+                       int32_t* n_pieces);
 
 /* ------------------------------------------------ exact cross-shard arg-best
  * A key's fp32 score cannot order two shards' winners whose fp64 scores differ by less

@@ -261,3 +261,65 @@ def test_gallery_cache_recognize(tmp_path):
     idx1, s1 = m2.recognize(x[:50], "cosine")
     np.testing.assert_array_equal(idx1, idx0)
     np.testing.assert_array_equal(s1, s0)
+
+
+def test_model_without_pca_key_is_skipped_like_the_reference(tmp_path, capsys):
+    """a face_model.pkl keyed 'pca_model' instead of 'pca' — the layout of
+    the reference's own faces/lock_version/Joseph_Lai/face_model.pkl (SURVEY Appendix A:
+    float32 arrays, mean_face = pca.mean_; rebuilt here synthetically, the reference's
+    pickle is not read) — raises KeyError('pca') at scan-template-v4.py:266; the per-model
+    try prints "Error recognizing with model <name>: 'pca'" and skips the model (:312-314).
+    Alone it yields (-1, 'unknown', 0.0) for every face; beside a well-formed model it
+    changes nothing."""
+    from eigenface.cli import train_v4
+    from eigenface.compat import load_all_models, recognize_face_all_models, recognize_faces_all_models
+    xa = _person_dir(str(tmp_path), "alice", 120, 1)
+    assert train_v4("alice", str(tmp_path)) is True
+    base = tmp_path / "faces" / "lock_version"
+    good = pickle.load(open(base / "alice" / "face_model.pkl", "rb"))  # written by this package
+    bad = {k: v for k, v in good.items() if k != "pca"}
+    bad["pca_model"] = good["pca"]
+    for key in ("face_features", "eigenfaces"):
+        bad[key] = np.asarray(good[key], dtype=np.float32)
+    bad["mean_face"] = np.asarray(good["pca"].mean_, dtype=np.float32)
+    bad["person_id_map"] = {"joseph": 0}
+    jdir = tmp_path / "solo" / "faces" / "lock_version" / "joseph"
+    jdir.mkdir(parents=True)
+    pickle.dump(bad, open(jdir / "face_model.pkl", "wb"))
+    faces = [xa[i].reshape(64, 64) for i in (0, 5, 17, 33)]
+
+    solo = load_all_models(str(tmp_path / "solo"))
+    assert list(solo) == ["joseph"]
+    capsys.readouterr()
+    assert recognize_faces_all_models(faces, solo, 0.8) == [(-1, "unknown", 0.0)] * len(faces)
+    assert "Error recognizing with model joseph: 'pca'" in capsys.readouterr().out
+    assert recognize_face_all_models(faces[0], solo, 0.8) == (-1, "unknown", 0.0)
+
+    only_good = {"alice": {"model_data": good}}
+    want = recognize_faces_all_models(faces, only_good, 0.8)
+    assert [w[1] for w in want] == ["alice"] * len(faces)
+    both = {"alice": {"model_data": good}, "joseph": {"model_data": bad}}
+    capsys.readouterr()
+    assert recognize_faces_all_models(faces, both, 0.8) == want
+    assert "Error recognizing with model joseph: 'pca'" in capsys.readouterr().out
+    both_rev = {"joseph": {"model_data": bad}, "alice": {"model_data": good}}
+    assert recognize_faces_all_models(faces, both_rev, 0.8) == want
+
+
+def test_resident_check_identity_mode():
+    """set_resident_check('identity') skips the per-call digest; an in-place edit
+    then needs invalidate_uploads (documented contract), after which the edit is seen."""
+    from eigenface import invalidate_uploads, recognize_face_with_model, set_resident_check
+    g = np.random.default_rng(4).standard_normal((64, 10))
+    md = {"face_features": g, "face_labels": np.arange(64), "person_id_map": {f"p{i}": i for i in range(64)}}
+    set_resident_check("identity")
+    try:
+        assert recognize_face_with_model(g[9], md, threshold=0.5)[0] == 9
+        assert recognize_face_with_model(g[9], md, threshold=0.5)[0] == 9
+        g[9] = -g[9]
+        invalidate_uploads()
+        assert recognize_face_with_model(g[9], md, threshold=0.5)[0] == 9
+    finally:
+        set_resident_check("digest")
+    g[3] = -g[3]  # digest mode again: the edit is caught without invalidation
+    assert recognize_face_with_model(g[3], md, threshold=0.5)[0] == 3

@@ -4,31 +4,23 @@ import pytest
 
 from conftest import golden
 from oracle import eigenface_oracle as orc
+from parity_util import assert_exact_argbest
 
 pytestmark = pytest.mark.gpu
 
 
 def _check_l2(q, g, idx, best):
-    ref_idx, ref_d = orc.l2_argmin(q, g)
+    """Exact fp64 first-argmin outside the engine's 1e-12 tie window (parity_util), and
+    the reported distance is the chosen row's difference-form distance."""
+    assert_exact_argbest(q, g, idx, "l2")
     d_gpu = ((q.astype(np.float64) - g[idx].astype(np.float64)) ** 2).sum(1)
-    scale = (q.astype(np.float64) ** 2).sum(1) + (g.astype(np.float64) ** 2).max()
-    # the chosen row must be an argmin up to fp32 rounding of ||g||^2 - 2 q.g ...
-    assert np.all(d_gpu - ref_d <= 1e-5 * scale)
-    # ... and identical wherever the runner-up is not within that rounding
-    # (expanded-form fp64 distances: their cancellation error ~1e-16 * scale is far below
-    # the 1e-5 * scale margin tested here)
-    clear = np.ones(len(q), bool)
-    if len(g) >= 2:
-        g64 = g.astype(np.float64)
-        gn = (g64**2).sum(1)
-        for i0 in range(0, len(q), 512):
-            q64 = q[i0 : i0 + 512].astype(np.float64)
-            dd = (q64**2).sum(1)[:, None] + gn[None, :] - 2.0 * (q64 @ g64.T)
-            s = np.partition(dd, 1, axis=1)[:, :2]
-            clear[i0 : i0 + 512] = (s[:, 1] - s[:, 0]) > 1e-5 * scale[i0 : i0 + 512]
-    np.testing.assert_array_equal(idx[clear], ref_idx[clear])
-    # reported distance is the exact (difference-form) fp32 distance of the chosen row
-    np.testing.assert_allclose(best, d_gpu, rtol=1e-4, atol=1e-4 * np.sqrt(scale).max() * 1e-3)
+    np.testing.assert_allclose(best, d_gpu, rtol=1e-6, atol=1e-30)
+
+
+def _check_cos(q, g, idx, best):
+    assert_exact_argbest(q, g, idx, "cosine")
+    s_gpu = orc.cosine_scores(q, g)[np.arange(len(q)), idx]
+    np.testing.assert_allclose(best, s_gpu, atol=2e-6)
 
 
 @pytest.mark.parametrize("k", [8, 16, 50, 64, 96, 128, 200, 256, 300, 512])
@@ -55,11 +47,8 @@ def test_wide_xcd_block_deal(eng, k, b):
     eng.set_gallery(g)
     idx, best = eng.search(q, "l2")
     _check_l2(q, g, idx, best)
-    idx_c, _ = eng.search(q, "cosine")
-    ref_idx, _ = orc.cosine_argmax(q, g)
-    srt = np.sort(orc.cosine_scores(q, g), axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 1e-6
-    np.testing.assert_array_equal(idx_c[clear], ref_idx[clear])
+    idx_c, best_c = eng.search(q, "cosine")
+    _check_cos(q, g, idx_c, best_c)
 
 
 @pytest.mark.parametrize("k", [16, 64, 128, 256, 512])
@@ -69,13 +58,7 @@ def test_cosine_random(eng, k):
     q = rng.standard_normal((513, k)).astype(np.float32)
     eng.set_gallery(g)
     idx, best = eng.search(q, "cosine")
-    ref_idx, ref_s = orc.cosine_argmax(q, g)
-    s_gpu = orc.cosine_scores(q, g)[np.arange(len(q)), idx]
-    assert np.all(ref_s - s_gpu <= 1e-6)
-    srt = np.sort(orc.cosine_scores(q, g), axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 1e-6
-    np.testing.assert_array_equal(idx[clear], ref_idx[clear])
-    np.testing.assert_allclose(best, s_gpu, atol=2e-6)
+    _check_cos(q, g, idx, best)
 
 
 def test_cosine_ties_and_zero_norm_golden(eng):

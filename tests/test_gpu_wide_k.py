@@ -10,22 +10,11 @@ import numpy as np
 import pytest
 
 from oracle import eigenface_oracle as orc
-from test_gpu_search import _check_l2
+from test_gpu_search import _check_cos as _cos_check, _check_l2
 
 pytestmark = pytest.mark.gpu
 
 WIDE_K = [513, 601, 1024]
-
-
-def _cos_check(q, g, idx, best):
-    ref_idx, ref_s = orc.cosine_argmax(q, g)
-    sc = orc.cosine_scores(q, g)
-    s_gpu = sc[np.arange(len(q)), idx]
-    assert np.all(ref_s - s_gpu <= 1e-6)
-    srt = np.sort(sc, axis=1)
-    clear = (srt[:, -1] - srt[:, -2]) > 1e-6 if sc.shape[1] > 1 else np.ones(len(q), bool)
-    np.testing.assert_array_equal(idx[clear], ref_idx[clear])
-    np.testing.assert_allclose(best, s_gpu, atol=2e-6)
 
 
 @pytest.fixture(params=[0, 1, 2], ids=["fp32", "split16", "split32"])

@@ -61,7 +61,7 @@ def test_one_hip_runtime_per_process():
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
-    assert lib.ef_api_version() == 5
+    assert lib.ef_api_version() == 6
     n = ctypes.c_int(-1)
     assert lib.ef_device_count(ctypes.byref(n)) == 0
     if n.value == 0:  # build container: creating a context must fail cleanly, not crash
@@ -193,3 +193,43 @@ def test_host_merge_checks_record_shapes():
     recs["key"] = N.EF_KEY_NONE
     recs["score"] = np.inf
     assert (merge_matches_host(recs, 3) == N.EF_KEY_NONE).all()
+
+
+def test_search_schedule_plans_each_piece_from_its_launched_rows():
+    """every search launch's plan must be built from the row count the
+    piece is launched with.  The sharded projection pads its feature block to
+    round_up(R * ceil(b / R), 256) rows (b = 4096, R = 3: 4352), more than the
+    round_up(b, 256) = 4096 rows the kernels are told about; a plan built from the larger
+    count gives a part_key stride the kernels do not use.  ef_search_schedule reports what
+    search_local launches (host arithmetic, no GPU)."""
+    from eigenface import _native
+    lib = _native.lib()
+    i32 = ctypes.c_int32
+
+    def sched(b, k, n, split):
+        cnt = i32(-1)
+        assert lib.ef_search_schedule(b, k, n, split, None, 0, ctypes.byref(cnt)) == 0
+        out = np.zeros((max(cnt.value, 1), 6), np.int64)
+        assert lib.ef_search_schedule(b, k, n, split, out.ctypes.data, cnt.value, ctypes.byref(cnt)) == 0
+        return out[:cnt.value]
+
+    def kp_of(k):
+        for p in (16, 32, 64, 128, 256, 512):
+            if k <= p:
+                return p
+        return -(-k // 128) * 128
+
+    for b, k, n, split in [(4096, 128, 1_000_000, 0), (4096, 512, 1_000_000, 3), (4096, 512, 1_000_000, 0),
+                           (1, 64, 10, 0), (257, 16, 5000, 1), (8200, 65536, 20_000, 1), (8200, 65536, 20_000, 0),
+                           (3000, 601, 7001, 3), (70_000, 1024, 1000, 0), (1366, 128, 333_334, 0)]:
+        p = sched(b, k, n, split)
+        kp = kp_of(k)
+        assert p[0, 0] == 0 and p[:, 1].sum() == b
+        np.testing.assert_array_equal(p[1:, 0], np.cumsum(p[:-1, 1]))        # contiguous pieces
+        np.testing.assert_array_equal(p[:, 2], -(-p[:, 1] // 256) * 256)      # rows = round_up(b_i, 256)
+        assert np.all(p[:, 2] * kp * 4 <= 2**31 - 1) or len(p) == 1 and p[0, 2] == 256
+        tile = 256 if kp <= 128 or split else 128                               # probes per workgroup
+        np.testing.assert_array_equal(p[:, 3] * tile, p[:, 2])                  # plan == launch
+        assert np.all(p[:, 4] % 8 == 0) and np.all(p[:, 4] * p[:, 5] * (64 if kp <= 128 else 128 if not split else 256)
+                                                    >= n)
+    assert lib.ef_search_schedule(10, 0, 10, 0, None, 0, ctypes.byref(i32())) != 0
