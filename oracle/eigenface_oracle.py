@@ -211,18 +211,35 @@ def pca_cov_fit(x, n_components, standardize=True, chunk=2048):
     = its eigenvalues, sklearn's svd_flip sign rule, extmath.py:946-952), affordable
     at the C3 shape (d = 16384).  Only the top ``n_components`` pairs are computed
     (LAPACK dsyevr through scipy).  Returns the dict of :func:`pca_full_fit` plus
-    ``scaler``."""
-    import scipy.linalg as sla
+    ``scaler``.  The three phases are separate functions (cov_standardised,
+    top_eigh, project_standardised) so a CPU baseline can time them apart."""
+    k = int(n_components)
+    st = cov_standardised(x, standardize, chunk)
+    lam, vt = top_eigh(st["cov"], k)
+    del st["cov"]
+    feats = project_standardised(x, st, vt, chunk)
+    total = st["total_var"]
+    return {
+        "scaler": (st["s_mean"], st["s_var"], st["s_scale"]),
+        "mean_": st["zmean"],
+        "components_": vt,
+        "explained_variance_": lam,
+        "explained_variance_ratio_": lam / total,
+        "total_var": total,
+        "fit_transform": feats,
+    }
 
+
+def cov_standardised(x, standardize=True, chunk=2048):
+    """Phase 1 of :func:`pca_cov_fit`: StandardScaler statistics, then the fp64
+    covariance of the standardised data (PCA centres z again: _pca.py:741-743)."""
     x = np.asarray(x)
     n, d = x.shape
-    k = int(n_components)
     if standardize:
         s_mean, s_var, s_scale = standard_scaler_fit(x)
     else:
         s_mean = x.astype(np.float64).mean(axis=0)
         s_var = s_scale = np.ones(d)
-    # z = (x - mu)/sigma; PCA centres z again (mean ~1e-17) — _pca.py:741-743
     zmean = np.zeros(d)
     for a in range(0, n, chunk):
         zmean += ((x[a:a + chunk].astype(np.float64) - s_mean) / s_scale).sum(axis=0)
@@ -232,24 +249,29 @@ def pca_cov_fit(x, n_components, standardize=True, chunk=2048):
         zc = (x[a:a + chunk].astype(np.float64) - s_mean) / s_scale - zmean
         cov += zc.T @ zc
     cov /= n - 1
-    total = float(np.trace(cov))
-    lam, vec = sla.eigh(cov, subset_by_index=[d - k, d - 1], driver="evr", overwrite_a=True)
-    del cov
+    return {"s_mean": s_mean, "s_var": s_var, "s_scale": s_scale, "zmean": zmean, "cov": cov,
+            "total_var": float(np.trace(cov))}
+
+
+def top_eigh(cov, k, overwrite=True):
+    """Phase 2: the top k eigenpairs (LAPACK dsyevr), descending, svd_flip signs.
+    Returns (eigenvalues, components as rows)."""
+    import scipy.linalg as sla
+    d = cov.shape[0]
+    lam, vec = sla.eigh(cov, subset_by_index=[d - k, d - 1], driver="evr", overwrite_a=overwrite)
     order = np.argsort(lam)[::-1]
-    lam = lam[order]
     vt, _ = _svd_flip_rows(vec[:, order].T)
-    feats = np.empty((n, k))
-    for a in range(0, n, chunk):
-        feats[a:a + chunk] = ((x[a:a + chunk].astype(np.float64) - s_mean) / s_scale - zmean) @ vt.T
-    return {
-        "scaler": (s_mean, s_var, s_scale),
-        "mean_": zmean,
-        "components_": vt,
-        "explained_variance_": lam,
-        "explained_variance_ratio_": lam / total,
-        "total_var": total,
-        "fit_transform": feats,
-    }
+    return lam[order], vt
+
+
+def project_standardised(x, st, vt, chunk=2048):
+    """Phase 3: the training projection of the standardised, re-centred data."""
+    x = np.asarray(x)
+    feats = np.empty((x.shape[0], vt.shape[0]))
+    for a in range(0, x.shape[0], chunk):
+        feats[a:a + chunk] = ((x[a:a + chunk].astype(np.float64) - st["s_mean"]) / st["s_scale"]
+                              - st["zmean"]) @ vt.T
+    return feats
 
 
 def train_pca_model(face_images, n_components):

@@ -163,3 +163,36 @@ def test_manual_helpers_keep_recognition_gallery_resident():
     assert shared.gallery_owner is tok  # still resident: no re-upload on the next recognise
     assert recognize_face_with_model(feats[7], md, 0.5)[:2] == (0, "p")
     assert shared.gallery_owner is tok
+
+
+def test_fit_exact_light_spectrum(eng):
+    """Config 1's real spectrum through the GPU Gram path (within the
+    privacy decision — see DESIGN "Oracle and parity"): float64 data whose centred Gram
+    matrix has EXACTLY the 50 leading eigenvalues the reference's manual_pca gives for
+    faces/Light_version (tests/golden/light_stats.npz, an aggregate statistic) above a
+    synthetic tail, n = 229 faces, d = 10000 (> n: the Gram path of useless/train.py:82-95).
+    Eigenvalues equal the reference's at 1e-9, eigenfaces equal the constructed ones
+    (sign-aligned) at 1e-6, the projection equals U diag(sqrt((n-1) lam)); the real
+    spectrum's clustered gaps (min 1.1 %) are what stress the eigensolver.  Not covered: the
+    photographs' pixels (uint8 statistics, int8 Gram) — not committable."""
+    from eigenface import manual_pca
+    st = golden("light_stats.npz")
+    lam_ref = st["eigenvalues"]
+    n, d, k = int(st["n"]), int(st["d"]), len(lam_ref)
+    r = n - 1
+    tail = lam_ref[-1] * np.geomspace(0.97, 1e-3, r - k)
+    lam = np.concatenate([lam_ref, tail])
+    rng = np.random.default_rng(2029)
+    U = np.linalg.qr(rng.standard_normal((n, r)) - 0.0)[0]
+    U -= U.mean(0)                                    # columns orthogonal to 1: centred
+    U = np.linalg.qr(U)[0]                            # re-orthonormalise inside 1-perp
+    V = np.linalg.qr(rng.standard_normal((d, r)))[0]  # eigenfaces
+    X = (U * np.sqrt((n - 1) * lam)) @ V.T + 100.0    # mean face 100: removed by the fit
+    e, m, p, got = manual_pca(X, k)
+    np.testing.assert_allclose(m, X.mean(0), rtol=1e-13)
+    np.testing.assert_allclose(got, lam_ref, rtol=1e-9)
+    np.testing.assert_allclose(orc.manual_model_info_evr(got), st["evr_json"], atol=1e-10)
+    s = np.sign((e * V[:, :k]).sum(0))
+    np.testing.assert_allclose(e * s, V[:, :k], atol=1e-6)  # (north star: 1e-4 relative)
+    P = U[:, :k] * np.sqrt((n - 1) * lam_ref)
+    np.testing.assert_allclose(p * s, P, atol=1e-6 * np.abs(P).max())

@@ -130,3 +130,21 @@ def test_oracle_manual_pca_on_light_like_hard_spectrum():
     R = np.random.default_rng([5]).integers(0, 2, size=(x.shape[1], 8)).astype(np.float64) * 2.0 - 1.0
     np.testing.assert_allclose(comps @ R, g["comps_R"], atol=1e-8)
     np.testing.assert_allclose(comps[:, g["px"]], g["comps_px"], atol=1e-10)
+
+
+def test_oracle_exact_light_spectrum():
+    """The oracle's manual_pca on the committed real Light eigenvalues (the GPU test
+    test_gpu_manual.py::test_fit_exact_light_spectrum's construction, smaller d)."""
+    st = golden("light_stats.npz")
+    lam_ref = st["eigenvalues"]
+    n, k = int(st["n"]), len(lam_ref)
+    r = n - 1
+    lam = np.concatenate([lam_ref, lam_ref[-1] * np.geomspace(0.97, 1e-3, r - k)])
+    rng = np.random.default_rng(2029)
+    U = np.linalg.qr(rng.standard_normal((n, r)))[0]
+    U = np.linalg.qr(U - U.mean(0))[0]
+    V = np.linalg.qr(rng.standard_normal((1024, r)))[0]
+    X = (U * np.sqrt((n - 1) * lam)) @ V.T + 100.0
+    _, _, _, got = orc.manual_pca(X, k)
+    np.testing.assert_allclose(got, lam_ref, rtol=1e-10)
+    np.testing.assert_allclose(orc.manual_model_info_evr(got), st["evr_json"], atol=1e-10)
