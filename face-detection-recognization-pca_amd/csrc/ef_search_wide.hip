@@ -34,6 +34,9 @@ namespace ef {
 #ifndef EF_WIDE_INTERLEAVE
 #define EF_WIDE_INTERLEAVE 0
 #endif
+#ifndef EF_WIDE_ROLES  // wide16: 1 = waves 0-3 issue every gallery DMA piece, 4-7 every probe piece (experiment)
+#define EF_WIDE_ROLES 0
+#endif
 #ifndef EF_WIDE_SERP  // wide16: 1 = serpentine k-slice order over a sweep's tiles (experiment)
 #define EF_WIDE_SERP 1  // with EF_WIDE3_PB 8: C5 HBM fetch 12.0 -> 8.1 GB per launch, same time (profiles/r04/c5_hbm_ab.txt)
 #endif
@@ -684,6 +687,28 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
   // carries row 8 j + (l >> 3), physical chunk l & 7 = logical chunk (l & 7) ^ s(row),
   // s(row) = (row >> 1) & 5 = (4 jj + (l >> 4)) & 5.
   const int prow = lane >> 3;
+#if EF_WIDE_ROLES
+  // split roles: waves 0-3 carry the 32 gallery pieces of a slice (8 each, issued at the
+  // slice's start: the gallery streams from HBM / MALL), waves 4-7 the 32 probe pieces
+  // (L2-resident, issued at the stagger point)
+  const bool gwave = wave < 4;
+  unsigned off[8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int j = (wave & 3) * 8 + jj;
+    const unsigned lch16 = (unsigned)(((lane & 7) ^ ((4 * jj + (lane >> 4)) & 5)) * 16);
+    if (gwave) {
+      off[jj] = (unsigned)(j * 8 + prow) * (geo.kp * 4) + lch16;
+    } else {
+      const int slot = pt * W3P + j * 8 + prow;
+      int qrow = slot;
+      if constexpr (COLLECT) qrow = slot < n_amb ? ws.amb_list[slot] : 0;
+      off[jj] = (unsigned)qrow * (geo.kp * 4) + lch16;
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) asm volatile("" ::"v"(off[jj]));
+#else
   unsigned goff[4], qoff[4];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
@@ -694,14 +719,15 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     goff[jj] = (unsigned)((wave * 4 + jj) * 8 + prow) * (geo.kp * 4) + lch16;
     qoff[jj] = (unsigned)qrow * (geo.kp * 4) + lch16;
   }
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qoff[jj]));
+#endif
   float thr[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
   if constexpr (COLLECT) {
 #pragma unroll
     for (int pb = 0; pb < 4; ++pb)
       if (sl0[pb] < n_amb) thr[pb] = ws.thr[sl0[pb]];
   }
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) asm volatile("" ::"v"(qoff[jj]));
   asm volatile("" ::"v"(thr[0]), "v"(thr[1]), "v"(thr[2]), "v"(thr[3]));
 
   const unsigned lds_base = lds_addr(smem);
@@ -716,6 +742,22 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
     // slices used last by one tile are the first the next tile re-reads (L2 reuse)
     if ((t - t0) & 1) sl = NS - 1 - sl;
 #endif
+#if EF_WIDE_ROLES
+    const int jj = p, j = (wave & 3) * 8 + jj;
+    if (gwave) {
+      const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
+      const unsigned long long gb = (unsigned long long)(size_t)(G3 + t * W3R * geo.kp + sl * WBK);
+      unsigned go = off[jj];
+      if (nrem < W3R) {  // tail tile: rows past the end re-read the last row (masked later)
+        const unsigned row = go / (geo.kp * 4);
+        go = (row < (unsigned)nrem ? row : (unsigned)(nrem - 1)) * (geo.kp * 4) + go % (geo.kp * 4);
+      }
+      glds16s(go, gb, lds_base + (unsigned)((buf * 2 * W3SL + j * 256) * 4));
+    } else {
+      const unsigned long long qb = (unsigned long long)(size_t)(q3 + sl * WBK);
+      glds16s(off[jj], qb, lds_base + (unsigned)((buf * 2 * W3SL + W3SL + j * 256) * 4));
+    }
+#else
     const int jj = p >> 1, j = wave * 4 + jj;
     if ((p & 1) == 0) {
       const int nrem = (int)((n - t * W3R) < W3R ? (n - t * W3R) : W3R);
@@ -730,6 +772,7 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
       const unsigned long long qb = (unsigned long long)(size_t)(q3 + sl * WBK);
       glds16s(qoff[jj], qb, lds_base + (unsigned)((buf * 2 * W3SL + W3SL + j * 256) * 4));
     }
+#endif
   };
   auto issue = [&](int64_t it, int buf) {
     const int64_t t = t0 + geo.tile(it);

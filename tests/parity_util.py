@@ -3,7 +3,7 @@
 The engine resolves every probe's arg-best in fp64 (ef_search.hip reduce_kernel /
 resolve_kernel): the returned row is the lowest index among the rows whose fp64 score is
 within 1e-12 * (|best| + scale) of the best, with scale = ||q||^2 + max ||g||^2 for L2 and,
-for cosine, scores -q.g/||g|| (q not normalised) with scale 1.  So:
+for cosine, scores -cos(q, g) (ef_search_common.hpp score64) with scale 1.  So:
 
 * every probe whose fp64 top-2 gap exceeds that window must get exactly the oracle's
   first-arg-best row (np.argmin / np.argmax semantics) — no fraction floor;
@@ -67,10 +67,9 @@ def window(q, g, metric, best, gmax2=None):
     if metric == "l2":
         scale = qn2 + (gmax2_of(g) if gmax2 is None else gmax2)
         return WINDOW * (np.abs(best) + scale)
-    # raw score -q.g/|g| = |q| * (unit score); raw window 1e-12 (|raw| + 1)
-    qn = np.sqrt(qn2)
-    with np.errstate(divide="ignore"):
-        return WINDOW * (np.abs(best) + np.where(qn > 0, 1.0 / qn, np.inf))
+    # cosine: resolve_kernel's fp64 score is -cos (score64: -q.g / (|q| |g|)), window
+    # 1e-12 (|score| + 1)
+    return WINDOW * (np.abs(best) + 1.0)
 
 
 def chosen_scores(q, g, idx, metric):

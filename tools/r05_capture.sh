@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-5 profile capture (after the kernels are final): the default bench line, its
+# kernel trace, and separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ) for every search
+# kernel a BENCH traffic figure cites — the C3 fp32 scan, the C5 bf16 screen, the C5 fp32
+# side leg and the C5 bf16 projection — summarised by tools/pmc_summary.py.
+# usage: bash tools/r05_capture.sh <tag> [part]   part: bench | c3 | c5 | c5fp32 | all (default)
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 9
+TAG=${1:-r05cap}
+PART=${2:-all}
+O=gpurun_out/$TAG
+mkdir -p $O
+step() {  # name, timeout, command...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >> $O/steps.log
+  timeout -k 10 $to "$@" > $O/$name.out 2> $O/$name.err
+  local rc=$?
+  echo "== $name rc=$rc" >> $O/steps.log
+  return $rc
+}
+pmc3() {  # tag, kernel regex, config, bench args...
+  local t=$1 R=$2 cfg=$3; shift 3
+  step ${t}_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${t}_trace -o run -- python "$@" || return $?
+  step ${t}_fetch 180 rocprofv3 --kernel-include-regex "$R" --pmc FETCH_SIZE --output-format csv -d $O/${t}_fetch -o run -- python "$@" || return $?
+  step ${t}_write 180 rocprofv3 --kernel-include-regex "$R" --pmc WRITE_SIZE --output-format csv -d $O/${t}_write -o run -- python "$@" || return $?
+  step ${t}_sq 180 rocprofv3 --kernel-include-regex "$R" --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $O/${t}_sq -o run -- python "$@" || return $?
+  python tools/pmc_summary.py $O/${t}_fetch/run_counter_collection.csv $O/${t}_write/run_counter_collection.csv \
+    $O/${t}_sq/run_counter_collection.csv $O/${t}_trace/run_kernel_stats.csv $O/pmc_summary_$cfg.json $cfg > $O/${t}_summary.txt
+}
+if [ "$PART" = all ] || [ "$PART" = bench ]; then
+  step bench 900 python bench.py || exit $?
+fi
+if [ "$PART" = all ] || [ "$PART" = c3 ]; then
+  pmc3 c3 "search_kernel<128, 0, false, false, 0>" c3 bench.py --steps 5 --warmup 2 --no-cpu --no-fit --no-c2 --no-c5 --no-image || exit $?
+fi
+if [ "$PART" = all ] || [ "$PART" = c5 ]; then
+  pmc3 c5hi "search_wide16" c5hi bench.py --config c5 --split-opt 3 --steps 3 --warmup 1 --no-cpu --no-fit --no-split --no-image || exit $?
+  pmc3 c5proj "project_bf16_wide" c5proj bench.py --config c5 --split-opt 3 --steps 3 --warmup 1 --no-cpu --no-fit --no-split --no-image || exit $?
+fi
+if [ "$PART" = all ] || [ "$PART" = c5fp32 ]; then
+  pmc3 c5 "search_wide_kernel<512" c5 bench.py --config c5 --search fp32 --steps 3 --warmup 1 --no-cpu --no-fit --no-split --no-image || exit $?
+fi
+echo done >> $O/steps.log
