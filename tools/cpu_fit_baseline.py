@@ -82,6 +82,9 @@ def main():
     ap.add_argument("--impl", nargs="+", default=["sklearn_randomized", "oracle_exact_cov"])
     ap.add_argument("--n-full", type=int, default=1_000_000)
     ap.add_argument("--eig-repeats", type=int, default=3)
+    ap.add_argument("--eigh-from", default=None, help="take the (n-independent) eigensolve timing from an earlier "
+                                                     "record of this tool instead of re-measuring it")
+    ap.add_argument("--merge", default=None, help="earlier record whose runs are merged into this one")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import threading
@@ -106,6 +109,10 @@ def main():
                                   "OPENBLAS/OMP_NUM_THREADS=16 (its rules: leave them); the affinity mask spans "
                                   "the whole host, so 16 threads is the job's share, not a pinning",
            "warmups": a.warmups, "repeats": a.repeats, "runs": {}}
+    if a.eigh_from:
+        res["eigh"] = dict(json.load(open(a.eigh_from))["eigh"], source=a.eigh_from)
+    if a.merge:
+        res["runs"].update(json.load(open(a.merge))["runs"])
     for n in a.n:
         X = faces(n)
         print(f"generated {n} faces", flush=True)
