@@ -22,7 +22,9 @@
 // k > 80 (BASELINE.json config 3: k = 128; config 5: k = 512) and for direct solves of
 // moderate orders.  Quadratic convergence: a nearly diagonal input (warm subspace) needs
 // 2-3 sweeps.
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "ef_linalg.hpp"
 
@@ -112,6 +114,9 @@ __global__ __launch_bounds__(256) void jbig_round_kernel(const double* __restric
 }
 
 // ------------------------------------------------------------------ block Jacobi
+#ifndef EF_BJ_EARLY  // 0: no early convergence test (A/B builds)
+#define EF_BJ_EARLY 1
+#endif
 constexpr int kBlockJacobiMin = 128;
 constexpr int BJ = 16;           // block width; a pair problem is 2 * BJ = 32
 constexpr int kInnerSweeps = 1;  // inner sweeps per pair problem (the outer sweeps revisit every pair)
@@ -198,8 +203,8 @@ __device__ __forceinline__ void bj_locate(int r, int nb, int blk, int* pair, int
 __device__ __forceinline__ void bj_solve_part(const double* __restrict__ Gprev, const double* Gcur,
                                               double* __restrict__ Gnext, int mp, int r, int rp,
                                               const double* __restrict__ Zprev, double* __restrict__ Zcur,
-                                              int* __restrict__ flag, const double* __restrict__ tolp, int pair,
-                                              Tile* sm) {
+                                              int* __restrict__ flag, const double* __restrict__ tolp,
+                                              unsigned long long* __restrict__ pmax, int pair, Tile* sm) {
   const int nb = mp / BJ;
   int I, J;
   bj_pair(r, pair, nb, &I, &J);
@@ -250,12 +255,21 @@ __device__ __forceinline__ void bj_solve_part(const double* __restrict__ Gprev, 
   // outer convergence: any off-diagonal entry above tol (1e-12, or the looser tolerance
   // of a coarse-phase Rayleigh-Ritz solve) of its diagonal scale
   const double tol = *tolp;
+  double rmax = 0.0;  // the sweep's largest off-diagonal ratio (JacobiBig::solve's early check)
   for (int e = tid; e < BS * BS; e += 256) {
     const int a = e >> 5, b = e & 31;
-    if (a != b && fabs(S[0][a][b]) > tol * sqrt(fabs(S[0][a][a] * S[0][b][b]))) any = 1;
+    const double x = fabs(S[0][a][b]), sc = sqrt(fabs(S[0][a][a] * S[0][b][b]));
+    if (a != b && x > tol * sc) any = 1;
+    if (a != b && x > 0.0) rmax = fmax(rmax, sc > 0.0 ? x / sc : __builtin_huge_val());
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, off));
+  if ((tid & 63) == 0 && rmax > 0.0) atomicMax(pmax, (unsigned long long)__double_as_longlong(rmax));
   __syncthreads();
-  if (any) *flag = 1;
+  if (any && tid == 0) {
+    *flag = 1;
+    pmax[1] = 1ull;  // the sweep's flag beside its ratio: one host read per sweep
+  }
   const int t = tid >> 4, u = tid & 15;
   int cur = 0;
   for (int sw = 0; sw < kInnerSweeps && any; ++sw) {
@@ -365,11 +379,12 @@ __global__ __launch_bounds__(256) void bj_round_kernel(const double* __restrict_
                                                        double* __restrict__ Gnext, double* __restrict__ V, int mp,
                                                        int r, int rp, int nsolve, const double* __restrict__ Zprev,
                                                        double* __restrict__ Zcur, int* __restrict__ flag,
-                                                       const double* __restrict__ tolp) {
+                                                       const double* __restrict__ tolp,
+                                                       unsigned long long* __restrict__ pmax) {
   __shared__ Tile sm[7];
   const int b = blockIdx.x;
   if (b < nsolve) {
-    bj_solve_part(Gprev, Gcur, Gnext, mp, r, rp, Zprev, Zcur, flag, tolp, b, sm);
+    bj_solve_part(Gprev, Gcur, Gnext, mp, r, rp, Zprev, Zcur, flag, tolp, pmax, b, sm);
     return;
   }
   const int npair = mp / BS, a = b - nsolve;
@@ -377,6 +392,20 @@ __global__ __launch_bounds__(256) void bj_round_kernel(const double* __restrict_
 }
 
 __global__ void set_scalar_kernel(double* p, double v) { *p = v; }
+
+// Early convergence test of the block method (JacobiBig::solve): *flag = 1 when any
+// off-diagonal entry of the completed matrix G exceeds tol of its diagonal scale — the
+// decision the next sweep's pair problems would take before rotating anything (they read
+// these same entries), without running that sweep.  grid: one block per row.
+__global__ void bj_check_kernel(const double* __restrict__ G, int m, int mp, const double* __restrict__ tolp,
+                                unsigned long long* __restrict__ flag) {
+  const int i = blockIdx.x;
+  const double tol = *tolp, gii = G[(int64_t)i * mp + i];
+  bool bad = false;
+  for (int j = threadIdx.x; j < m; j += blockDim.x)
+    if (j != i && fabs(G[(int64_t)i * mp + j]) > tol * sqrt(fabs(gii * G[(int64_t)j * mp + j]))) bad = true;
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1ull;
+}
 
 // G^(-1) = G^(0) = the symmetrised input in buffers 2 and 0, V = I, Z^(-1) = I: the first
 // round's pending apply is an exact identity
@@ -452,6 +481,7 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
     hipError_t e = hipStreamBeginCapture(capture, hipStreamCaptureModeRelaxed);
     if (e != hipSuccess) return e;
     (void)hipMemsetAsync(flag, 0, sizeof(int), capture);
+    if (block) (void)hipMemsetAsync(pmax_slot(), 0, 2 * sizeof(unsigned long long), capture);
     body();
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(capture, &g);
@@ -493,9 +523,9 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
         int cur = par;
         for (int r = 0; r < R; ++r) {
           hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair), dim3(256), 0, capture, G[cur], G[cur],
-                             G[cur ^ 1], V, mp, r, r, npair, nullptr, Z[0], flag, tolv);
+                             G[cur ^ 1], V, mp, r, r, npair, nullptr, Z[0], flag, tolv, pmax_slot());
           hipLaunchKernelGGL(bj_round_kernel, dim3(napply), dim3(256), 0, capture, G[cur], G[cur ^ 1], G[cur ^ 1],
-                             V, mp, r, r, 0, Z[0], Z[1], flag, tolv);
+                             V, mp, r, r, 0, Z[0], Z[1], flag, tolv, pmax_slot());
           cur ^= 1;
         }
       });
@@ -511,7 +541,7 @@ hipError_t JacobiBig::init(int m_, double* work_, int* flag_, hipStream_t captur
         const int g = ph + r;
         hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)npair + napply), dim3(256), 0, capture,
                            G[mod_pos(g - 1, 3)], G[g % 3], G[(g + 1) % 3], V, mp, r, r == 0 ? R - 1 : r - 1, npair,
-                           Z[mod_pos(g - 1, 2)], Z[g % 2], flag, tolv);
+                           Z[mod_pos(g - 1, 2)], Z[g % 2], flag, tolv, pmax_slot());
       }
     });
     if (e != hipSuccess) return e;
@@ -541,12 +571,46 @@ int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals,
     if (*err != hipSuccess) return -1;
     cur = three ? cur + R : cur ^ (R & 1);  // an odd number of rounds swaps the ping-pong buffers
     int hflag = 0;
-    *err = hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
+    unsigned long long hreg[2] = {0, 0};  // block path: {largest ratio (double bits), flag}
+    if (block) {
+      *err = hipMemcpyAsync(hreg, pmax_slot(), sizeof(hreg), hipMemcpyDeviceToHost, s);
+    } else {
+      *err = hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
+    }
     if (*err == hipSuccess) *err = hipStreamSynchronize(s);
     if (*err != hipSuccess) return -1;
+    if (block) hflag = hreg[1] != 0;
+    const unsigned long long hmax = hreg[0];
     if (hflag == 0) {
       converged = true;
       break;
+    }
+    // Early exit (round 5): Jacobi converges quadratically, so when the largest off-diagonal
+    // ratio this sweep rotated away was below sqrt(tol) / 4, the next sweep is very likely
+    // the confirming one that rotates nothing (~15 rounds of pair solves).  Complete G with
+    // the pending apply of the last round (G tiles only: idempotent, the next round would
+    // write the same values; V is left to the final apply), test every off-diagonal entry
+    // as that sweep's pair problems would, and stop when none exceeds tol.  When the test
+    // passes the result is bit-identical to running the confirming sweep (whose rotations
+    // are all the identity); when it fails the next sweep runs as before.
+    double dmax;
+    memcpy(&dmax, &hmax, sizeof dmax);
+    if (EF_BJ_EARLY && three && dmax > 0.0 && dmax < 0.25 * std::sqrt(tol)) {
+      const int npair = mp / BS, gl = cur - 1;
+      *err = hipMemsetAsync(pmax_slot() + 1, 0, sizeof(unsigned long long), s);
+      if (*err != hipSuccess) return -1;
+      hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)(npair * npair)), dim3(256), 0, s, G[gl % 3], G[cur % 3],
+                         G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag, tolv, pmax_slot());
+      hipLaunchKernelGGL(bj_check_kernel, dim3((unsigned)m), dim3(256), 0, s, G[cur % 3], m, mp, tolv,
+                         pmax_slot() + 1);
+      *err = hipMemcpyAsync(hreg, pmax_slot(), sizeof(hreg), hipMemcpyDeviceToHost, s);
+      if (*err == hipSuccess) *err = hipStreamSynchronize(s);
+      if (*err != hipSuccess) return -1;
+      if (hreg[1] == 0) {
+        converged = true;
+        ++sweep;  // the confirming sweep this test replaced
+        break;
+      }
     }
   }
   const double* Gfinal = G[cur];
@@ -554,7 +618,7 @@ int JacobiBig::solve(hipStream_t s, const double* A, int64_t lda, double* evals,
     // the last round's rotations still go to V (and to G's off-diagonal blocks)
     const int npair = mp / BS, gl = cur - 1;
     hipLaunchKernelGGL(bj_round_kernel, dim3((unsigned)(npair * (npair + mp / BS))), dim3(256), 0, s, G[gl % 3],
-                       G[cur % 3], G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag, tolv);
+                       G[cur % 3], G[cur % 3], V, mp, 0, R - 1, 0, Z[gl % 2], Z[cur % 2], flag, tolv, pmax_slot());
     Gfinal = G[cur % 3];
   }
   hipLaunchKernelGGL(jbig_sort_kernel, dim3((unsigned)m), dim3(256), 0, s, Gfinal, V, m, mp, evals, evecs, ldv);

@@ -140,6 +140,11 @@ struct JacobiBig {
   double* work = nullptr;
   int* flag = nullptr;
   void* exec[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // block path: the sweep's largest off-diagonal ratio (double bits, atomicMax), the slot
+  // after the tolerance scalar in work
+  unsigned long long* pmax_slot() const {
+    return reinterpret_cast<unsigned long long*>(work + 4 * (int64_t)mp * mp + 4 * 16 * (int64_t)mp + 1);
+  }
   hipError_t init(int m, double* work, int* flag, hipStream_t capture);
   // tol: a sweep in which no off-diagonal entry exceeds tol of its diagonal scale ends the
   // solve (block path; the scalar rounds always use 1e-12)
