@@ -365,6 +365,97 @@ def bf16_ceiling(loop, name="bf16_clock.json"):
     return None
 
 
+FIT_CHUNK = 32768
+
+
+def c3_fit_rows(lo, hi, dev, side=128, r=256):
+    """Rows [lo, hi) of the C3 fit workload (SURVEY.md §8d generator: mean face +
+    256-component spectrum + N(0, 2^2) pixel noise, uint8), generated on the GPU in chunks
+    of FIT_CHUNK rows, each from its own seed — any rank regenerates exactly the rows of its
+    shard, so the sample-sharded fit (fit_bench_sharded) sees the single-GPU fit's data."""
+    import torch
+    from eigenface import synth
+    d = side * side
+    B = torch.from_numpy(synth.basis(d, r, 5)).to(dev, torch.float32)
+    sp = torch.from_numpy(synth.spectrum(r)).to(dev, torch.float32)
+    mu = torch.from_numpy(synth.mean_face(side)).to(dev, torch.float32)
+    X = torch.empty((hi - lo, d), dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev)
+    for c in range(lo // FIT_CHUNK, (hi + FIT_CHUNK - 1) // FIT_CHUNK):
+        a, e = c * FIT_CHUNK, (c + 1) * FIT_CHUNK
+        g.manual_seed(77_000 + c)
+        z = torch.randn((FIT_CHUNK, r), generator=g, device=dev) * sp
+        pix = mu + z @ B.T + 2.0 * torch.randn((FIT_CHUNK, d), generator=g, device=dev)
+        a0, e0 = max(a, lo), min(e, hi)
+        X[a0 - lo:e0 - lo] = pix[a0 - a:e0 - a].round_().clamp_(0, 255).to(torch.uint8)
+        del z, pix
+    torch.cuda.synchronize(dev)
+    return X
+
+
+def _sha(t):
+    import hashlib
+    a = t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def fit_bench_sharded(eng, rank, world, backend, dev, n=1_000_000, side=128, k=128, repeats=3):
+    """BASELINE.json configs[3] for the fit (the fit collective): the C3
+    fit workload split by samples over the ranks (rank r holds rows [n r / G, n (r + 1) / G),
+    c3_fit_rows); each rank's exact integer pieces (int8 SYRK of its rows), one
+    all-reduce(sum) of the pieces (RCCL int64 over xGMI; the d x d piece is 2 GiB), then the
+    covariance-path fit from the sums on every rank (distributed.sharded_fit).  Timed like
+    the search: barrier + synchronize around each fit, the max over ranks, median of
+    `repeats` after a cold fit.  The eigenvalues' hash equals fit.c3's at N = 1 (the same
+    integers give the same covariance); for n <= 100k rank 0 also runs the single-GPU fit on
+    all rows and checks bit identity."""
+    import torch
+    import torch.distributed as dist
+    from eigenface.distributed import shard_range, sharded_fit
+    d = side * side
+    lo, hi = shard_range(n, rank, world)
+    X = c3_fit_rows(lo, hi, dev, side)
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return out, float(el.item())
+
+    _, t_cold = timed(lambda: sharded_fit(eng, X, k, standardize=True, projection=False))
+    fits = []
+    for _ in range(repeats):
+        res, el = timed(lambda: sharded_fit(eng, X, k, standardize=True, projection=False))
+        fits.append(el)
+    _, t_tr = timed(lambda: sharded_fit(eng, X, k, standardize=True, projection=True))
+    out = {"config": f"C4 fit: the C3 fit workload ({n} synthetic {side}x{side} uint8 faces, k={k}, "
+                     f"StandardScaler+PCA) sample-sharded over {world} ranks ({hi - lo} rows on rank {rank}), "
+                     f"exact integer pieces + all-reduce(sum) ({'RCCL' if backend == 'nccl' else 'gloo'}) + "
+                     "covariance-path fit on every rank",
+           "gpu_fit_s": round(float(np.median(fits)), 4), "gpu_fit_s_repeats": [round(x, 4) for x in fits],
+           "gpu_fit_transform_s": round(t_tr, 4), "gpu_fit_cold_s": round(t_cold, 4),
+           "protocol": f"max over ranks per fit, median of {repeats} after a cold fit",
+           "eigensolver_iters": res.iters,
+           "explained_variance_top3": [float(v) for v in res.eigenvalues[:3].cpu().numpy()],
+           "eigenvalues_sha1": _sha(res.eigenvalues), "components_sha1": _sha(res.components)}
+    if n <= 100_000 and rank == 0:
+        Xa = c3_fit_rows(0, n, dev, side)
+        ref = eng.fit(Xa, k, standardize=True, projection=False)
+        out["identical_to_single_gpu_fit"] = bool(torch.equal(ref.eigenvalues, res.eigenvalues)
+                                                  and torch.equal(ref.components, res.components)
+                                                  and torch.equal(ref.mean, res.mean))
+        del Xa
+    del X
+    torch.cuda.empty_cache()
+    return out
+
+
 def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu=10_000, repeats=5):
     """Headline secondary metric "covariance+SVD fit sec" on config 3's shape: train-v4.py's
     train_pca_model semantics (StandardScaler + PCA, k=128) on 1M synthetic 128x128 uint8
@@ -378,22 +469,9 @@ def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu
     oracle's exact covariance path, same protocol, same box type), which takes ~15 min and
     so is not rerun inside the bench."""
     import torch
-    from eigenface import synth
     d = side * side
     dev = torch.device("cuda", torch.cuda.current_device())
-    B = torch.from_numpy(synth.basis(d, r, 5)).to(dev, torch.float32)
-    sp = torch.from_numpy(synth.spectrum(r)).to(dev, torch.float32)
-    mu = torch.from_numpy(synth.mean_face(side)).to(dev, torch.float32)
-    X = torch.empty((n, d), dtype=torch.uint8, device=dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(77)
-    for a in range(0, n, 32768):
-        e = min(n, a + 32768)
-        z = torch.randn((e - a, r), generator=g, device=dev) * sp
-        pix = mu + z @ B.T + 2.0 * torch.randn((e - a, d), generator=g, device=dev)
-        X[a:e] = pix.round_().clamp_(0, 255).to(torch.uint8)
-        del z, pix
-    torch.cuda.synchronize(dev)
+    X = c3_fit_rows(0, n, dev, side, r)
     # first call: code paths + the context's fit workspaces (~30 GB at this shape, kept
     # for later fits, ef_trim frees them) — reported as the cold time
     t = time.perf_counter()
@@ -429,6 +507,7 @@ def fit_bench_c3(eng, with_cpu: bool, n=1_000_000, side=128, k=128, r=256, n_cpu
         "gpu_fit_transform_cold_s": round(t_cold, 4),
         "eigensolver_iters": r1.iters,
         "explained_variance_top3": [float(v) for v in ev[:3]],
+        "eigenvalues_sha1": _sha(r1.eigenvalues), "components_sha1": _sha(r1.components),
         "repeat_identical": bool(torch.equal(r1.components, r2.components)),
     }
     # fit roofline: the int8 SYRK (syrk_i8_kernel) is the fit's dominant kernel.  Algorithmic
@@ -837,6 +916,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary fit timing")
+    ap.add_argument("--fit-n", type=int, default=1_000_000, help="faces in the C3 / C4 fit workload")
+    ap.add_argument("--fit-side", type=int, default=128, help="face side of the fit workload (tests: smaller)")
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 recognition line")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 sub-record of the default run")
     ap.add_argument("--no-image", action="store_true", help="skip the ingest / template-localiser timing")
@@ -1017,6 +1098,11 @@ def main():
                      "search_avg_ms": s2_ms / max(s2_n, 1), "launches": s2_n,
                      "keys_identical": bool(torch.equal(keys2, keys))}
 
+    fit_sharded = None
+    if world > 1 and not args.no_fit:  # every rank: the sample-sharded fit is collective
+        eng.set_stream(stream.cuda_stream)
+        fit_sharded = fit_bench_sharded(eng, rank, world, args.backend, dev, n=args.fit_n, side=args.fit_side)
+
     tol = None
     if world == 1 and precision == "bf16":
         # the bf16 projection's tolerance vs fp32 — max relative feature
@@ -1113,7 +1199,10 @@ def main():
             rec["c5"] = c5_bench(eng, dev, not args.no_cpu, args.steps, args.warmup, args.repeats,
                                  min(args.cpu_budget, 8.0), args.c5_opt)
         if world == 1 and not args.no_fit:
-            rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu), "c2": fit_bench(eng, not args.no_cpu)}
+            rec["fit"] = {"c3": fit_bench_c3(eng, not args.no_cpu, n=args.fit_n, side=args.fit_side),
+                          "c2": fit_bench(eng, not args.no_cpu)}
+        if fit_sharded is not None:
+            rec["fit"] = {"c4": fit_sharded}
         if world == 1 and not args.no_image:
             eng.use_own_stream()
             eng.timing(True)

@@ -902,4 +902,47 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
   return hipGetLastError();
 }
 
+hipError_t launch_cov_i8_cross(hipStream_t s, const CovPlan& p, int64_t d, const uint8_t* At, int* slabs,
+                               long long* S64, void* order_dev) {
+  const std::vector<int2> order = syrk_tiles(d, p.tj);
+  if ((int)order.size() != p.ntiles) return hipErrorInvalidValue;
+  hipError_t e = hipMemcpyAsync(order_dev, order.data(), order.size() * sizeof(int2), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(S64, 0, (size_t)d * d * sizeof(long long), s);
+  if (e != hipSuccess) return e;
+  const int nitems = p.ntiles * p.splits;
+  const int grid = (nitems + 7) / 8 * 8;
+  const int nfb = (int)((d + FB - 1) / FB);
+  for (int pass = 0; pass < p.passes; ++pass) {
+    const int64_t st0 = (int64_t)pass * p.stages_per_pass;
+    const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
+    if (p.njb == 6)
+      hipLaunchKernelGGL((syrk16_i8_kernel<6, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, d, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+#ifdef EF_DIAGNOSTICS
+    else if (p.njb == 5)
+      hipLaunchKernelGGL((syrk16_i8_kernel<5, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, d, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+#endif
+    else if (p.tj == 384)
+      hipLaunchKernelGGL((syrk_i8_kernel<384, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, d, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+    else
+      hipLaunchKernelGGL((syrk_i8_kernel<256, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, d, st0, st1, p.kps,
+                         p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+    hipLaunchKernelGGL(slab_accumulate_kernel, dim3((unsigned)nfb, (unsigned)nfb), dim3(256), 0, s, slabs, p.splits,
+                       d, S64);
+  }
+  return hipStreamSynchronize(s);  // the host list must outlive the copy
+}
+
+hipError_t launch_cov_from_cross(hipStream_t s, const long long* S64, const unsigned long long* S1, int64_t n,
+                                 int64_t d, const double* w, long long* cvec, double* C) {
+  const int nfb = (int)((d + FB - 1) / FB);
+  hipLaunchKernelGGL(shifted_sums_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, n, d, cvec);
+  hipLaunchKernelGGL(d % 4 == 0 ? cov_finalize4_kernel : cov_finalize_kernel, dim3((unsigned)nfb, (unsigned)nfb),
+                     dim3(256), 0, s, nullptr, 0, S64, d, n, 0, cvec, nullptr, nullptr, w, C);
+  return hipGetLastError();
+}
+
 }  // namespace ef

@@ -726,6 +726,183 @@ extern "C" int ef_fit(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, int32_t
                    k_out, iters_out);
 }
 
+// ---------------------------------------------------------------- sample-sharded fit
+// SURVEY.md §8(e), the fit collective: rank r holds rows X_r; the exact integer pieces
+// (column sums of x and x^2, X'_r^T X'_r) of every rank add up to the pieces of the whole
+// set, so after a sum over ranks the covariance, and everything computed from it, equals
+// ef_fit's on the concatenated rows bit for bit (covariance path: n_total >= d).
+extern "C" int ef_fit_shard_stats(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, uint64_t* sum_out,
+                                  uint64_t* sumsq_out, int64_t* cross_out, uint32_t flags) {
+  if (!c) return EF_E_INVALID;
+  if ((!X && n > 0) || n < 0 || d < 1 || !sum_out || !sumsq_out || !cross_out)
+    return set_err(c, EF_E_INVALID, "ef_fit_shard_stats: bad arguments (need X, n >= 0, d >= 1, outputs)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->stream;
+  const bool dev = flags & EF_MEM_DEVICE;
+  Bufs B;
+  unsigned long long *S1, *S2;
+  long long* S64;
+  EF_TRY(B.get(c, (size_t)d, &S1));
+  EF_TRY(B.get(c, (size_t)d, &S2));
+  if (dev) {
+    S64 = reinterpret_cast<long long*>(cross_out);
+  } else {
+    EF_TRY(B.get(c, (size_t)d * d, &S64));
+  }
+  EF_HIP(c, hipMemsetAsync(S1, 0, d * sizeof(unsigned long long), s), "memset");
+  EF_HIP(c, hipMemsetAsync(S2, 0, d * sizeof(unsigned long long), s), "memset");
+  if (n == 0) {  // an empty shard contributes nothing
+    EF_HIP(c, hipMemsetAsync(S64, 0, (size_t)d * d * sizeof(long long), s), "memset");
+  } else {
+    const uint8_t* Xd = X;
+    if (!dev) {
+      uint8_t* xb;
+      EF_TRY(B.get(c, (size_t)n * d, &xb));
+      EF_HIP(c, hipMemcpyAsync(xb, X, (size_t)n * d, hipMemcpyHostToDevice, s), "H2D X");
+      Xd = xb;
+    }
+    uint8_t* At;
+    EF_TRY(B.get(c, (size_t)d * cov_i8_kpad(n) + kSyrkPadBytes, &At));
+    const bool fused = cov_i8_fused_stats(Xd, d);
+    EF_HIP(c, launch_cov_i8_prep(s, Xd, n, d, false, At, fused ? S1 : nullptr, fused ? S2 : nullptr), "cov prep");
+    if (!fused) EF_HIP(c, launch_colstats(s, Xd, n, d, S1, S2), "colstats");
+    const CovPlan plan = cov_i8_plan(d, n, c->opt_cov_slab_bytes);
+    int* slabs;
+    uint8_t* order;
+    EF_TRY(B.get(c, (size_t)plan.slab_elems, &slabs));
+    EF_TRY(B.get(c, (size_t)cov_i8_order_bytes(d), &order));
+    EF_HIP(c, launch_cov_i8_cross(s, plan, d, At, slabs, S64, order), "X'^T X' (int8)");
+  }
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  EF_HIP(c, hipMemcpyAsync(sum_out, S1, d * sizeof(uint64_t), kind, s), "out sum");
+  EF_HIP(c, hipMemcpyAsync(sumsq_out, S2, d * sizeof(uint64_t), kind, s), "out sumsq");
+  if (!dev) EF_HIP(c, hipMemcpyAsync(cross_out, S64, (size_t)d * d * sizeof(int64_t), kind, s), "out cross");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  return EF_OK;
+}
+
+extern "C" int ef_fit_from_stats(ef_ctx* c, const uint64_t* sum, const uint64_t* sumsq, const int64_t* cross,
+                                 int64_t n_total, int64_t d, int32_t k, uint32_t flags, double* mean_out,
+                                 double* var_out, double* scale_out, double* comps_out, double* eig_out, double* tv_out,
+                                 int32_t* k_out, int32_t* iters_out) {
+  if (!c) return EF_E_INVALID;
+  if (!sum || !sumsq || !cross || d < 1 || k < 1 || !mean_out || !comps_out || !eig_out)
+    return set_err(c, EF_E_INVALID, "ef_fit_from_stats: bad arguments (need the pieces, d >= 1, k >= 1, outputs)");
+  if (n_total < 2 || n_total < d)
+    return set_err(c, EF_E_INVALID, "ef_fit_from_stats: the sample-sharded fit is the covariance path (n_total >= d, "
+                                    "n_total >= 2)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->stream;
+  const bool dev = flags & EF_MEM_DEVICE;
+  const bool stdz = flags & EF_FIT_STANDARDIZE;
+  const int kk = (int)(k < d ? k : d);
+  Bufs B;
+  const unsigned long long *S1 = reinterpret_cast<const unsigned long long*>(sum),
+                           *S2 = reinterpret_cast<const unsigned long long*>(sumsq);
+  const long long* S64 = reinterpret_cast<const long long*>(cross);
+  if (!dev) {  // stage the host pieces
+    unsigned long long *h1, *h2;
+    long long* h3;
+    EF_TRY(B.get(c, (size_t)d, &h1));
+    EF_TRY(B.get(c, (size_t)d, &h2));
+    EF_TRY(B.get(c, (size_t)d * d, &h3));
+    EF_HIP(c, hipMemcpyAsync(h1, sum, d * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D sum");
+    EF_HIP(c, hipMemcpyAsync(h2, sumsq, d * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D sumsq");
+    EF_HIP(c, hipMemcpyAsync(h3, cross, (size_t)d * d * sizeof(int64_t), hipMemcpyHostToDevice, s), "H2D cross");
+    S1 = h1, S2 = h2, S64 = h3;
+  }
+  double *mean, *var, *scale, *w, *C, *work, *U, *lam, *comps, *En, *tv;
+  long long* cvec;
+  EF_TRY(B.get(c, (size_t)d, &mean));
+  EF_TRY(B.get(c, (size_t)d, &var));
+  EF_TRY(B.get(c, (size_t)d, &scale));
+  EF_TRY(B.get(c, (size_t)d, &w));
+  EF_TRY(B.get(c, (size_t)d * d, &C));
+  EF_TRY(B.get(c, kWorkElems, &work));
+  EF_TRY(B.get(c, (size_t)d * kk, &U));
+  EF_TRY(B.get(c, (size_t)kk, &lam));
+  EF_TRY(B.get(c, (size_t)kk * d, &comps));
+  EF_TRY(B.get(c, (size_t)d * kk, &En));
+  EF_TRY(B.get(c, 1, &tv));
+  EF_TRY(B.get(c, (size_t)d, &cvec));
+  EF_HIP(c, launch_stats_finalize(s, S1, S2, n_total, d, stdz ? 1 : 0, mean, var, scale, w), "stats");
+  EF_HIP(c, launch_cov_from_cross(s, S64, S1, n_total, d, stdz ? w : nullptr, cvec, C), "covariance (from pieces)");
+  EF_HIP(c, launch_trace(s, C, d, d, tv), "trace");
+  int iters = 0;
+  EF_TRY(eig_topk(c, B, C, d, kk, work, U, lam, &iters));
+  EF_HIP(c, launch_normalize_sign(s, U, d, kk, kk, comps, En), "normalize");
+  EF_TRY(complete_null_components(c, n_total, d, kk, lam, comps, En));
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  EF_HIP(c, hipMemcpyAsync(mean_out, mean, d * sizeof(double), kind, s), "out mean");
+  if (var_out) EF_HIP(c, hipMemcpyAsync(var_out, var, d * sizeof(double), kind, s), "out var");
+  if (scale_out) EF_HIP(c, hipMemcpyAsync(scale_out, scale, d * sizeof(double), kind, s), "out scale");
+  EF_HIP(c, hipMemcpyAsync(comps_out, comps, (size_t)kk * d * sizeof(double), kind, s), "out comps");
+  EF_HIP(c, hipMemcpyAsync(eig_out, lam, kk * sizeof(double), kind, s), "out eig");
+  if (tv_out) EF_HIP(c, hipMemcpyAsync(tv_out, tv, sizeof(double), kind, s), "out tv");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  if (k_out) *k_out = kk;
+  if (iters_out) *iters_out = iters;
+  return EF_OK;
+}
+
+namespace {
+__global__ void recip_kernel(const double* __restrict__ a, int64_t n, double* __restrict__ b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = 1.0 / a[i];  // the division stats_finalize_kernel makes for w
+}
+}  // namespace
+
+extern "C" int ef_fit_transform(ef_ctx* c, const uint8_t* X, int64_t n, int64_t d, const double* mean,
+                                const double* scale, const double* comps, int32_t k, uint32_t flags, double* proj_out) {
+  if (!c) return EF_E_INVALID;
+  if (!X || n < 1 || d < 1 || k < 1 || !mean || !comps || !proj_out)
+    return set_err(c, EF_E_INVALID, "ef_fit_transform: bad arguments (need X, n >= 1, d >= 1, k >= 1, model, out)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->stream;
+  const bool dev = flags & EF_MEM_DEVICE;
+  Bufs B;
+  const uint8_t* Xd = X;
+  const double *mu = mean, *sc = scale, *cp = comps;
+  if (!dev) {
+    uint8_t* xb;
+    double *m1, *s1 = nullptr, *c1;
+    EF_TRY(B.get(c, (size_t)n * d, &xb));
+    EF_TRY(B.get(c, (size_t)d, &m1));
+    EF_TRY(B.get(c, (size_t)k * d, &c1));
+    EF_HIP(c, hipMemcpyAsync(xb, X, (size_t)n * d, hipMemcpyHostToDevice, s), "H2D X");
+    EF_HIP(c, hipMemcpyAsync(m1, mean, d * sizeof(double), hipMemcpyHostToDevice, s), "H2D mean");
+    EF_HIP(c, hipMemcpyAsync(c1, comps, (size_t)k * d * sizeof(double), hipMemcpyHostToDevice, s), "H2D comps");
+    if (scale) {
+      EF_TRY(B.get(c, (size_t)d, &s1));
+      EF_HIP(c, hipMemcpyAsync(s1, scale, d * sizeof(double), hipMemcpyHostToDevice, s), "H2D scale");
+    }
+    Xd = xb, mu = m1, sc = s1, cp = c1;
+  }
+  double *w = nullptr, *En, *proj, *work;
+  if (sc) {
+    EF_TRY(B.get(c, (size_t)d, &w));
+    hipLaunchKernelGGL(recip_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, sc, d, w);
+  }
+  EF_TRY(B.get(c, (size_t)d * k, &En));
+  EF_TRY(B.get(c, (size_t)n * k, &proj));
+  EF_TRY(B.get(c, kWorkElems, &work));
+  EF_HIP(c, launch_transpose_f64(s, cp, d, k, d, En, k), "E = comps^T");
+  if (proj_i8_supported(Xd, n, d, k)) {
+    uint8_t* pw;
+    EF_TRY(B.get(c, proj_i8_work_bytes(n, d, k), &pw));
+    EF_HIP(c, launch_proj_i8(s, Xd, n, d, mu, w, En, k, pw, proj), "F = A.E (int8 digits)");
+  } else {
+    EF_HIP(c, gemm64(s, Operand::pixels(Xd, EF_U8, d, false, mu, w), Operand::dense(En, k, false), n, k, d, 1.0, proj,
+                     k, work, kWorkElems),
+           "F = A.E");
+  }
+  EF_HIP(c, hipMemcpyAsync(proj_out, proj, (size_t)n * k * sizeof(double),
+                           dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s),
+         "out proj");
+  EF_HIP(c, hipStreamSynchronize(s), "sync");
+  return EF_OK;
+}
+
 // Column statistics alone (ManualStandardScaler.fit, scripts/manual/train-v2.py:58-64, and
 // StandardScaler.fit): exact integer sums for uint8, two-pass fp64 for float input.
 extern "C" int ef_colstats(ef_ctx* c, const void* Xv, int32_t x_dtype, int64_t n, int64_t d, uint32_t flags,

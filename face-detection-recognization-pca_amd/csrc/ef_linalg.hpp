@@ -178,6 +178,14 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
                          const unsigned long long* S1, const double* w, const uint8_t* At, int* slabs,
                          long long* S64, long long* cvec, long long* R, unsigned long long* Q2, void* order_dev,
                          double* C, hipEvent_t syrk_begin = nullptr, hipEvent_t syrk_end = nullptr);
+// Sample-sharded covariance (ef_fit_shard_stats / ef_fit_from_stats): S64 (int64, d x d;
+// the upper 64-blocks exact) = X'^T X' of the rows in At (covariance-path layout, K = n),
+// every pass's int32 slabs accumulated; then C from globally summed pieces (S64, S1, n) with
+// the finalize arithmetic of launch_cov_i8 — the same integer gives the same double.
+hipError_t launch_cov_i8_cross(hipStream_t s, const CovPlan& p, int64_t d, const uint8_t* At, int* slabs,
+                               long long* S64, void* order_dev);
+hipError_t launch_cov_from_cross(hipStream_t s, const long long* S64, const unsigned long long* S1, int64_t n,
+                                 int64_t d, const double* w, long long* cvec, double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
 // Li = L^-1 (row-major, zeros above the diagonal) for G = L L^T in one register-resident
 // workgroup (m <= 256, m even: chol_inv_supported); G is not modified; *info as

@@ -270,3 +270,59 @@ class ShardedGallery:
             one()
         torch.cuda.synchronize(device)
         return (time.perf_counter() - t) / reps * 1e3
+
+
+# ------------------------------------------------------------------ sharded fit
+def allreduce_fit_stats(pieces, group=None):
+    """Sum the exact integer fit pieces (sum x, sum x^2, X'^T X'; int64) over the ranks of
+    ``group`` in place: an integer sum, so the result is exact in any order.  RCCL takes
+    device tensors directly; gloo reduces host copies."""
+    import torch
+    import torch.distributed as dist
+
+    gloo = dist.get_backend(group) == "gloo"
+    out = []
+    for t in pieces:
+        if not isinstance(t, torch.Tensor):
+            t = torch.from_numpy(np.ascontiguousarray(t, dtype=np.int64))
+        if gloo and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=group)
+        out.append(t)
+    return out
+
+
+def sharded_fit(engine, X_local, n_components: int, standardize: bool = False, group=None, projection: bool = True,
+                stats_fn=None, fit_fn=None, transform_fn=None):
+    """The sample-sharded fit of SURVEY.md §8(e) (the fit collective): every rank holds the
+    uint8 rows X_local of its shard; each computes the exact integer pieces of its rows
+    (``Engine.fit_shard_stats``: sum x, sum x^2 and X'^T X' with X' = X - 128), one
+    all-reduce(sum) per piece adds them up (the d x d piece is 2 GiB at d = 16384:
+    bandwidth-bound over xGMI, beside a SYRK of n_total / world rows), and every rank runs
+    the covariance-path fit from the sums (``Engine.fit_from_stats``) — bit-identical to
+    ``Engine.fit`` on the concatenated rows, because the same integers give the same
+    covariance — then projects its own rows (``Engine.fit_transform_rows``).  Returns the
+    FitResult with ``projection`` = this rank's rows.  The ``*_fn`` hooks replace the
+    engine calls (CPU tests)."""
+    import torch
+    import torch.distributed as dist
+
+    stats_fn = stats_fn or engine.fit_shard_stats
+    fit_fn = fit_fn or engine.fit_from_stats
+    transform_fn = transform_fn or engine.fit_transform_rows
+    n_local = int(X_local.shape[0])
+    n = torch.tensor([n_local], dtype=torch.int64)
+    if dist.get_backend(group) != "gloo":
+        n = n.to(X_local.device if isinstance(X_local, torch.Tensor) and X_local.is_cuda else "cuda")
+    dist.all_reduce(n, group=group)
+    n_total = int(n.item())
+    pieces = allreduce_fit_stats(stats_fn(X_local), group)
+    if not isinstance(X_local, torch.Tensor) or not X_local.is_cuda:
+        pieces = [p.cpu().numpy() if isinstance(p, torch.Tensor) else p for p in pieces]
+    res = fit_fn(*pieces, n_total, n_components, standardize)
+    if projection and n_local > 0:
+        res.projection = transform_fn(X_local, res, standardize)
+    return res

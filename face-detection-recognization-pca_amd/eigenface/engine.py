@@ -301,6 +301,104 @@ class Engine:
         self._chk(self._lib.ef_colstats(self._h, xp, xdt, n, d, 0, mean.ctypes.data, var.ctypes.data))
         return mean, var
 
+    # --------------------------------------------------------- sample-sharded fit
+    def fit_shard_stats(self, X):
+        """ef_fit_shard_stats: the exact integer pieces of this rank's uint8 rows X (n x d) —
+        (sum x [d], sum x^2 [d], X'^T X' [d, d] with X' = X - 128, upper 64-blocks exact) as
+        int64 arrays: torch tensors on X's device for a device X, numpy otherwise.  Summed
+        over ranks they are the pieces of the whole set (distributed.sharded_fit)."""
+        x, xp, xdt, dev = self._fit_input(X)
+        if xdt != N.EF_U8 or x.ndim != 2:
+            raise TypeError("fit_shard_stats takes 2-D uint8 pixels")
+        n, d = (int(v) for v in x.shape)
+        if dev:
+            import torch
+            s1 = torch.empty(d, dtype=torch.int64, device=x.device)
+            s2 = torch.empty(d, dtype=torch.int64, device=x.device)
+            cr = torch.empty((d, d), dtype=torch.int64, device=x.device)
+            with self._torch_order(x, s1, s2, cr):
+                self._chk(self._lib.ef_fit_shard_stats(self._h, xp, n, d, s1.data_ptr(), s2.data_ptr(),
+                                                       cr.data_ptr(), N.EF_MEM_DEVICE))
+            return s1, s2, cr
+        s1, s2 = np.empty(d, np.int64), np.empty(d, np.int64)
+        cr = np.empty((d, d), np.int64)
+        self._chk(self._lib.ef_fit_shard_stats(self._h, xp, n, d, s1.ctypes.data, s2.ctypes.data, cr.ctypes.data, 0))
+        return s1, s2, cr
+
+    def fit_from_stats(self, sums, sumsqs, cross, n_total: int, n_components: int, standardize: bool = False) -> FitResult:
+        """ef_fit_from_stats: the fit (covariance path, n_total >= d) from the pieces of
+        fit_shard_stats summed over every rank — equal to fit() on the concatenated rows bit
+        for bit (projection None: see fit_transform_rows).  Device pieces give device
+        (float64 torch) outputs."""
+        if _is_dev(sums):
+            import torch
+            s1, p1 = _dev(sums, torch.int64)
+            s2, p2 = _dev(sumsqs, torch.int64)
+            cr, p3 = _dev(cross, torch.int64)
+            d = int(s1.shape[0])
+            kk = min(int(n_components), d)
+
+            def alloc(*shape):
+                return torch.empty(shape, dtype=torch.float64, device=s1.device)
+
+            def ptr(a):
+                return a.data_ptr()
+            flags = N.EF_MEM_DEVICE
+        else:
+            s1, p1 = _host(np.asarray(sums), np.int64)
+            s2, p2 = _host(np.asarray(sumsqs), np.int64)
+            cr, p3 = _host(np.asarray(cross), np.int64)
+            d = int(s1.shape[0])
+            kk = min(int(n_components), d)
+
+            def alloc(*shape):
+                return np.empty(shape)
+
+            def ptr(a):
+                return a.ctypes.data
+            flags = 0
+        if tuple(cr.shape) != (d, d) or tuple(s2.shape) != (d,):
+            raise ValueError(f"pieces must be sum[{d}], sumsq[{d}], cross[{d}, {d}]")
+        mean, var, scale = alloc(d), alloc(d), alloc(d)
+        comps, eig, tv = alloc(kk, d), alloc(kk), alloc(1)
+        k_out, it = C.c_int32(0), C.c_int32(0)
+        flags |= N.EF_FIT_STANDARDIZE if standardize else 0
+        ctx = self._torch_order(s1, s2, cr, mean, var, scale, comps, eig, tv) if flags & N.EF_MEM_DEVICE \
+            else contextlib.nullcontext()
+        with ctx:
+            self._chk(self._lib.ef_fit_from_stats(self._h, p1, p2, p3, int(n_total), d, int(n_components), flags,
+                                                  ptr(mean), ptr(var), ptr(scale), ptr(comps), ptr(eig), ptr(tv),
+                                                  C.byref(k_out), C.byref(it)))
+        if flags & N.EF_MEM_DEVICE:
+            self.synchronize()
+        return FitResult(mean, var, scale, comps, eig, None, float(tv[0]), int(k_out.value), int(it.value))
+
+    def fit_transform_rows(self, X, result: FitResult, standardize: bool = False):
+        """ef_fit_transform: the training projection of uint8 rows X with a fitted model —
+        the rows fit()'s projection holds for them (the sample-sharded fit projects each
+        rank's own rows)."""
+        x, xp, xdt, dev = self._fit_input(X)
+        if xdt != N.EF_U8 or x.ndim != 2:
+            raise TypeError("fit_transform_rows takes 2-D uint8 pixels")
+        n, d = (int(v) for v in x.shape)
+        k = int(result.k)
+        if dev:
+            import torch
+            mean, pm = _dev(result.mean, torch.float64)
+            comps, pc = _dev(result.components, torch.float64)
+            sc, ps = _dev(result.scale, torch.float64) if standardize else (None, None)
+            out = torch.empty((n, k), dtype=torch.float64, device=x.device)
+            with self._torch_order(x, mean, comps, sc, out):
+                self._chk(self._lib.ef_fit_transform(self._h, xp, n, d, pm, ps, pc, k, N.EF_MEM_DEVICE,
+                                                     out.data_ptr()))
+            return out
+        mean, pm = _host(np.asarray(result.mean), np.float64)
+        comps, pc = _host(np.asarray(result.components), np.float64)
+        sc, ps = _host(np.asarray(result.scale), np.float64) if standardize else (None, None)
+        out = np.empty((n, k))
+        self._chk(self._lib.ef_fit_transform(self._h, xp, n, d, pm, ps, pc, k, 0, out.ctypes.data))
+        return out
+
     # ----------------------------------------------------------------- projection
     def set_model(self, mean, W, precision="fp32", owner=None):
         """Resident recognition model f = (p - mean) . W, W is d x k (k <= 512).

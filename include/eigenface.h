@@ -131,6 +131,31 @@ int ef_fit_ex(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d,
 int ef_colstats(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d, uint32_t flags,
                 double* mean_out, double* var_out);
 
+/* ---------------------------------------------------- sample-sharded fit (API v6)
+ * The fit collective of SURVEY §8(e): rank r holds uint8 rows X_r (n_r x d) on its GPU.
+ * ef_fit_shard_stats: the exact integer pieces of the local rows —
+ *   sum_out[d] = sum x, sumsq_out[d] = sum x^2 (uint64) per pixel,
+ *   cross_out[d*d] (int64) = X'_r^T X'_r with X' = X - 128 (the upper 64 x 64 blocks exact,
+ *   the rest of the matrix unspecified);
+ * the caller sums the three arrays over ranks (an all-reduce, integer sum — e.g. RCCL
+ * int64 over xGMI), then every rank calls
+ * ef_fit_from_stats with the sums and n_total = sum n_r: mean / var / scale / components /
+ *   eigenvalues / total variance exactly as ef_fit computes them on the concatenated rows
+ *   (the same integers give the same covariance, bit for bit), covariance path only
+ *   (n_total >= d; EF_FIT_STANDARDIZE as in ef_fit);
+ * ef_fit_transform: the training projection (projected_data / fit_transform output) of
+ *   local rows with a fitted model (mean[d], scale[d] or NULL = no StandardScaler,
+ *   comps[k*d]) — the rows ef_fit's proj_out would hold for them.
+ * Host pointers unless EF_MEM_DEVICE (then every array argument is a device pointer). */
+int ef_fit_shard_stats(ef_ctx* ctx, const uint8_t* X, int64_t n, int64_t d, uint64_t* sum_out, uint64_t* sumsq_out,
+                       int64_t* cross_out, uint32_t flags);
+int ef_fit_from_stats(ef_ctx* ctx, const uint64_t* sum, const uint64_t* sumsq, const int64_t* cross, int64_t n_total,
+                      int64_t d, int32_t k, uint32_t flags, double* mean_out, double* var_out, double* scale_out,
+                      double* components_out, double* eigvals_out, double* total_var_out, int32_t* k_out,
+                      int32_t* iters_out);
+int ef_fit_transform(ef_ctx* ctx, const uint8_t* X, int64_t n, int64_t d, const double* mean, const double* scale,
+                     const double* components, int32_t k, uint32_t flags, double* proj_out);
+
 /* --------------------------------------------------------------- projection
  * Recognition model f = (p - mean) . W  (useless/scan.py:93-96; sklearn
  * scaler.transform + pca.transform folded, scan-template-v4.py:265-266).

@@ -323,3 +323,75 @@ def test_merge_mode_is_checked():
     from eigenface.distributed import ShardedGallery
     with pytest.raises(ValueError):
         ShardedGallery(None, None, 10, 0, 1, merge="sum")
+
+
+# ------------------------------------------------------------- sample-sharded fit
+def _np_pieces(x):
+    """The exact integer pieces of include/eigenface.h ef_fit_shard_stats, in numpy."""
+    xi = np.asarray(x, np.int64)
+    xs = xi - 128
+    return xi.sum(0), (xi * xi).sum(0), xs.T @ xs
+
+
+def _np_fit_from_pieces(s1, s2, cr, n, k, standardize):
+    """ef_fit_from_stats's arithmetic restated (the covariance from exact integers,
+    oracle.top_eigh): what the sum over ranks must reproduce."""
+    _paths()
+    from eigenface import FitResult
+    from oracle import eigenface_oracle as orc
+    s1, s2, cr = (np.asarray(a, np.int64) for a in (s1, s2, cr))
+    mean = s1 / n
+    var = (n * s2 - s1 * s1) / float(n) ** 2
+    scale = np.where(var > 0, np.sqrt(var), 1.0) if standardize else np.ones_like(mean)
+    c = s1 - 128 * n
+    C = (n * cr.astype(np.float64) - np.outer(c, c).astype(np.float64)) / (n * (n - 1.0))
+    C /= np.outer(scale, scale)
+    lam, vt = orc.top_eigh(C.copy(), k)
+    return FitResult(mean, var, scale, vt, lam, None, float(np.trace(C)), k, 0)
+
+
+def _fit_worker(rank, world, port, x, k, standardize, out):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eigenface.distributed import shard_range, sharded_fit
+    lo, hi = shard_range(len(x), rank, world)
+    xl = x[lo:hi]
+
+    def transform(rows, res, stdz):
+        z = (np.asarray(rows, np.float64) - res.mean) / res.scale
+        return z @ res.components.T
+    res = sharded_fit(None, xl, k, standardize, stats_fn=_np_pieces, fit_fn=_np_fit_from_pieces,
+                      transform_fn=transform)
+    out[rank] = (res.eigenvalues.copy(), res.components.copy(), res.projection.copy(), res.mean.copy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fit_pieces_allreduce(world):
+    """distributed.sharded_fit on gloo (world 2 / 3, uneven shards): n_total and the summed
+    integer pieces reach every rank, every rank fits the same model, and the per-rank
+    projections stack to the projection of the whole set — equal to the fit from the
+    pieces of all rows at once (and to the oracle's covariance-path PCA)."""
+    _paths()
+    from oracle import eigenface_oracle as orc
+    x, _ = orc.synth_faces(401, 8, r=20, seed=world)  # n = 401 >= d = 64
+    k = 10
+    ref = _np_fit_from_pieces(*_np_pieces(x), len(x), k, True)
+    o = orc.pca_cov_fit(x, k, standardize=True)
+    np.testing.assert_allclose(ref.eigenvalues, o["explained_variance_"], rtol=1e-9)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_fit_worker, args=(world, _free_port(), x, k, True, out), nprocs=world, join=True)
+    for r in range(world):
+        lam, comps, proj, mean = out[r]
+        np.testing.assert_array_equal(lam, ref.eigenvalues)
+        np.testing.assert_array_equal(comps, ref.components)
+        np.testing.assert_array_equal(mean, ref.mean)
+    proj = np.concatenate([out[r][2] for r in range(world)])
+    z = (x.astype(np.float64) - ref.mean) / ref.scale
+    np.testing.assert_allclose(proj, z @ ref.components.T, atol=1e-9)
