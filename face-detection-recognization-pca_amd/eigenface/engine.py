@@ -102,6 +102,16 @@ class Engine:
             raise N.EigenfaceError(rc, f"ef_create(device={device}) failed (no usable HIP device?)")
         self._h = h
         self.device = int(device)
+        # The engine's own stream is a torch pool stream when torch is present: pool streams
+        # live as long as the process, so a tensor marked with record_stream (_torch_order)
+        # never outlives the stream it was recorded on.  A stream the library created would
+        # be destroyed by close() while such a tensor, freed later, still records an event
+        # on it (a host crash at free time).
+        self._pool_stream = None
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_available():
+            self._pool_stream = torch.cuda.Stream(device=self.device)
+            self._chk(self._lib.ef_set_stream(h, C.c_void_p(self._pool_stream.cuda_stream)))
         self.model_k = None
         self.model_d = None
         self.gallery_n = 0
@@ -139,8 +149,12 @@ class Engine:
         self._chk(self._lib.ef_set_stream(self._h, C.c_void_p(int(stream_handle) or None)))
 
     def use_own_stream(self):
-        """Back to the context's own non-blocking stream."""
-        self._chk(self._lib.ef_use_own_stream(self._h))
+        """Back to the engine's own non-blocking stream (its torch pool stream, or the
+        library's stream without torch)."""
+        if self._pool_stream is not None:
+            self.set_stream(self._pool_stream.cuda_stream)
+        else:
+            self._chk(self._lib.ef_use_own_stream(self._h))
 
     def synchronize(self):
         self._chk(self._lib.ef_synchronize(self._h))
@@ -159,21 +173,29 @@ class Engine:
         every tensor the call reads or writes — inputs included, e.g. a dtype-converted
         temporary that dies when the wrapper returns — is marked as used on the engine's
         stream, so the caching allocator hands its memory to no other stream before the
-        engine's kernels are done.  No host wait either way; a no-op when the engine
-        already runs on torch's stream."""
+        engine's kernels are done.  The mark is made only on streams that live as long as
+        the process (the engine's torch pool stream, the default stream): a tensor freed
+        after its stream was destroyed would crash the allocator; on a caller's external
+        stream (set_stream) inputs are safe to reuse on torch's current stream only.  No
+        host wait either way; a no-op when the engine already runs on torch's stream."""
         import torch
         h = self.stream_handle()
         cur = torch.cuda.current_stream(self.device)
         if h == cur.cuda_stream:
             yield
             return
-        ext = torch.cuda.ExternalStream(h, device=self.device) if h else torch.cuda.default_stream(self.device)
+        pool = self._pool_stream
+        if pool is not None and h == pool.cuda_stream:
+            ext = pool
+        else:
+            ext = torch.cuda.ExternalStream(h, device=self.device) if h else torch.cuda.default_stream(self.device)
         ext.wait_stream(cur)
         yield
         cur.wait_stream(ext)
-        for t in tensors:
-            if t is not None:
-                t.record_stream(ext)
+        if ext is pool or not h:
+            for t in tensors:
+                if t is not None:
+                    t.record_stream(ext)
 
     def trim(self):
         """Free the fit workspaces the context keeps between fits (ef_trim)."""

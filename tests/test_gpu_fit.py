@@ -428,3 +428,32 @@ def test_fit_c3_full_size_properties():
     assert res_rel <= 1e-6
     del X, CV
     torch.cuda.empty_cache()
+
+
+def test_device_tensors_outlive_a_closed_engine():
+    """Tensors that a device call marked as used on the engine's stream (record_stream, so
+    the caching allocator does not hand them to another stream too early) are freed after
+    the engine is closed: the engine's own stream is a process-lifetime torch pool stream,
+    so the allocator's free-time event record cannot hit a destroyed stream (round 5: with
+    a library-created stream this crashed the process at the tensor's free)."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    code = (f"import sys; sys.path.insert(0, {PKG!r})\n"
+            "import torch\n"
+            "from eigenface import Engine\n"
+            "from oracle import eigenface_oracle as orc\n"
+            "x, _ = orc.synth_faces(600, 32, r=24, seed=2)\n"
+            "X = torch.from_numpy(x).cuda()\n"
+            "e = Engine(0)\n"
+            "r = e.fit(X, 8, projection=True)\n"
+            "e.set_model(r.mean.float().cpu().numpy(), r.components.T.float().contiguous().cpu().numpy())\n"
+            "f = e.project(X)\n"
+            "e.close()\n"
+            "del X, f, r\n"
+            "y = torch.ones(1 << 20, device='cuda').sum()\n"
+            "torch.cuda.synchronize(); print('ok', float(y))\n")
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                         cwd=__import__("conftest").ROOT)
+    assert res.returncode == 0, (res.returncode, res.stderr[-2000:])
+    assert res.stdout.strip().startswith("ok")
