@@ -276,21 +276,37 @@ class ShardedGallery:
 def allreduce_fit_stats(pieces, group=None):
     """Sum the exact integer fit pieces (sum x, sum x^2, X'^T X'; int64) over the ranks of
     ``group`` in place: an integer sum, so the result is exact in any order.  RCCL takes
-    device tensors directly; gloo reduces host copies."""
+    device tensors directly; gloo reduces host copies.  Of X'^T X' only the upper 64-blocks
+    travel (d % 64 == 0)."""
     import torch
     import torch.distributed as dist
 
     gloo = dist.get_backend(group) == "gloo"
-    out = []
-    for t in pieces:
-        if not isinstance(t, torch.Tensor):
-            t = torch.from_numpy(np.ascontiguousarray(t, dtype=np.int64))
+
+    def reduce(t):
         if gloo and t.is_cuda:
             h = t.cpu()
             dist.all_reduce(h, group=group)
             t.copy_(h)
         else:
             dist.all_reduce(t, group=group)
+
+    out = []
+    for t in pieces:
+        if not isinstance(t, torch.Tensor):
+            t = torch.from_numpy(np.ascontiguousarray(t, dtype=np.int64))
+        d = t.shape[0]
+        if t.ndim == 2 and d % 64 == 0:
+            # X'^T X': only its upper 64 x 64 blocks are specified (and read by the covariance
+            # finalize), so only they travel — half the bytes of the d x d matrix
+            nb = d // 64
+            iu = torch.triu_indices(nb, nb, device=t.device)
+            blocks = t.view(nb, 64, nb, 64).permute(0, 2, 1, 3)
+            packed = blocks[iu[0], iu[1]].contiguous()
+            reduce(packed)
+            blocks[iu[0], iu[1]] = packed
+        else:
+            reduce(t)
         out.append(t)
     return out
 
@@ -304,7 +320,7 @@ def sharded_fit(engine, X_local, n_components: int, standardize: bool = False, g
     bandwidth-bound over xGMI, beside a SYRK of n_total / world rows), and every rank runs
     the covariance-path fit from the sums (``Engine.fit_from_stats``) — bit-identical to
     ``Engine.fit`` on the concatenated rows, because the same integers give the same
-    covariance — then projects its own rows (``Engine.fit_transform_rows``).  Returns the
+    covariance (only the upper 64-blocks of X'^T X' are reduced: 1 GiB at d = 16384) — then projects its own rows (``Engine.fit_transform_rows``).  Returns the
     FitResult with ``projection`` = this rank's rows.  The ``*_fn`` hooks replace the
     engine calls (CPU tests)."""
     import torch

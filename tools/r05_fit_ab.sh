@@ -21,6 +21,6 @@ print('eigenvalues identical', bool(np.array_equal(a['eigenvalues'], b['eigenval
       'components identical', bool(np.array_equal(a['components'], b['components'])),
       'max rel eig diff', float(np.max(np.abs(a['eigenvalues'] - b['eigenvalues']) / b['eigenvalues'])))
 " >> $O/ab.txt || exit $?
-timeout -k 10 600 python -u -m pytest tests/test_gpu_sharded_fit.py tests/test_gpu_fit.py tests/test_gpu_manual.py -x -v --timeout 300 -p no:cacheprovider > $O/pytest.txt 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fit.py::test_device_tensors_outlive_a_closed_engine tests/test_gpu_sharded_fit.py tests/test_gpu_fit.py tests/test_gpu_manual.py -x -v --timeout 300 -p no:cacheprovider > $O/pytest.txt 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/fr -o run -- python tools/prof_fit.py > $O/prof.txt 2>&1 || exit $?
 python tools/fit_breakdown.py /tmp/fr/run_kernel_trace.csv > $O/breakdown.txt && cp /tmp/fr/run_kernel_stats.csv $O/kernel_stats.csv
