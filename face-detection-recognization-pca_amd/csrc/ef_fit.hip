@@ -191,6 +191,8 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   EF_TRY(B.get(c, (size_t)m * m, &W2));
   EF_TRY(B.get(c, (size_t)m, &lam));
   EF_TRY(B.get(c, 4, &cinfo));
+  double* CW;  // blocked Cholesky + inverse scratch
+  EF_TRY(B.get(c, chol_inv_work_elems(m), &CW));
   // Chebyshev recurrence state (EF_OPT_FIT_CHEBYSHEV): Qold = the block before the last
   // orthonormalisation, Wc = the previous filter iterate in the current block's frame
   double *Qold, *Wc;
@@ -210,9 +212,14 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
                          kWorkElems, Bt),
            "G = Y^T.Y");
     int hinfo = -1;
-    const bool fused = chol_inv_supported(m);  // Cholesky + L^-1 in one register-resident workgroup
+    const bool fused = chol_inv_supported(m);  // blocked Cholesky + L^-1 (ef_chol_blk.hip)
     if (fused) {
-      EF_HIP(c, launch_chol_inv(s, G, m, m, 1e-13, Li, cinfo), "cholesky + L^-1");
+#ifdef EF_CHOL_REG  // A/B build (tools/r05_chol.sh): round 4's register-resident kernel
+      if (chol_inv_reg_supported(m))
+        EF_HIP(c, launch_chol_inv_reg(s, G, m, m, 1e-13, Li, cinfo), "cholesky + L^-1");
+      else
+#endif
+      EF_HIP(c, launch_chol_inv(s, G, m, m, 1e-13, Li, cinfo, CW), "cholesky + L^-1");
     } else if (m <= kCholeskyMax) {
       EF_HIP(c, launch_cholesky(s, G, m, m, 1e-13, cinfo), "cholesky");
     }

@@ -790,10 +790,11 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double* __restrict
   if (tid == 0) *info = 0;
 }
 
-bool chol_inv_supported(int m) { return m >= 1 && m <= kCholInvMax && m % 2 == 0; }
+bool chol_inv_reg_supported(int m) { return m >= 1 && m <= kCholInvMax && m % 2 == 0; }
 
-hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li, int* info) {
-  if (!chol_inv_supported(m)) return hipErrorInvalidValue;
+hipError_t launch_chol_inv_reg(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li,
+                               int* info) {
+  if (!chol_inv_reg_supported(m)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(1024), 0, s, G, m, lda, tol_rel, Li, info);
   return hipGetLastError();
 }

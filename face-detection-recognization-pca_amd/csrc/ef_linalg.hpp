@@ -187,11 +187,18 @@ hipError_t launch_cov_i8_cross(hipStream_t s, const CovPlan& p, int64_t d, const
 hipError_t launch_cov_from_cross(hipStream_t s, const long long* S64, const unsigned long long* S1, int64_t n,
                                  int64_t d, const double* w, long long* cvec, double* C);
 hipError_t launch_cholesky(hipStream_t s, double* A, int m, int64_t lda, double tol_rel, int* info);
-// Li = L^-1 (row-major, zeros above the diagonal) for G = L L^T in one register-resident
-// workgroup (m <= 256, m even: chol_inv_supported); G is not modified; *info as
-// launch_cholesky.
+// Li = L^-1 (row-major, zeros above the diagonal) for G = L L^T, m <= 256
+// (chol_inv_supported); G is not modified; *info as launch_cholesky.  launch_chol_inv: the
+// blocked one-workgroup Cholesky + block-column-parallel inverse (ef_chol_blk.hip; work:
+// chol_inv_work_elems(m) doubles); launch_chol_inv_reg: round 4's register-resident
+// single-workgroup kernel (m even), kept for A/B and the microbenchmark.
 bool chol_inv_supported(int m);
-hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li, int* info);
+size_t chol_inv_work_elems(int m);
+hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li, int* info,
+                           double* work);
+bool chol_inv_reg_supported(int m);
+hipError_t launch_chol_inv_reg(hipStream_t s, const double* G, int m, int64_t lda, double tol_rel, double* Li,
+                               int* info);
 // Training projection F (n x kk, fp64) = ((X - mu) * w) . E on int8 MFMA with E split into
 // base-256 digits (ef_proj_i8.hip); w may be null.  work: proj_i8_work_bytes bytes.
 bool proj_i8_supported(const uint8_t* X, int64_t n, int64_t d, int kk);
