@@ -16,9 +16,9 @@
 //      T2 (workers)   A_IK -= L_IJ . L_KJ^T for K > J + 1 (the rest of the trailing matrix).
 //    Three barriers per block column; the serial part is 16 diagonal factorisations
 //    instead of 512 workgroup-wide column steps.
-//  tri_inv_blk_kernel (one workgroup per block column J, 4 waves): X = L^-1 by blocked
-//    forward substitution, X_JJ = Inv_JJ, X_IJ = -Inv_II . sum_{K=J}^{I-1} L_IK X_KJ, the
-//    K sum split over the 4 waves and added in a fixed order.
+//  tri_inv_blk_kernel (one workgroup per block column J, 16 waves): X = L^-1 by blocked
+//    forward substitution, X_JJ = Inv_JJ, X_IJ = -Inv_II . sum_{K=J}^{I-1} L_IK X_KJ, one
+//    K term per wave, the terms added in a fixed order.
 //
 // Operand images.  For v_mfma_f64_16x16x4_f64 (A lane l = A[l&15][l>>4], B lane l =
 // B[l>>4][l&15], D lane l reg r = D[(l>>4)+4r][l&15]) every operand and accumulator here is
@@ -38,6 +38,7 @@
 #include "ef_linalg.hpp"
 
 #include <cmath>
+#include <utility>
 
 namespace ef {
 namespace {
@@ -74,6 +75,90 @@ __device__ __forceinline__ f64x4 block_mma(const double* Mcol, const double* Xro
   return acc;
 }
 
+// Block ownership: block (I, K) -> worker (I + 2K) mod 7, listed in column order.  The
+// blocks of every block column fall on consecutive residues, so the panel solve and the
+// column-(J+1) update of each block column spread over all workers (at most 3 blocks
+// each; round robin over b put 5 on one wave), and so do every block row's, which keeps
+// the trailing updates balanced too.  At most kCbSlots blocks per worker.
+struct CbTab {
+  short ik[kCbWorkers][kCbSlots];  // 32 I + K, -1 past the wave's last block
+};
+constexpr CbTab make_cb_tab() {
+  CbTab t{};
+  int cnt[kCbWorkers] = {};
+  for (int w = 0; w < kCbWorkers; ++w)
+    for (int s = 0; s < kCbSlots; ++s) t.ik[w][s] = -1;
+  for (int K = 0; K < kCbMaxNb; ++K)
+    for (int I = K; I < kCbMaxNb; ++I) {
+      const int w = (I + 2 * K) % kCbWorkers;
+      if (cnt[w] < kCbSlots) t.ik[w][cnt[w]] = (short)(32 * I + K);
+      ++cnt[w];
+    }
+  return t;
+}
+constexpr bool cb_tab_fits() {
+  int cnt[kCbWorkers] = {};
+  for (int K = 0; K < kCbMaxNb; ++K)
+    for (int I = K; I < kCbMaxNb; ++I) ++cnt[(I + 2 * K) % kCbWorkers];
+  for (int w = 0; w < kCbWorkers; ++w)
+    if (cnt[w] > kCbSlots) return false;
+  return true;
+}
+static_assert(cb_tab_fits(), "a worker owns more blocks than it has slots");
+__constant__ CbTab kCbTab = make_cb_tab();
+
+// The diagonal wave's LDS images (dbuf, ibuf) are column-major with a 17-double column
+// stride: its column reads (lane c: column c) and the lane-contiguous MFMA operand reads
+// (flat index f = 64 r + lane -> column f >> 4, row f & 15) are then both conflict-free.
+constexpr int kPs = 17;
+__device__ __forceinline__ int pidx(int f) { return f + (f >> 4); }
+
+// acc += src(lane T of this 16-lane row) * mul: one v_fmac_f64 with a DPP row_newbcast
+// source (gfx950 allows 64-bit DPP with that control only); s_nop 1 covers the
+// VALU-write -> DPP-read hazard the compiler cannot see through the asm
+template <int T>
+__device__ __forceinline__ void fmac_bcast(double& acc, double src, double mul) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(src), "v"(mul), "i"(T));
+}
+
+// Column T of the diagonal block's Cholesky (unscaled right-looking form): lane c > T
+// updates a[i] -= A[i][T] A[T][c] / d for i > T, A[i][T] broadcast from lane T
+template <int T>
+__device__ __forceinline__ void chol_step(double (&a)[16], int c, double tol, int& bad, double& dc) {
+  const double d = rdlane(a[T], T);  // the pivot (uniform)
+  // uniform; the sweep runs on (its results unused) so every index stays static
+  if (bad == 0 && !(d > tol)) bad = T + 1;
+  const double nf = c > T ? -(a[T] * rcp_nr(d)) : 0.0;  // a[T] = A[T][c] = A[c][T]
+#pragma unroll
+  for (int i = T + 1; i < 16; ++i) fmac_bcast<T>(a[i], a[i], nf);
+  dc = (c == T) ? d : dc;
+}
+template <int... Ts>
+__device__ __forceinline__ void chol_sweep(double (&a)[16], int c, double tol, int& bad, double& dc,
+                                           std::integer_sequence<int, Ts...>) {
+  (chol_step<Ts>(a, c, tol, bad, dc), ...);
+}
+// Row K of the forward substitution L x = e_c: x_K = b_K / L_KK, then x_i -= L_iK x_K for
+// i > K with L_iK broadcast from lane K (which holds column K of L in l)
+template <int K>
+__device__ __forceinline__ void inv_step(double (&x)[16], const double (&l)[16], double rc) {
+  x[K] *= rdlane(rc, K);
+  const double nx = -x[K];
+#pragma unroll
+  for (int i = K + 1; i < 16; ++i) fmac_bcast<K>(x[i], l[i], nx);
+}
+template <int... Ks>
+__device__ __forceinline__ void inv_sweep(double (&x)[16], const double (&l)[16], double rc,
+                                          std::integer_sequence<int, Ks...>) {
+  (inv_step<Ks>(x, l, rc), ...);
+}
+
+// LDS-only barrier: waits for this wave's LDS operations, not its global stores (which the
+// next kernel reads; __syncthreads would wait for their write-back every block column)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 }  // namespace
 
 #ifdef EF_CB_STAMP  // phase timing (tools/micro/chol_inv_bench.cpp -DEF_CB_STAMP): s_memtime
@@ -101,16 +186,14 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
                                                               double* __restrict__ invN, double* __restrict__ invT,
                                                               int* __restrict__ info) {
   __shared__ double panel[kCbMaxNb][256];  // column-major L_IJ of the current block column
-  __shared__ double dbuf[256];             // column-major -A_JJ (after all its updates)
-  __shared__ double ibuf[256];             // column-major -Inv_JJ
-  __shared__ double lbuf[256];             // column-major L_JJ (diagonal wave only)
-  __shared__ double rsb[16];               // 1 / L_tt
+  __shared__ double dbuf[16 * kPs];        // column-major -A_JJ (after all its updates)
+  __shared__ double ibuf[16 * kPs];        // column-major -Inv_JJ
   __shared__ double red[kCbWorkers + 1];
   __shared__ int fail;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block ownership in SGPRs
   const int c = lane & 15, g = lane >> 4;
-  const int nb = (m + 15) >> 4, nblk = nb * (nb + 1) / 2;
+  const int nb = (m + 15) >> 4;
   const bool worker = wave < kCbWorkers;
   if (tid == 0) fail = 0;
 
@@ -136,15 +219,10 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
     f64x4 acc[kCbSlots];
 #pragma unroll
     for (int s = 0; s < kCbSlots; ++s) {
-      const int b = wave + kCbWorkers * s;
-      int I = -1, K = -1;
-      if (b < nblk) {
-        I = (int)((sqrtf(8.0f * (float)b + 1.0f) - 1.0f) * 0.5f);
-        while (I * (I + 1) / 2 > b) --I;
-        while ((I + 1) * (I + 2) / 2 <= b) ++I;
-        K = b - I * (I + 1) / 2;
-      }
-      sIK[s] = I < 0 ? -1 : 32 * I + K;
+      int ik = kCbTab.ik[wave][s];
+      if (ik >= 0 && (ik >> 5) >= nb) ik = -1;  // (K <= I: the block is outside the order)
+      const int I = ik < 0 ? -1 : ik >> 5, K = ik < 0 ? -1 : ik & 31;
+      sIK[s] = ik;
       acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
       if (I >= 0) {
 #pragma unroll
@@ -160,11 +238,11 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
         }
         if (I == 0 && K == 0)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dbuf[64 * r + lane] = acc[s][r];
+          for (int r = 0; r < 4; ++r) dbuf[pidx(64 * r + lane)] = acc[s][r];
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+    lds_barrier();
     for (int J = 0; J < nb; ++J) {
       // (laundered each iteration: what derives from them is recomputed, not hoisted into
       // registers the accumulators need)
@@ -183,17 +261,17 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
         }
       }
       if (wave == 0) CB_STAMP(0, J, 1);
-      __syncthreads();  // B1
+      lds_barrier();  // B1
       if (fail) return;
       if (wave == 0) CB_STAMP(0, J, 2);
       // ---- P: L_IJ (column-major) = row-major result of (-Inv_JJ) . (-A_IJ)^T
+      double a[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = ibuf[pidx(64 * r + lane_j)];
 #pragma unroll
       for (int s = 0; s < kCbSlots; ++s) {
         const int I = sIK[s] >> 5, K = sIK[s] & 31;
         if (sIK[s] >= 0 && K == J && I > J) {
-          double a[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) a[r] = ibuf[64 * r + lane_j];
           f64x4 L = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int r = 0; r < 4; ++r) L = mma(a[r], acc[s][r], L);
@@ -207,56 +285,45 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
         __builtin_amdgcn_sched_barrier(0);
       }
       if (wave == 0) CB_STAMP(0, J, 3);
-      __syncthreads();  // B2
+      lds_barrier();  // B2
       if (wave == 0) CB_STAMP(0, J, 4);
       // ---- T1: block column J + 1 (its diagonal block goes to dbuf for the next D)
+      if (J + 1 < nb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = panel[J + 1][64 * r + lane_j];  // L_{J+1,J}: every block's A
+      }
 #pragma unroll
       for (int s = 0; s < kCbSlots; ++s) {
         const int I = sIK[s] >> 5, K = sIK[s] & 31;
         if (sIK[s] >= 0 && K == J + 1) {
-          acc[s] = block_mma(panel[K], panel[I], acc[s], lane_j);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[s] = mma(a[r], panel[I][64 * r + lane_j], acc[s]);
           if (I == K)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dbuf[64 * r + lane_j] = acc[s][r];
+            for (int r = 0; r < 4; ++r) dbuf[pidx(64 * r + lane_j)] = acc[s][r];
         }
         __builtin_amdgcn_sched_barrier(0);
       }
       if (wave == 0) CB_STAMP(0, J, 5);
-      __syncthreads();  // B3
+      lds_barrier();  // B3
       if (wave == 0) CB_STAMP(0, J, 6);
     }
   } else {
-    __syncthreads();
+    lds_barrier();
     for (int J = 0; J < nb; ++J) {
       int c = lane & 15;
       asm volatile("" : "+v"(c));  // keeps the lane-dependent masks and constants out of
                                    // loop-invariant hoisting (they would pin ~80 registers)
       CB_STAMP(1, J, 0);
       // ---- D: factor and invert the diagonal block; lane c holds column c (lanes 16..63
-      // repeat lanes 0..15).  The block is symmetrised from its lower triangle.
+      // repeat lanes 0..15, so every 16-lane row can broadcast from its own lane t).  The
+      // block is symmetrised from its lower triangle.
       double a[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) a[i] = -((i >= c) ? dbuf[16 * c + i] : dbuf[16 * i + c]);
+      for (int i = 0; i < 16; ++i) a[i] = -((i >= c) ? dbuf[kPs * c + i] : dbuf[kPs * i + c]);
       int bad = 0;
-      double dc = 0.0, rc = 0.0;  // this lane's pivot and 1 / sqrt of it
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const double d = rdlane(a[t], t);
-        // uniform; the sweep runs on (its results unused) so every index stays static
-        if (bad == 0 && !(d > tol)) bad = t + 1;
-        const double inv = rcp_nr(d);
-        const double own = a[t];  // A[t][c] = A[c][t]
-        const bool act = c > t;
-#pragma unroll
-        for (int i = t + 1; i < 16; ++i) {
-          const double ci = rdlane(a[i], t);  // A[i][t]
-          // (A[i][t] A[c][t]) / d: the same product for (i, c) and (c, i), so the trailing
-          // block stays exactly symmetric
-          const double nv = fma(-(ci * own), inv, a[i]);
-          a[i] = act ? nv : a[i];
-        }
-        dc = (c == t) ? d : dc;
-      }
+      double dc = 0.0;  // this lane's pivot
+      chol_sweep(a, c, tol, bad, dc, std::make_integer_sequence<int, 16>{});
       CB_STAMP(1, J, 1);
       if (bad) {
         if (lane == 0) {
@@ -264,106 +331,119 @@ __global__ __launch_bounds__(kCbThreads) void chol_blk_kernel(const double* __re
           fail = 1;
         }
       } else {
-        // column c of L: a[i] / sqrt(d_c) below the diagonal, sqrt(d_c) on it; staged in
-        // LDS (column-major) with the reciprocal diagonal for the inverse's broadcasts
-        rc = rsq_nr(dc);
-        double* lf = LF + (int64_t)blk_index(J, J) * 256;
+        // column c of L: a[i] / sqrt(d_c) below the diagonal, sqrt(d_c) on it
+        const double rc = rsq_nr(dc);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const double v = i > c ? a[i] * rc : (i == c ? dc * rc : 0.0);
-          if (lane < 16) {
-            lbuf[16 * c + i] = v;
-            lf[16 * c + i] = v;
-          }
-        }
-        if (lane < 16) rsb[c] = rc;
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
-        __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < 16; ++i) a[i] = i > c ? a[i] * rc : (i == c ? dc * rc : 0.0);
         CB_STAMP(1, J, 2);
-        // column c of X = L^-1: forward substitution on e_c (x_k = 0 for k < c); the L
-        // entries are same-address LDS reads, independent of x
+        // column c of X = L^-1: forward substitution on e_c (x_k = 0 for k < c)
         double x[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          x[k] *= rsb[k];
-#pragma unroll
-          for (int i = k + 1; i < 16; ++i) x[i] = fma(-lbuf[16 * k + i], x[k], x[i]);
-        }
+        inv_sweep(x, a, rc, std::make_integer_sequence<int, 16>{});
         if (lane < 16) {
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            ibuf[16 * c + i] = -x[i];
-            invN[J * 256 + 16 * c + i] = -x[i];
-            invT[J * 256 + 16 * i + c] = x[i];
+          for (int i = 0; i < 16; ++i) ibuf[kPs * c + i] = -x[i];
+        }
+        // global images, four stores per array: row group q (the lane's replica) stores
+        // rows i = 4j + q
+        const int q = lane >> 4;
+        double* lf = LF + (int64_t)blk_index(J, J) * 256;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          double xv = x[4 * j], lv = a[4 * j];
+#pragma unroll
+          for (int u = 1; u < 4; ++u) {
+            xv = q == u ? x[4 * j + u] : xv;
+            lv = q == u ? a[4 * j + u] : lv;
           }
+          const int i = 4 * j + q;
+          invN[J * 256 + 16 * c + i] = -xv;
+          invT[J * 256 + 16 * i + c] = xv;
+          lf[16 * c + i] = lv;
         }
       }
       CB_STAMP(1, J, 3);
-      __syncthreads();  // B1
+      lds_barrier();  // B1
       if (fail) return;
       CB_STAMP(1, J, 4);
-      __syncthreads();  // B2
+      lds_barrier();  // B2
       CB_STAMP(1, J, 5);
-      __syncthreads();  // B3
+      lds_barrier();  // B3
       CB_STAMP(1, J, 6);
     }
     if (lane == 0) *info = 0;
   }
 }
 
-__global__ __launch_bounds__(256) void tri_inv_blk_kernel(const double* __restrict__ LF, const double* __restrict__ invN,
-                                                          const double* __restrict__ invT, int m,
-                                                          double* __restrict__ Li, const int* __restrict__ info) {
-  __shared__ double xb[kCbMaxNb][256];  // row-major X_KJ of this block column
-  __shared__ double part[4][256];       // the waves' partial sums
-  if (*info != 0) return;               // failed factorisation: Li untouched
-  const int J = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// Wave w of block column J's workgroup owns X_{J+w,J} in its accumulator registers (the
+// B image its products read): at step I every wave w < I - J adds its partial
+// L_{I,J+w} . X_{J+w,J} into LDS, one barrier, and wave I - J, the only later reader of
+// X_IJ, sums the partials in wave order and forms X_IJ = (-Inv_II) . sum.  One barrier per
+// block row; the L blocks of the next step and the wave's own -Inv are loaded a step ahead.
+__global__ __launch_bounds__(64 * kCbMaxNb) void tri_inv_blk_kernel(const double* __restrict__ LF,
+                                                                  const double* __restrict__ invN,
+                                                                  const double* __restrict__ invT, int m,
+                                                                  double* __restrict__ Li,
+                                                                  const int* __restrict__ info) {
+  __shared__ double part[2][kCbMaxNb][256];  // partial sums, double-buffered by step parity
+  if (*info != 0) return;                    // failed factorisation: Li untouched
+  const int J = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, g = lane >> 4;
   const int nb = (m + 15) >> 4;
+  const int own = J + w;  // the block row this wave finalises and then holds
   auto store = [&](int I, int r, double v) {  // element 64r + lane of row-major X_IJ
     const int row = 16 * I + 4 * r + g, col = 16 * J + c;
     if (row < m && col < m) Li[(int64_t)row * m + col] = v;
   };
-  for (int e = tid; e < 256 * J; e += 256) {  // zeros above the diagonal: rows < 16 J
+  for (int e = tid; e < 256 * J; e += 64 * kCbMaxNb) {  // zeros above the diagonal: rows < 16 J
     const int row = e >> 4, col = 16 * J + (e & 15);
     if (row < m && col < m) Li[(int64_t)row * m + col] = 0.0;
   }
-  if (w == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double v = invT[J * 256 + 64 * r + lane];
-      xb[J][64 * r + lane] = v;
-      store(J, r, v);
-    }
-  }
-  __syncthreads();
-  for (int I = J + 1; I < nb; ++I) {
-    f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int K = J + w; K < I; K += 4) acc = block_mma(LF + (int64_t)blk_index(I, K) * 256, xb[K], acc, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[w][64 * r + lane] = acc[r];
-    __syncthreads();
+  f64x4 X = f64x4{0.0, 0.0, 0.0, 0.0};
+  double ninv[4] = {0.0, 0.0, 0.0, 0.0}, lf[4] = {0.0, 0.0, 0.0, 0.0};
+  if (own < nb) {
     if (w == 0) {
-      double a[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        X[r] = invT[J * 256 + 64 * r + lane];
+        store(J, r, X[r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ninv[r] = invN[own * 256 + 64 * r + lane];
+    }
+    if (own + 1 < nb)  // L_{J+w+1, J+w}: this wave's first partial (step I = own + 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lf[r] = LF[(int64_t)blk_index(own + 1, own) * 256 + 64 * r + lane];
+  }
+  for (int I = J + 1; I < nb; ++I) {
+    const int buf = I & 1;
+    if (own < I) {  // partial L_{I,own} . X_{own,J}
+      f64x4 p = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p = mma(lf[r], X[r], p);
+      if (I + 1 < nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lf[r] = LF[(int64_t)blk_index(I + 1, own) * 256 + 64 * r + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[buf][w][64 * r + lane] = p[r];
+    }
+    lds_barrier();
+    if (own == I) {  // X_IJ = (-Inv_II) . sum of the partials of waves 0 .. I-J-1
       f64x4 T;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] = invN[I * 256 + 64 * r + lane];
-        const int e = 64 * r + lane;
-        T[r] = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
-      }
-      f64x4 X = f64x4{0.0, 0.0, 0.0, 0.0};
+      for (int r = 0; r < 4; ++r) T[r] = part[buf][0][64 * r + lane];
+      for (int v = 1; v < w; ++v)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) X = mma(a[r], T[r], X);
+        for (int r = 0; r < 4; ++r) T[r] += part[buf][v][64 * r + lane];
+      X = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        xb[I][64 * r + lane] = X[r];
-        store(I, r, X[r]);
-      }
+      for (int r = 0; r < 4; ++r) X = mma(ninv[r], T[r], X);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) store(I, r, X[r]);
     }
-    __syncthreads();
   }
 }
 
@@ -377,7 +457,7 @@ hipError_t launch_chol_inv(hipStream_t s, const double* G, int m, int64_t lda, d
   double* invN = LF + (size_t)nblk * 256;
   double* invT = invN + (size_t)nb * 256;
   hipLaunchKernelGGL(chol_blk_kernel, dim3(1), dim3(kCbThreads), 0, s, G, m, lda, tol_rel, LF, invN, invT, info);
-  hipLaunchKernelGGL(tri_inv_blk_kernel, dim3(nb), dim3(256), 0, s, LF, invN, invT, m, Li, info);
+  hipLaunchKernelGGL(tri_inv_blk_kernel, dim3(nb), dim3(64 * kCbMaxNb), 0, s, LF, invN, invT, m, Li, info);
   return hipGetLastError();
 }
 
