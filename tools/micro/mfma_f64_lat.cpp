@@ -6,7 +6,7 @@
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 __global__ void k(const double* in, double* out, unsigned long long* t) {
   const int lane = threadIdx.x;
-  double a = in[lane], b = in[lane + 64];
+  double a = in[lane], b = in[lane + 64], b1 = in[lane + 1], b2 = in[lane + 2], b3 = in[lane + 3];
   f64x4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #pragma unroll
@@ -17,9 +17,9 @@ __global__ void k(const double* in, double* out, unsigned long long* t) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
-    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
-    c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1, c1, 0, 0, 0);  // distinct operands: no CSE
+    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b2, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b3, c3, 0, 0, 0);
   }
   out[lane + 64] = c0[0] + c1[1] + c2[2] + c3[3];
   unsigned long long t2 = __builtin_amdgcn_s_memtime();
