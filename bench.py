@@ -350,6 +350,29 @@ def pmc_traffic(config):
     return None, None
 
 
+def pmc_record(config):
+    """The newest committed PMC summary whose "config" is `config` (tools/pmc_summary.py,
+    tools/img_summary.py), and its path."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary*.json")), reverse=True):
+        rec = json.load(open(f))
+        if rec.get("config") == config:
+            return rec, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def tmatch_executed_ops(probs, H, W, tile=128, blk=32):
+    """int8 MFMA work tm_corr_kernel executes for these maps: whole 128 x 128 output tiles,
+    and per template row the band's (w + 31) columns rounded up to whole 32-column k-blocks
+    (DESIGN K11) — against the algorithmic 2 (H-h+1)(W-w+1) h w."""
+    ex = 0.0
+    for _, ph, pw in probs:
+        oh, ow = H - ph + 1, W - pw + 1
+        kb = -(-(pw + blk - 1) // blk) * blk
+        ex += 2.0 * (-(-oh // tile) * tile) * (-(-ow // tile) * tile) * ph * kb
+    return ex
+
+
 def bf16_ceiling(loop, name="bf16_clock.json"):
     """TFLOP/s a bare bf16 MFMA loop of this shape (operands re-read from LDS, 2 waves per
     SIMD, every CU busy, random data) holds under the chip's power-limited clock: the
@@ -753,6 +776,15 @@ def image_bench(eng, with_cpu: bool, frames=20):
         "ms_per_frame_device": round(kdt * 1e3, 4),
         "algorithmic_ops": ops, "achieved_TOPS": round(ops / kdt / 1e12, 2), "peak_TOPS": PEAK_I8_TOPS,
         "frac": round(ops / kdt / 1e12 / PEAK_I8_TOPS, 4)}
+    # where the gap to peak goes: executed MFMA work (tiles, band) and the counters
+    ex = tmatch_executed_ops(probs, H, W)
+    res["tmatch"]["executed_ops"] = ex
+    res["tmatch"]["executed_to_algorithmic"] = round(ex / ops, 3)
+    pm, src = pmc_record("tmatch")
+    if pm:
+        res["tmatch"]["tm_corr_kernel"] = {"mfma_busy_frac": round(pm["mfma_busy_frac"], 4),
+                                           "clock_ghz": round(pm["clock_ghz"], 3),
+                                           "avg_ms_profiled": round(pm["trace_avg_ns"] / 1e6, 4), "source": src}
     if with_cpu:
         from oracle import image_oracle as io
         from eigenface.image import scaled_sizes as ss  # noqa: F401
@@ -841,6 +873,14 @@ def haar_bench(eng, with_cpu: bool, frames=10):
            "frames_per_s": round(1 / dt, 2), "ms_per_frame_host": round(dt * 1e3, 4),
            "ms_per_frame_device": round(k_ms / max(k_n, 1), 4), "candidates": int(len(cand)),
            "detections": int(len(rects))}
+    # roofline: the stage groups are bound by the texture-address unit every integral-image
+    # gather passes through (no MFMA, L2-resident tables): its busy fraction from the
+    # committed PMC summary (tools/img_summary.py)
+    pm, src = pmc_record("haar")
+    if pm:
+        out["roofline"] = {"bound": "ta", "kernel": pm["kernel"], "achieved": round(100 * pm["ta_busy_frac"], 1),
+                           "peak": 100.0, "unit": "% of cycles the TA is busy", "frac": round(pm["ta_busy_frac"], 4),
+                           "traffic": None, "source": src}
     if with_cpu:
         sys.path.insert(0, ROOT)
         from oracle import haar_oracle as ho

@@ -62,3 +62,17 @@ def test_launch_ranks_passes_environment(tmp_path, monkeypatch):
         assert (rank, local, world, addr) == (str(r), str(r), "3", "127.0.0.1")
         assert port in (None, p)
         port = p
+
+
+def test_tmatch_executed_work_model():
+    """bench.tmatch_executed_ops: whole 128 x 128 output tiles, band columns rounded up to
+    32-column k-blocks (DESIGN K11)."""
+    sys.path.insert(0, ROOT)
+    import importlib
+    bench = importlib.import_module("bench")
+    # output exactly one tile (128 x 128), template 40 x 33: band 33 + 31 = 64 columns
+    H, W, h, w = 127 + 40, 127 + 33, 40, 33
+    ex = bench.tmatch_executed_ops([(0, h, w)], H, W)
+    assert ex == 2.0 * 128 * 128 * h * 64
+    # one more output column needs a second tile column
+    assert bench.tmatch_executed_ops([(0, h, w)], H, W + 1) == 2 * ex
