@@ -147,6 +147,17 @@ inline double rr_loose_tol() {
 #endif
   return 1e-4;
 }
+// The first Rayleigh-Ritz step's tolerance: its Ritz values only set the first shift and
+// Chebyshev rate (there is no previous step to compare with), and its basis is re-mixed
+// by the products and CholQR factors that follow.  1e-2 takes 2 of the C3 fit's 20 Jacobi
+// sweeps off, ~1.9 ms, same 23 iterations, eigenvalues equal to 3e-15
+// (profiles/r05/rr_first_ab.txt).
+inline double rr_first_tol() {
+#ifdef EF_DIAGNOSTICS  // EF_FIT_RR_FIRST (A/B)
+  if (const char* e = getenv("EF_FIT_RR_FIRST")) return atof(e);
+#endif
+  return 1e-2;
+}
 constexpr int kCholeskyMax = 512;  // launch_cholesky's LDS panel limit (wider: eigen-orthonormalise)
 
 __global__ void f64_to_f32_kernel(const double* __restrict__ a, int64_t n, float* __restrict__ b) {
@@ -352,7 +363,7 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       // gap) instead of 1e-12 — the last sweeps of those solves (C3: 1e-4 0.1461 s, 1e-6
       // 0.1467 s, 1e-3 one more iteration; profiles/r04/rr_loose_ab.txt).  The Ritz basis V stays
       // orthogonal to rounding either way (rotations), so the block's span is unchanged.
-      EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(H)", fine ? 1e-12 : rr_loose_tol()));
+      EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(H)", fine ? 1e-12 : have_prev ? rr_loose_tol() : rr_first_tol()));
       EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
       if (!std::isfinite(th[0])) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
