@@ -5,6 +5,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -76,3 +77,17 @@ def test_tmatch_executed_work_model():
     assert ex == 2.0 * 128 * 128 * h * 64
     # one more output column needs a second tile column
     assert bench.tmatch_executed_ops([(0, h, w)], H, W + 1) == 2 * ex
+
+
+def test_ingest_touched_bytes_model():
+    """bench.ingest_touched_bytes: the copy path touches every line of the crop; a 4x
+    downscale only the lines of its sampled rows (2 per output row)."""
+    sys.path.insert(0, ROOT)
+    import importlib
+    bench = importlib.import_module("bench")
+    # 64 x 64 grey copy at a line-aligned offset: every byte, 32 lines + the output
+    assert bench.ingest_touched_bytes([0], [64], [64], [1]) == 64 * 64 + 64 * 64
+    # 256 x 256 grey -> 64 x 64: 128 distinct source rows of 256 B (2 lines each)
+    rows = np.unique(np.concatenate(bench._lin_src(64, 256)))
+    assert rows.size == 128
+    assert bench.ingest_touched_bytes([0], [256], [256], [1]) == 128 * 256 + 64 * 64
