@@ -158,6 +158,20 @@ inline double rr_first_tol() {
 #endif
   return 1e-2;
 }
+// Ritz-residual acceptance: a Rayleigh-Ritz step after an fp64 product also ends the
+// iteration when every kept pair has |C u_i - theta_i u_i| <= 1e-9 theta_1.  Then each
+// theta_i is within |r|^2 / gap of an eigenvalue and u_i within |r| / gap of its vector.
+// The value-change test needs a second fp64 step to compare with.  The residual test
+// decides from one step, so the C3 fit stops after 22 products instead of 23.  Its
+// eigenvalues move by 1.6e-13 and its components by 1.7e-8 against the 23-product fit,
+// 4.7 ms per fit (profiles/r05/resid_ab.txt).  The residuals come from Y.V, the
+// continuation product, and U = Q.V, the result's.
+inline double fit_resid_tol() {
+#ifdef EF_DIAGNOSTICS  // EF_FIT_RESID_TOL (A/B; 0 = off)
+  if (const char* e = getenv("EF_FIT_RESID_TOL")) return atof(e);
+#endif
+  return 1e-9;
+}
 constexpr int kCholeskyMax = 512;  // launch_cholesky's LDS panel limit (wider: eigen-orthonormalise)
 
 __global__ void f64_to_f32_kernel(const double* __restrict__ a, int64_t n, float* __restrict__ b) {
@@ -180,6 +194,33 @@ __global__ void cheb_combine_kernel(double* __restrict__ y, const double* __rest
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = w ? fma(sc, y[i], -w[i]) : sc * y[i];
 }
+// Ritz residuals of a Rayleigh-Ritz step: partial sums of |YV_i - lam_i U_i|^2 over row
+// chunk blockIdx.y for columns 64 blockIdx.x + (tid & 63) (rows strided by the four
+// 64-thread groups), YV = (C - sigma I) Q V and U = Q V; summed in chunk order on the host
+// (deterministic).  part: [gridDim.y][kk].
+constexpr int kResidChunks = 16;
+__global__ __launch_bounds__(256) void ritz_resid_kernel(const double* __restrict__ YV, int64_t ldy,
+                                                         const double* __restrict__ U, int64_t ldu,
+                                                         const double* __restrict__ lam, int64_t dim, int kk,
+                                                         double* __restrict__ part) {
+  __shared__ double red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const int64_t r0 = dim * blockIdx.y / gridDim.y, r1 = dim * (blockIdx.y + 1) / gridDim.y;
+  double acc = 0.0;
+  if (col < kk) {
+    const double l = lam[col];
+    for (int64_t r = r0 + g; r < r1; r += 4) {
+      const double d = fma(-l, U[r * ldu + col], YV[r * ldy + col]);
+      acc = fma(d, d, acc);
+    }
+  }
+  red[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && col < kk)
+    part[(int64_t)blockIdx.y * kk + col] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) +
+                                           red[3][threadIdx.x];
+}
+
 static void cvt64to32(hipStream_t s, const double* a, int64_t n, float* b) {
   hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, a, n,
                      b);
@@ -204,6 +245,9 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   EF_TRY(B.get(c, 4, &cinfo));
   double* CW;  // blocked Cholesky + inverse scratch
   EF_TRY(B.get(c, chol_inv_work_elems(m), &CW));
+  double* RP;  // Ritz residual partial sums [kResidChunks][kk]
+  EF_TRY(B.get(c, (size_t)kResidChunks * kk, &RP));
+  std::vector<double> rp((size_t)kResidChunks * kk);
   // Chebyshev recurrence state (EF_OPT_FIT_CHEBYSHEV): Qold = the block before the last
   // orthonormalisation, Wc = the previous filter iterate in the current block's frame
   double *Qold, *Wc;
@@ -315,6 +359,13 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   const bool cheb_on = c->opt_fit_chebyshev != 0;
   int cheb_j = 0;  // recurrence steps since the last restart (Wc valid when > 0)
   const unsigned ew_blocks = (unsigned)std::min<int64_t>((dim * m + 255) / 256, 8192);
+  // Ritz-residual acceptance (see the Rayleigh-Ritz step): a step after an fp64 product is
+  // also converged when every kept pair's |C u - theta u| <= resid_tol * theta_1
+  double resid_tol = fit_resid_tol();
+  bool fit_debug = false;
+#ifdef EF_DIAGNOSTICS
+  fit_debug = getenv("EF_FIT_DEBUG") != nullptr;
+#endif
   int it = 0;
   const int max_iters = (int)std::max<int64_t>(1, std::min<int64_t>(c->opt_fit_max_iters, 1 << 20));
   bool converged = false;
@@ -364,8 +415,31 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       // 0.1467 s, 1e-3 one more iteration; profiles/r04/rr_loose_ab.txt).  The Ritz basis V stays
       // orthogonal to rounding either way (rotations), so the block's span is unchanged.
       EF_TRY(se.solve(c, G, m, lam, V, m, "jacobi(H)", fine ? 1e-12 : have_prev ? rr_loose_tol() : rr_first_tol()));
+      // Ritz residuals |C u_i - theta_i u_i| of the kept pairs after an fp64 product: YV = Y.V
+      // is the continuation product anyway, U = Q.V the result's
+      const bool resid = fine && (resid_tol > 0.0 || fit_debug);
+      if (resid) {
+        EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(V, m, false), dim, m, m, 1.0, Y2, m,
+                             work, kWorkElems, Bt),
+               "Y.V");
+        EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
+                             kk, work, kWorkElems, Bt),
+               "U = Q.V");
+        hipLaunchKernelGGL(ritz_resid_kernel, dim3((unsigned)((kk + 63) / 64), kResidChunks), dim3(256), 0, s, Y2,
+                           (int64_t)m, U_out, (int64_t)kk, lam, dim, kk, RP);
+        EF_HIP(c, hipMemcpyAsync(rp.data(), RP, rp.size() * sizeof(double), hipMemcpyDeviceToHost, s), "D2H resid");
+      }
       EF_HIP(c, hipMemcpyAsync(th.data(), lam, m * sizeof(double), hipMemcpyDeviceToHost, s), "D2H lam");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
+      double resid_max = 1.0;
+      if (resid) {
+        resid_max = 0.0;
+        for (int i = 0; i < kk; ++i) {
+          double a = 0.0;
+          for (int q = 0; q < kResidChunks; ++q) a += rp[(size_t)q * kk + i];
+          resid_max = std::fmax(resid_max, std::sqrt(a));
+        }
+      }
       if (!std::isfinite(th[0])) return set_err(c, EF_E_NUMERIC, "subspace iteration diverged");
       for (int i = 0; i < m; ++i) th[i] += sigma;  // Ritz values of C (H = Q^T (C - sigma I) Q)
       // converged when every kept Ritz value moved by <= 1e-13 relative (floor 1e-15 of
@@ -373,6 +447,8 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       bool ok = have_prev && prev_fine && fine;
       for (int i = 0; i < kk && ok; ++i)
         ok = std::fabs(th[i] - prev[i]) <= std::fmax(1e-13 * std::fabs(th[i]), 1e-15 * std::fabs(th[0]));
+      resid_max /= std::fabs(th[0]);
+      if (resid && resid_tol > 0.0 && resid_max <= resid_tol) ok = true;
       double worst = have_prev ? 0.0 : 1.0;
       int wi = 0;
       for (int i = 0; i < kk && have_prev; ++i) {
@@ -381,8 +457,8 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       }
 #ifdef EF_DIAGNOSTICS
       if (getenv("EF_FIT_DEBUG"))
-        fprintf(stderr, "[ef_fit] rr it=%d %s sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g\n", it,
-                fine ? "fp64" : "fp32", se.sweeps, worst, wi, th[kk - 1], th[m - 1]);
+        fprintf(stderr, "[ef_fit] rr it=%d %s sweeps_total=%ld worst_rel=%.3e at %d theta_k=%.6g theta_m=%.6g resid=%.3e\n",
+                it, fine ? "fp64" : "fp32", se.sweeps, worst, wi, th[kk - 1], th[m - 1], resid ? resid_max : -1.0);
 #else
       (void)wi;
 #endif
@@ -443,17 +519,19 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
       // the iteration cap ends the loop with EF_E_NUMERIC (useless/train.py has no cap:
       // LAPACK either converges or raises LinAlgError; train-v4.py:114-120 returns False)
       if (ok || it == max_iters) {
-        EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
-                             kk, work, kWorkElems, Bt),
-               "U = Q.V");
+        if (!resid)  // (the residual check formed it already)
+          EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, false), Operand::dense(V, m, false), dim, kk, m, 1.0, U_out,
+                               kk, work, kWorkElems, Bt),
+                 "U = Q.V");
         EF_HIP(c, hipMemcpyAsync(lam_out, th.data(), kk * sizeof(double), hipMemcpyHostToDevice, s), "lam");
         EF_HIP(c, hipStreamSynchronize(s), "sync");
         break;
       }
       // continue from the Ritz basis: C.(Q.V) = Y.V (and restart the recurrence there)
-      EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(V, m, false), dim, m, m, 1.0, Y2, m,
-                           work, kWorkElems, Bt),
-             "Y.V");
+      if (!resid)
+        EF_HIP(c, dense_gemm(c, s, Operand::dense(Y, m, false), Operand::dense(V, m, false), dim, m, m, 1.0, Y2, m,
+                             work, kWorkElems, Bt),
+               "Y.V");
       std::swap(Y, Y2);
       restarted = true;
     }
