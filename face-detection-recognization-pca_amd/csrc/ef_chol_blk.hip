@@ -155,10 +155,6 @@ __device__ __forceinline__ void inv_sweep(double (&x)[16], const double (&l)[16]
   (inv_step<Ks>(x, l, rc), ...);
 }
 
-// LDS-only barrier: waits for this wave's LDS operations, not its global stores (which the
-// next kernel reads; __syncthreads would wait for their write-back every block column)
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 }  // namespace
 
 #ifdef EF_CB_STAMP  // phase timing (tools/micro/chol_inv_bench.cpp -DEF_CB_STAMP): s_memtime

@@ -19,6 +19,11 @@ __device__ __forceinline__ double rsq_nr(double x) {
   return fma(0.5 * y, fma(-x * y, y, 1.0), y);
 }
 
+// LDS-only workgroup barrier: waits for this wave's LDS operations (and scalar loads), not
+// for its global stores and atomics, which __syncthreads also waits to complete.  For
+// kernels whose global writes are read only by later launches or the host.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Loader semantics: L(r, c) = trans ? M[c][r] : M[r][c] for the stored row-major M.
 // A operands are read as A(m, k), B operands as B(k, n).  kfast tells the staging loop
 // which tile index is contiguous in memory so global reads coalesce.
