@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 9
 O=gpurun_out/$1
 mkdir -p $O
-R="syrk|gemm_tall|chol_inv|bj_round|transpose_stats|proj_i8|cov_finalize"
+R="syrk|gemm_tall|chol_blk|tri_inv_blk|bj_round|transpose_stats|proj_i8|cov_finalize|gemm_s3"
 timeout -s KILL 300 rocprofv3 --kernel-include-regex "$R" --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $O/pmc_sq -o run -- python tools/prof_fit.py > $O/ps.txt 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --kernel-include-regex "$R" --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python tools/prof_fit.py > $O/pf.txt 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --kernel-include-regex "$R" --pmc TCC_HIT_sum TCC_MISS_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d $O/pmc_l2 -o run -- python tools/prof_fit.py > $O/pl.txt 2>&1 || exit $?
