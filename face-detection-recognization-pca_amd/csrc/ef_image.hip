@@ -39,6 +39,7 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "ef_dma.hpp"
@@ -293,10 +294,69 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 //   * B ring: the band slices of template rows 2p, 2p + 1 (nkb KiB each, lane-linear
 //     fragments) in stage p % 3.
 // One barrier per template-row pair (half the barriers, and half the LDS fragment reads
-// per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).
+// per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).  The wide kernel
+// (MAXNKB 12, one workgroup per CU) software-pipelines the pairs: the last 8 MFMAs of pair
+// p run after the barrier, interleaved with the reads of pair p + 1's fragments, so the
+// LDS round trip after a barrier is hidden under MFMAs (bench frame 0.418 -> 0.397 ms,
+// profiles/r05/tm_pipeline_ab.txt); the narrow kernel (2 workgroups per CU) overlaps one
+// workgroup's barrier with the other's MFMAs instead.
+#ifndef EF_TM_PIPE  // software-pipelined pairs in the wide kernel (variant builds: 0 = off, A/B)
+#define EF_TM_PIPE 1
+#endif
 constexpr int kTmRing = 144;  // A-ring slots (>= 133; 144 * 16 = 0 mod 256 keeps banks aligned)
 constexpr int tm_max_sa(int maxnkb) { return (32 * (maxnkb + 3) + 255) / 256 * 256 + 16; }
 constexpr int tm_lds_bytes(int maxnkb) { return kTmRing * tm_max_sa(maxnkb) + 3 * 2 * maxnkb * 1024 + 1024; }
+
+// The wide kernel's software pipelining (tm_corr_kernel): which fragments the last T MFMAs
+// of a template row use (kb-major sequence, block n on k-block kb - n), the order of the
+// other fragments' reads (ea / eb, -1 = a tail fragment; ne of them), and the (kb, n) of
+// each tail MFMA.
+struct TmTail {
+  bool a[16], b[16];
+  int ea[16], eb[16], ne;
+  int tk[32], tn[32];
+};
+constexpr TmTail tm_tail(int nkb, int t) {
+  TmTail s{};
+  int m = 0;
+  for (int kb = 0; kb < nkb + 3; ++kb)
+    for (int n = 0; n < 4; ++n)
+      if (kb - n >= 0 && kb - n < nkb) {
+        if (m >= 4 * nkb - t) {
+          s.a[kb] = s.b[kb - n] = true;
+          s.tk[m - (4 * nkb - t)] = kb;
+          s.tn[m - (4 * nkb - t)] = n;
+        }
+        ++m;
+      }
+  for (int kb = 0; kb < nkb + 3; ++kb) {  // consumption order: A[kb], then B[kb]
+    s.ea[kb] = s.a[kb] ? -1 : s.ne++;
+    s.eb[kb] = kb < nkb && !s.b[kb] ? s.ne++ : -1;
+  }
+  return s;
+}
+
+// position of MFMA (kb, n) in a template row's kb-major sequence
+constexpr int tm_mfma_index(int nkb, int kb, int n) {
+  int m = 0;
+  for (int k = 0; k < nkb + 3; ++k)
+    for (int q = 0; q < 4; ++q)
+      if (k - q >= 0 && k - q < nkb) {
+        if (k == kb && q == n) return m;
+        ++m;
+      }
+  return m;
+}
+template <int NKB, int T>
+struct TmTailOf {
+  static constexpr TmTail v = tm_tail(NKB, T);
+};
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction (no reliance on
+// the loop unroller: a table lookup left in a rolled loop lands in scratch memory)
+template <typename F, int... I>
+__device__ __forceinline__ void tm_static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
 
 // MAXNKB: the largest k-block count of the launch's pieces (12 for 352-column pieces; the
 // diagnostic build's EF_TM_PIECE = 96 runs MAXNKB = 5, whose 71 KiB of LDS let two
@@ -383,6 +443,117 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
 #else
 #define EF_STAMP(i) do {} while (0)
 #endif
+    if constexpr (EF_TM_PIPE && MAXNKB > 5) {  // (the 2-workgroup narrow kernel overlaps by occupancy)
+    // Software-pipelined pairs: the barrier of pair p sits before its last T MFMAs, and
+    // the fragments of pair p + 1 that those MFMAs do not use are read right after it, so
+    // their LDS round trip runs under the tail instead of the pipe idling between the
+    // barrier and the next pair's first MFMA; the tail's own fragments (the highest A and B
+    // k-blocks, needed last by the next pair) are re-read after it.  One register set.
+    // Stage p % 3 is rewritten by pair p + 3's DMA, issued during pair p + 1 — after this
+    // barrier, by which every wave has completed its reads of stage p (lgkmcnt(0) below).
+    constexpr int NM = 4 * NKB;                             // MFMAs per template row
+#ifndef EF_TM_TAIL  // (variant builds: A/B of the tail length)
+#define EF_TM_TAIL 8
+#endif
+    constexpr int T = NM / 2 < EF_TM_TAIL ? NM / 2 : EF_TM_TAIL;  // MFMAs after the barrier
+    static_assert(T <= 32, "TmTail holds 32 tail MFMAs");
+    using Tail = TmTailOf<NKB, T>;
+    i32x4 A[NKB + 3], B[NKB];
+    // fragment reads of pair p: the tail's (LATE) or the others, in consumption order
+    auto frag_read = [&](int p, auto late_c) {
+      constexpr bool LATE = decltype(late_c)::value;
+      const int j = 2 * p + par;
+      const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+      const uint8_t* bst = smem + kTmRing * kTmMaxSA + (p % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
+      tm_static_for(
+          [&](auto kc) {
+            constexpr int kb = decltype(kc)::value;
+            if constexpr (Tail::v.a[kb] == LATE) A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
+            if constexpr (kb < NKB && Tail::v.b[kb] == LATE) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
+          },
+          std::make_integer_sequence<int, NKB + 3>{});
+    };
+    // MFMAs [LO, HI) of a row's sequence (kb-major; block n uses k-block kb - n).  With
+    // dma, pair p + 2's pieces go between the first NM - T at evenly spaced positions.
+    auto mfmas = [&](auto lo_c, auto hi_c, bool dma, int p) {
+      constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
+      tm_static_for(
+          [&](auto kc) {
+            constexpr int kb = decltype(kc)::value;
+            tm_static_for(
+                [&](auto nc) {
+                  constexpr int n = decltype(nc)::value, m = tm_mfma_index(NKB, kb, n);
+                  if constexpr (kb - n >= 0 && kb - n < NKB && m >= LO && m < HI) {
+                    acc[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - n], acc[n], 0, 0, 0);
+                    tm_static_for(
+                        [&](auto ic) {
+                          constexpr int i = decltype(ic)::value;
+                          if constexpr (m + 1 == (i + 1) * (NM - T) / (Q + 1)) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            if (dma) issue_piece(p + 2, i);
+                            __builtin_amdgcn_sched_barrier(0);
+                          }
+                        },
+                        std::make_integer_sequence<int, Q>{});
+                  }
+                },
+                std::make_integer_sequence<int, 4>{});
+          },
+          std::make_integer_sequence<int, NKB + 3>{});
+    };
+    if (wact && par < J) {
+      frag_read(0, std::false_type{});
+      frag_read(0, std::true_type{});
+    }
+    for (int p = 0; p < NP; ++p) {
+      const bool ahead = p + 2 < NP;
+      const int j = 2 * p + par;
+      const bool act = wact && j < J;
+      if (act)
+        mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, NM - T>{}, ahead, p);
+      else if (ahead)
+        issue(p + 2);
+      __builtin_amdgcn_sched_barrier(0);  // (MFMAs are not memory ops: keep them on their side)
+      EF_STAMP(1);
+      if (ahead)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(Q) : "memory");  // pair p + 1 landed
+      else
+        dma_wait_all();
+      EF_STAMP(2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();  // pair p + 1 visible to every wave; stage p read by every wave
+      __builtin_amdgcn_sched_barrier(0);
+      EF_STAMP(3);
+      if (act) {
+        // pair p + 1's non-tail fragments spread evenly between this pair's tail MFMAs (a
+        // wave whose rows end here reads harmless stale slots it never uses)
+        const int j1 = j + 2;
+        const uint8_t* aslot = smem + ((j1 + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+        const uint8_t* bst =
+            smem + kTmRing * kTmMaxSA + ((p + 1) % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
+        tm_static_for(
+            [&](auto tc) {
+              constexpr int t = decltype(tc)::value;
+              tm_static_for(
+                  [&](auto kc) {
+                    constexpr int kb = decltype(kc)::value;
+                    if constexpr (Tail::v.ea[kb] >= 0 && Tail::v.ea[kb] * T / Tail::v.ne == t)
+                      A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
+                    if constexpr (kb < NKB && Tail::v.eb[kb] >= 0 && Tail::v.eb[kb] * T / Tail::v.ne == t)
+                      B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
+                  },
+                  std::make_integer_sequence<int, NKB + 3>{});
+              __builtin_amdgcn_sched_barrier(0);
+              constexpr int tk = Tail::v.tk[t], tn = Tail::v.tn[t];
+              acc[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[tk], B[tk - tn], acc[tn], 0, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            },
+            std::make_integer_sequence<int, T>{});
+        frag_read(p + 1, std::true_type{});  // the tail's own fragments, needed last by pair p + 1
+      }
+      EF_STAMP(0);  // "issue" = the next pair's reads + this pair's tail MFMAs
+    }
+    } else {
     for (int p = 0; p < NP; ++p) {
       const bool ahead = p + 2 < NP;
       const int j = 2 * p + par;
@@ -426,6 +597,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
       EF_STAMP(2);
       __syncthreads();  // ... for every wave; everyone is done with stage p % 3 and its slots
       EF_STAMP(3);
+    }
     }
 #ifdef EF_TM_STAMP
     if (blockIdx.x % 97 == 0 && lane == 0 && (wave == 0 || wave == 4))
