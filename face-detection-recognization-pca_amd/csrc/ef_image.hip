@@ -130,6 +130,7 @@ struct TmPiece {
 };
 struct TmWork {
   int piece, part, ya, yb, y0, x0;
+  int ncg;  // column groups of the output tile: 1 (128 x 128), 2 (64 x 256) or 4 (32 x 512)
 };
 struct TmStat {
   long long sT, varT;  // sum(T'), N*sum(T'^2) - sum(T')^2
@@ -287,10 +288,14 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 // sums at the end.  Per template row a wave reads NKB + 3 A and NKB B fragments for
 // 4 NKB MFMAs (the band's shift invariance: block n uses k-block kb - n).
 // Operands live in LDS, filled by LDS-DMA one row PAIR per barrier, two pairs ahead:
-//   * A ring: frame rows y0 + ya + q (q = 0 .. J + 126) in slot q % kTmRing, each row the
-//     32 (nkb + 3) bytes the tile reads, slot stride SA = 16 (mod 256) bytes, so the 16
-//     rows a ds_read_b128 lane group touches fall in distinct banks.  Pair p reads slots
-//     2p .. 2p + 128 and prefetches rows 2p + 131, 2p + 132.
+//   * A ring: frame rows y0 + ya + q (q = 0 .. J + WROWS - 2) in slot q mod ring, each row
+//     the 32 (nkb + 3) + 128 (ncg - 1) bytes the tile reads, slot stride SA = 16 (mod 256)
+//     bytes, so the 16 rows a ds_read_b128 lane group touches fall in distinct banks; ring
+//     = the slots of that stride the LDS region holds.  Pair p reads rows 2p .. 2p + WROWS
+//     and prefetches rows 2p + WROWS + 3, 2p + WROWS + 4 (WROWS = the tile's output rows).
+// Tile shapes (TmWork::ncg): 128 x 128, and for a map's last row band with one or two live
+// 32-row blocks 32 x 512 or 64 x 256 — wave pair wr4 then owns column group wr4 & (ncg - 1)
+// of row block wr4 / ncg, so no SIMD idles on dead rows.
 //   * B ring: the band slices of template rows 2p, 2p + 1 (nkb KiB each, lane-linear
 //     fragments) in stage p % 3.
 // One barrier per template-row pair (half the barriers, and half the LDS fragment reads
@@ -377,12 +382,24 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   const TmProblem pb = probs[pc.prob];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr4 = wave & 3, par = wave >> 2;  // 32-row block, template-row parity
+  const int wr4 = wave & 3, par = wave >> 2;  // wave pair (SIMD), template-row parity
   const int r = lane & 31, h = lane >> 5;
   const int nkb = pc.nkb;
-  const int RW = 32 * (nkb + 3);   // A-row bytes a tile reads
+  // tile shape: wave pair wr4 owns 32-row block rb and 128-column group cg
+  const int lc = wk.ncg == 4 ? 2 : wk.ncg == 2 ? 1 : 0;
+  const int rb = wr4 >> lc, cg = wr4 & (wk.ncg - 1);
+  const int WROWS = 32 * (4 >> lc);  // output rows of the tile
+  const int RW = 32 * (nkb + 3) + 128 * (wk.ncg - 1);  // A-row bytes a tile reads
   const int SA = (RW + 255) / 256 * 256 + 16;  // slot stride = 16 (mod 256)
-  const int nl = RW / 16;          // DMA lanes per A row
+  const int nl = RW / 16;          // DMA lanes per A row (<= 54)
+  const int ring = kTmRing * kTmMaxSA / SA;  // A-ring slots (host: >= WROWS + 6)
+  // q mod ring for q < 4 ring (every slot index here is < 260 and ring >= 38)
+  auto wrap = [&](int q) {
+    q -= q >= ring ? ring : 0;
+    q -= q >= ring ? ring : 0;
+    q -= q >= ring ? ring : 0;
+    return q;
+  };
   const int J = wk.yb - wk.ya;
   const int NP = (J + 1) / 2;      // template-row pairs
   const unsigned lds = lds_addr(smem);
@@ -392,7 +409,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   const uint8_t* bsl0 = bands + pc.band_off + (int64_t)wk.ya * nkb * 1024 + 16 * lane;     // + j * nkb KiB
   // Rows >= hr are skipped per wave (uniform); NKB is a compile-time constant so the
   // k-block loop unrolls and every fragment read of a template row is issued up front.
-  const bool wact = wk.y0 + 32 * wr4 < pb.hr;
+  const bool wact = wk.y0 + 32 * rb < pb.hr && wk.x0 + 128 * cg < pb.wr;
   i32x16 acc[4] = {};
   auto run = [&](auto nkb_c) {
     constexpr int NKB = decltype(nkb_c)::value;
@@ -412,9 +429,9 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
         else
           glds16(bsl0, ldsD);
       } else if (pi < NPC) {
-        const int q = 2 * p + 127 + (pi - 2 * NKB);
-        if (q < J + 127) {
-          if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)((q % kTmRing) * SA));
+        const int q = 2 * p + WROWS - 1 + (pi - 2 * NKB);
+        if (q < J + WROWS - 1) {
+          if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)(wrap(q) * SA));
         } else {
           glds16(bsl0, ldsD);
         }
@@ -426,7 +443,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
 #pragma unroll
       for (int i = 0; i < Q; ++i) issue_piece(p, i);
     };
-    for (int q = wave; q < 127; q += 8)
+    for (int q = wave; q < WROWS - 1; q += 8)
       if (lane < nl) glds16(arow0 + (int64_t)q * pitch, lds + (unsigned)(q * SA));
     issue(0);
     if (NP > 1) {
@@ -463,7 +480,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
     auto frag_read = [&](int p, auto late_c) {
       constexpr bool LATE = decltype(late_c)::value;
       const int j = 2 * p + par;
-      const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+      const uint8_t* aslot = smem + wrap(j + 32 * rb + r) * SA + 16 * h + 128 * cg;
       const uint8_t* bst = smem + kTmRing * kTmMaxSA + (p % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
       tm_static_for(
           [&](auto kc) {
@@ -528,7 +545,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
         // pair p + 1's non-tail fragments spread evenly between this pair's tail MFMAs (a
         // wave whose rows end here reads harmless stale slots it never uses)
         const int j1 = j + 2;
-        const uint8_t* aslot = smem + ((j1 + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+        const uint8_t* aslot = smem + wrap(j1 + 32 * rb + r) * SA + 16 * h + 128 * cg;
         const uint8_t* bst =
             smem + kTmRing * kTmMaxSA + ((p + 1) % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
         tm_static_for(
@@ -559,7 +576,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
       const int j = 2 * p + par;
       EF_STAMP(0);
       if (wact && j < J) {
-        const uint8_t* aslot = smem + ((j + 32 * wr4 + r) % kTmRing) * SA + 16 * h;
+        const uint8_t* aslot = smem + wrap(j + 32 * rb + r) * SA + 16 * h + 128 * cg;
         const uint8_t* bst = smem + kTmRing * kTmMaxSA + (p % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
         i32x4 A[NKB + 3], B[NKB];
 #pragma unroll
@@ -631,11 +648,11 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   int* out = parts + pb.part_off + (int64_t)wk.part * pb.hr * pb.wr;
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
-    const int x = wk.x0 + 32 * n + r;
+    const int x = wk.x0 + 128 * cg + 32 * n + r;
     if (x >= pb.wr) continue;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
-      const int y = wk.y0 + 32 * wr4 + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const int y = wk.y0 + 32 * rb + (g & 3) + 8 * (g >> 2) + 4 * h;
       if (y < pb.hr) out[(int64_t)y * pb.wr + x] = acc[n][g] + red[(n * 16 + g) * 64 + lane];
     }
   }
@@ -700,8 +717,18 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
         const int64_t a = a0 + x + 256 * u, b = b0 + x + 256 * u;
         T d1 = 0, d2 = 0;
         if (u == 0 || two) {
-          d1 = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
-          d2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
+          if constexpr (std::is_same<T, unsigned>::value) {
+            // 32-bit byte offsets from the uniform base (the images hold < 2^30 entries):
+            // base + zext(offset) addressing instead of 64-bit address arithmetic per load
+            auto ld = [](const unsigned* p, int64_t e) {
+              return *reinterpret_cast<const unsigned*>(reinterpret_cast<const char*>(p) + (uint32_t)e * 4u);
+            };
+            d1 = ld(ii1, b + pb.tw) - ld(ii1, a + pb.tw) - ld(ii1, b) + ld(ii1, a);
+            d2 = ld(ii2, b + pb.tw) - ld(ii2, a + pb.tw) - ld(ii2, b) + ld(ii2, a);
+          } else {
+            d1 = ii1[b + pb.tw] - ii1[a + pb.tw] - ii1[b] + ii1[a];
+            d2 = ii2[b + pb.tw] - ii2[a + pb.tw] - ii2[b] + ii2[a];
+          }
         }
         // uint32: d1 is the two's-complement window sum, d2 the (non-negative) one
         sI[u] = std::is_same<T, long long>::value ? (long long)d1 : (long long)(int)d1;
@@ -711,7 +738,18 @@ __global__ __launch_bounds__(256) void tm_score_kernel(const TmProblem* __restri
       for (int u = 0; u < 2; ++u) {
         if (u == 1 && !two) break;
         const int64_t i = row + x + 256 * u;
-        const float v = tm_score(n * P[u] - ts.sT * sI[u], n * sI2[u] - sI[u] * sI[u], ts.varT, sqT);
+        long long numN, varI;
+        if constexpr (std::is_same<T, unsigned>::value) {
+          // every template area < 2^18: |sI|, |sT| <= 128 n < 2^25 and sI2 <= 16384 n < 2^32,
+          // so the window terms are 32 x 32 -> 64-bit products (n * P keeps a 64-bit P)
+          const int n32 = (int)n, sI32 = (int)sI[u], sT32 = (int)ts.sT;
+          numN = (long long)n32 * P[u] - (long long)sT32 * sI32;
+          varI = (long long)((unsigned long long)(unsigned)n32 * (unsigned)sI2[u]) - (long long)sI32 * sI32;
+        } else {
+          numN = n * P[u] - ts.sT * sI[u];
+          varI = n * sI2[u] - sI[u] * sI[u];
+        }
+        const float v = tm_score(numN, varI, ts.varT, sqT);
         if (maps) maps[pb.map_off + i] = v;
         const unsigned long long k = tm_key(v, (unsigned)i);
         key = k < key ? k : key;
@@ -754,6 +792,21 @@ void tm_release(ef_ctx* c) {
 }
 
 static int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// Column groups of a tile whose row band has nrb live 32-row blocks: 4 (32 x 512) for one,
+// 2 (64 x 256) for two, when the kernel's A ring holds that shape's window (WROWS + 6
+// slots at its wider slot stride; tm_corr_kernel), else 1 (128 x 128).
+static int tm_tile_groups(int nrb, int nkb, int maxnkb) {
+  for (int g = nrb == 1 ? 4 : nrb == 2 ? 2 : 1; g > 1; g >>= 1) {
+    const int rw = 32 * (nkb + 3) + 128 * (g - 1);
+    const int sa = (rw + 255) / 256 * 256 + 16;
+    const int ring = kTmRing * tm_max_sa(maxnkb) / sa;
+    // window + prefetch, and the kernel's wrap() (three conditional subtracts) covers every
+    // slot index (< 128 template rows + the tile's rows + 6)
+    if (ring >= 32 * (4 / g) + 6 && 4 * ring > 128 + 32 * (4 / g) + 6 && rw <= 1024) return g;
+  }
+  return 1;
+}
 
 }  // namespace ef
 
@@ -827,7 +880,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
   t->H = frame_h;
   t->W = frame_w;
   t->nprob = n_problems;
-  t->pitch = rup((int64_t)frame_w + 256, 64);
+  t->pitch = rup((int64_t)frame_w + 640, 64);  // a 512-column tile's rows read past the frame
   t->ii64 = c->opt_tm_int64 != 0;
   const bool dev = flags & EF_MEM_DEVICE;
 
@@ -878,14 +931,27 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
       t->max_nkb = std::max(t->max_nkb, pc.nkb);
       pc.band_off = band_bytes;
       band_bytes += (int64_t)th * pc.nkb * 1024;
-      const int pi = (int)pieces.size();
       pieces.push_back(pc);
-      for (int ch = 0; ch < nchunk; ++ch)
-        for (int y0 = 0; y0 < pb.hr; y0 += kTmTile)
-          for (int x0 = 0; x0 < pb.wr; x0 += kTmTile)
-            works.push_back(TmWork{pi, ch * npiece + q, ch * kTmChunk, std::min(th, (ch + 1) * kTmChunk), y0, x0});
     }
     t->probs.push_back(pb);
+  }
+  // work items, once the launch's kernel (narrow or wide A ring) is known
+  const int kmax = t->max_nkb <= 5 ? 5 : 12;
+  for (int pi = 0; pi < (int)pieces.size(); ++pi) {
+    const TmPiece& pc = pieces[pi];
+    const TmProblem& pb = t->probs[pc.prob];
+    const int npiece = (pb.tw + piece_w - 1) / piece_w, nchunk = (pb.th + kTmChunk - 1) / kTmChunk;
+    const int q = pc.px / piece_w;
+    for (int ch = 0; ch < nchunk; ++ch)
+      for (int y0 = 0; y0 < pb.hr; y0 += kTmTile) {
+        // the map's last row band: with one or two live 32-row blocks the tile turns into
+        // 32 x 512 or 64 x 256 (4 or 2 column groups), so its waves are not left idle
+        const int nrb = std::min(4, (pb.hr - y0 + 31) / 32);
+        const int ncg = tm_tile_groups(nrb, pc.nkb, kmax);
+        for (int x0 = 0; x0 < pb.wr; x0 += kTmTile * ncg)
+          works.push_back(
+              TmWork{pi, ch * npiece + q, ch * kTmChunk, std::min(pb.th, (ch + 1) * kTmChunk), y0, x0, ncg});
+      }
   }
   // longest work items first (template rows x k-blocks), so the short ones fill the tail
   std::stable_sort(works.begin(), works.end(), [&](const TmWork& a, const TmWork& b) {

@@ -62,6 +62,9 @@ CASES = [  # frame (H, W), template (h, w)
     ((33, 33), (33, 33)),       # 1 x 1 result
     ((200, 300), (40, 130)),    # widest 5-k-block piece: the 71 KiB correlation kernel
     ((200, 300), (40, 131)),    # narrowest 6-k-block piece: the 148 KiB kernel
+    ((160, 600), (140, 40)),    # one live row block: 32 x 512 tiles, narrow kernel
+    ((160, 640), (135, 200)),   # one live row block: 32 x 512 tiles, 148 KiB kernel
+    ((200, 600), (150, 180)),   # two live row blocks: 64 x 256 tiles, 148 KiB kernel
 ]
 
 
