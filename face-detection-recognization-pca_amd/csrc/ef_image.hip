@@ -281,10 +281,11 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
   }
 }
 
-// One workgroup = one work item: a 128 x 128 output tile of one problem, template rows
-// [ya, ya + J) of one column piece.  8 waves (2 per SIMD): wave w owns output rows
-// y0 + 32 (w & 3) + [0, 32) and all four 32-column blocks, and the template rows of parity
-// w >> 2 — the two waves of a row block split the template rows and add their partial
+// One workgroup = one work item: an output tile of one problem (128 x 128, or 64 x 256 /
+// 32 x 512 — below), template rows [ya, ya + J) of one column piece.  8 waves (2 per SIMD):
+// wave w owns 32 output rows x the four 32-column blocks of one 128-column group (for the
+// 128 x 128 tile: rows y0 + 32 (w & 3) + [0, 32), all 128 columns), and the template rows of
+// parity w >> 2 — the two waves of a SIMD split the template rows and add their partial
 // sums at the end.  Per template row a wave reads NKB + 3 A and NKB B fragments for
 // 4 NKB MFMAs (the band's shift invariance: block n uses k-block kb - n).
 // Operands live in LDS, filled by LDS-DMA one row PAIR per barrier, two pairs ahead:
@@ -293,11 +294,12 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 //     bytes, so the 16 rows a ds_read_b128 lane group touches fall in distinct banks; ring
 //     = the slots of that stride the LDS region holds.  Pair p reads rows 2p .. 2p + WROWS
 //     and prefetches rows 2p + WROWS + 3, 2p + WROWS + 4 (WROWS = the tile's output rows).
-// Tile shapes (TmWork::ncg): 128 x 128, and for a map's last row band with one or two live
-// 32-row blocks 32 x 512 or 64 x 256 — wave pair wr4 then owns column group wr4 & (ncg - 1)
-// of row block wr4 / ncg, so no SIMD idles on dead rows.
 //   * B ring: the band slices of template rows 2p, 2p + 1 (nkb KiB each, lane-linear
 //     fragments) in stage p % 3.
+// Tile shapes (TmWork::ncg): 128 x 128, and for a map's last row band with one or two live
+// 32-row blocks 32 x 512 or 64 x 256 — wave pair wr4 then owns column group wr4 & (ncg - 1)
+// of row block wr4 / ncg, so no SIMD idles on dead rows (0.397 -> 0.383 ms per bench frame,
+// profiles/r05/tm_tile_shape_ab.txt).
 // One barrier per template-row pair (half the barriers, and half the LDS fragment reads
 // per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).  The wide kernel
 // (MAXNKB 12, one workgroup per CU) software-pipelines the pairs: the last 8 MFMAs of pair
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   const int SA = (RW + 255) / 256 * 256 + 16;  // slot stride = 16 (mod 256)
   const int nl = RW / 16;          // DMA lanes per A row (<= 54)
   const int ring = kTmRing * kTmMaxSA / SA;  // A-ring slots (host: >= WROWS + 6)
-  // q mod ring for q < 4 ring (every slot index here is < 260 and ring >= 38)
+  // q mod ring for q < 4 ring (tm_tile_groups: 4 ring > J + WROWS + 6 > every slot index)
   auto wrap = [&](int q) {
     q -= q >= ring ? ring : 0;
     q -= q >= ring ? ring : 0;
@@ -407,8 +409,8 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   const unsigned ldsD = ldsB + (unsigned)(3 * kTmBStage);  // dummy DMA target
   const int8_t* arow0 = f8 + (int64_t)(wk.y0 + wk.ya) * pitch + wk.x0 + pc.px + 16 * lane;  // + q * pitch
   const uint8_t* bsl0 = bands + pc.band_off + (int64_t)wk.ya * nkb * 1024 + 16 * lane;     // + j * nkb KiB
-  // Rows >= hr are skipped per wave (uniform); NKB is a compile-time constant so the
-  // k-block loop unrolls and every fragment read of a template row is issued up front.
+  // Row blocks past hr and column groups past wr are skipped per wave (uniform); NKB is a
+  // compile-time constant so the k-block loop unrolls and the fragment reads are static.
   const bool wact = wk.y0 + 32 * rb < pb.hr && wk.x0 + 128 * cg < pb.wr;
   i32x16 acc[4] = {};
   auto run = [&](auto nkb_c) {
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
     constexpr int NPC = 2 * NKB + 2;       // DMA pieces per pair: 2 NKB band slices + 2 A rows
     constexpr int Q = (NPC + 7) / 8;       // DMA instructions per wave per pair
     // Pair p's operands: band slices of rows 2p, 2p+1 into stage p % 3 and A rows
-    // q = 2p + 127, 2p + 128 (completing the windows of rows 2p, 2p + 1); wave w issues
+    // q = 2p + WROWS - 1, 2p + WROWS (completing the windows of rows 2p, 2p + 1); wave w issues
     // pieces w, w + 8, ..., padded with harmless dummy DMAs to exactly Q instructions, so
     // "pair p landed" is a vmcnt of Q x (pairs issued after it).
     auto issue_piece = [&](int p, int i) {
