@@ -65,6 +65,8 @@ CASES = [  # frame (H, W), template (h, w)
     ((160, 600), (140, 40)),    # one live row block: 32 x 512 tiles, narrow kernel
     ((160, 640), (135, 200)),   # one live row block: 32 x 512 tiles, 148 KiB kernel
     ((200, 600), (150, 180)),   # two live row blocks: 64 x 256 tiles, 148 KiB kernel
+    ((100, 640), (80, 400)),    # 32 x 512 tiles over two column pieces
+    ((150, 700), (100, 360)),   # 64 x 256 tiles over two column pieces
 ]
 
 
@@ -84,6 +86,38 @@ def test_match_template_map_bit_exact(eng, fs, ts):
         assert (best[p], xs[p], ys[p]) == (np.float32(v), mx, my)
     if ts != (1, 1):
         assert (xs[0], ys[0]) == (x, y)
+
+
+def _random_case(seed):
+    """A random (frame, template) shape whose oracle map costs <= ~5e8 multiply-adds:
+    covers both correlation kernels, all three tile shapes (the last row band's live 32-row
+    blocks), column pieces (> 352 template columns) and row chunks (> 128 template rows)."""
+    rng = np.random.default_rng(1000 + seed)
+    while True:
+        H, W = int(rng.integers(24, 300)), int(rng.integers(40, 700))
+        h, w = int(rng.integers(1, H + 1)), int(rng.integers(1, min(W, 420) + 1))
+        if (H - h + 1) * (W - w + 1) * h * w <= 5e8:
+            return rng, (H, W), (h, w)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_match_template_random_shapes(eng, seed):
+    """Random shapes, maps bit-exact to the oracle and the first raster-order maximum —
+    with and without the map output (the keys-only path scores without writing maps)."""
+    rng, fs, ts = _random_case(seed)
+    frame = rng.integers(0, 256, fs, dtype=np.uint8)
+    y, x = rng.integers(0, fs[0] - ts[0] + 1), rng.integers(0, fs[1] - ts[1] + 1)
+    t = frame[y:y + ts[0], x:x + ts[1]].copy()
+    other = rng.integers(0, 256, ts, dtype=np.uint8)
+    eng.tm_prepare([t, other], [(0,) + ts, (1,) + ts], fs)
+    best, xs, ys, maps = eng.tm_match(frame, maps=True)
+    best2, xs2, ys2, _ = eng.tm_match(frame)
+    for p, tt in enumerate((t, other)):
+        R = io.match_template_ccoeff_normed(frame, tt)
+        np.testing.assert_array_equal(maps[p], R)
+        v, (mx, my) = io.min_max_loc_max(R)
+        assert (best[p], xs[p], ys[p]) == (np.float32(v), mx, my)
+        assert (best2[p], xs2[p], ys2[p]) == (best[p], xs[p], ys[p])
 
 
 def test_match_template_extreme_pixels_and_flat(eng):
