@@ -111,7 +111,7 @@ def test_match_template_random_shapes(eng, seed):
     other = rng.integers(0, 256, ts, dtype=np.uint8)
     eng.tm_prepare([t, other], [(0,) + ts, (1,) + ts], fs)
     best, xs, ys, maps = eng.tm_match(frame, maps=True)
-    best2, xs2, ys2, _ = eng.tm_match(frame)
+    best2, xs2, ys2 = eng.tm_match(frame)
     for p, tt in enumerate((t, other)):
         R = io.match_template_ccoeff_normed(frame, tt)
         np.testing.assert_array_equal(maps[p], R)
