@@ -89,18 +89,18 @@ def test_match_template_map_bit_exact(eng, fs, ts):
 
 
 def _random_case(seed):
-    """A random (frame, template) shape whose oracle map costs <= ~5e8 multiply-adds:
+    """A random (frame, template) shape whose oracle map costs <= ~1e9 multiply-adds:
     covers both correlation kernels, all three tile shapes (the last row band's live 32-row
     blocks), column pieces (> 352 template columns) and row chunks (> 128 template rows)."""
     rng = np.random.default_rng(1000 + seed)
     while True:
-        H, W = int(rng.integers(24, 300)), int(rng.integers(40, 700))
-        h, w = int(rng.integers(1, H + 1)), int(rng.integers(1, min(W, 420) + 1))
-        if (H - h + 1) * (W - w + 1) * h * w <= 5e8:
+        H, W = int(rng.integers(24, 300)), int(rng.integers(40, 720))
+        h, w = int(rng.integers(1, H + 1)), int(rng.integers(1, min(W, 480) + 1))
+        if (H - h + 1) * (W - w + 1) * h * w <= 1e9:
             return rng, (H, W), (h, w)
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(40))
 def test_match_template_random_shapes(eng, seed):
     """Random shapes, maps bit-exact to the oracle and the first raster-order maximum —
     with and without the map output (the keys-only path scores without writing maps)."""
