@@ -664,6 +664,13 @@ def _face_jpegs(n, sides, seed=11):
     return out
 
 
+def _host_threads():
+    """The library's host worker count: the job's CPU share (OMP_NUM_THREADS, else the
+    affinity mask), capped at 16 (Engine sets EF_OPT_HOST_THREADS from the same rule)."""
+    from eigenface.engine import host_cpu_share
+    return host_cpu_share()
+
+
 def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
     """JPEG files -> grey 64x64 rows (ef_jpeg_ingest into a device tensor): a stream of
     `reps` batches, each call returning once queued, so batch i+1's host marker parse +
@@ -686,10 +693,13 @@ def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
     assert (st == 0).all()
     k_ms, k_n = eng.timing_get("jpeg")
     kdt = k_ms / reps * 1e-3  # device decode time per batch (the ingest decodes it in parts)
+    h_ms, h_n = eng.timing_get("jpeg_host")  # host staging (parse, destuff, tables) per part
     res = {"config": f"{n} JPEG face crops {min(sides)}-{max(sides)} px (q95 4:2:0, {nbytes / n / 1024:.1f} KiB avg)"
                      " -> decode -> grey 64x64, rows on the device",
            "faces_per_s": round(n / wall, 1), "ms_per_batch": round(wall * 1e3, 3),
            "decode_ms_device": round(kdt * 1e3, 3), "decode_launches_per_batch": round(k_n / reps, 2),
+           "host_parse_ms": round(h_ms / reps, 3), "host_parts_per_batch": round(h_n / reps, 2),
+           "host_threads": _host_threads(),
            "file_MBs": round(nbytes / wall / 1e6, 1)}
     if with_cpu:
         import io as _io

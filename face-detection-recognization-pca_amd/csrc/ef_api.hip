@@ -13,6 +13,8 @@
 
 #include "ef_internal.hpp"
 
+#include <atomic>
+
 namespace ef {
 
 int set_err(ef_ctx* c, int code, const std::string& msg) {
@@ -202,7 +204,8 @@ static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t b
   }
   int64_t pps = 0;
   const uint8_t* mu8 = c->mean_u8_ok ? static_cast<const uint8_t*>(c->mean_u8.p) : nullptr;
-  const int ns = c->bf16 ? project_bf16_nsplit(dtype, P, mu8, bpad, c->d, c->kpw, &pps)
+  const void* wf = c->w16f_ok ? c->W16f.p : nullptr;
+  const int ns = c->bf16 ? project_bf16_nsplit(dtype, P, mu8, wf, bpad, c->d, c->kpw, &pps)
                          : project_nsplit(bpad, c->d, c->kpw, &pps);
   EF_TRY(ensure(c, c->proj_part, (size_t)ns * bpad * c->kpw * sizeof(float)));
   TimerEvt t;
@@ -210,7 +213,7 @@ static int project_dev(ef_ctx* c, const void* P, int dtype, int64_t b, int64_t b
   if (c->bf16) {
     EF_HIP(c,
            launch_project_bf16(c->stream, dtype, P, b, bpad, c->d, static_cast<const float*>(c->mean_r.p),
-                               mu8, static_cast<const unsigned short*>(c->W16.p),
+                               mu8, static_cast<const unsigned short*>(c->W16.p), wf,
                                c->kpw,
                                static_cast<float*>(c->proj_part.p), ns, pps),
            "project kernel (bf16)");
@@ -318,13 +321,25 @@ class HostPool {
 };
 }  // namespace
 
+// Host worker count (EF_OPT_HOST_THREADS, process-wide): the job's CPU share.  The machine's
+// hardware_concurrency() is the wrong size on a shared host (256 on the GPU pool's boxes,
+// whose one-GPU jobs get 16 CPUs), so the default is min(16, hardware threads) and the
+// Python layer sets the share it sees (OMP_NUM_THREADS, else the affinity mask).
+static std::atomic<int> g_host_threads{0};
+int host_threads() {
+  const int v = g_host_threads.load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
 void host_parallel(int n, const std::function<void(int)>& fn) {
   if (n <= 1) {
     if (n == 1) fn(0);
     return;
   }
   // never destroyed: the workers block on the condition variable until the process exits
-  static HostPool* pool = new HostPool((int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()) - 1));
+  // (sized on first use; the caller takes tasks too, so n tasks always finish)
+  static HostPool* pool = new HostPool(std::max(0, std::min(host_threads(), 64) - 1));
   pool->run(n, fn);
 }
 
@@ -404,7 +419,7 @@ void ef_destroy(ef_ctx* c) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
-  DevBuf* bufs[] = {&c->mean,      &c->W,         &c->W16,       &c->mean_r,    &c->mean_u8, &c->corr,
+  DevBuf* bufs[] = {&c->mean,      &c->W,         &c->W16,       &c->W16f,      &c->mean_r,    &c->mean_u8, &c->corr,
                     &c->G,         &c->G3,        &c->q3,        &c->gnorm2,    &c->ginv,    &c->gmax2,
                     &c->q_pad,     &c->keys,      &c->search_ws, &c->p_stage,   &c->proj_part,
                     &c->feats_dev, &c->jpeg_ws,   &c->jpeg_out,  &c->jpeg_rows, &c->jpeg_up[0], &c->jpeg_up[1]};
@@ -522,6 +537,14 @@ int ef_model_set(ef_ctx* c, const float* mean, const float* W, int64_t d, int32_
     release(cp);
     if (e != hipSuccess) return hip_err(c, e, "bf16 model");
     c->mean_u8_ok = bad == 0;
+    c->w16f_ok = false;
+    if (bf16_frag_supported(d, ldw)) {
+      EF_TRY(ensure(c, c->W16f, (size_t)ldw * d * sizeof(unsigned short)));
+      EF_HIP(c, launch_bf16_frag(c->stream, static_cast<const unsigned short*>(c->W16.p), d, ldw, c->W16f.p),
+             "bf16 fragment model");
+      EF_HIP(c, hipStreamSynchronize(c->stream), "sync");
+      c->w16f_ok = true;
+    }
   }
   c->bf16 = bf16;
   c->d = d;
@@ -745,6 +768,10 @@ int ef_set_option(ef_ctx* c, int32_t option, int64_t value) {
       if (value < 0 || value > 3) return set_err(c, EF_E_INVALID, "EF_OPT_SEARCH_SPLIT_BF16 must be 0, 1, 2 or 3");
       c->opt_search_split_bf16 = value;
       return EF_OK;
+    case EF_OPT_HOST_THREADS:
+      if (value < 0 || value > 256) return set_err(c, EF_E_INVALID, "EF_OPT_HOST_THREADS must be 0..256");
+      g_host_threads.store((int)value, std::memory_order_relaxed);
+      return EF_OK;
     default:
       return set_err(c, EF_E_INVALID, "ef_set_option: unknown option " + std::to_string(option));
   }
@@ -762,6 +789,7 @@ int ef_get_option(const ef_ctx* c, int32_t option, int64_t* value) {
     case EF_OPT_SEARCH_SPLIT_BF16: *value = c->opt_search_split_bf16; return EF_OK;
     case EF_OPT_JPEG_PART_FILES: *value = c->opt_jpeg_part_files; return EF_OK;
     case EF_OPT_FIT_CHEBYSHEV: *value = c->opt_fit_chebyshev; return EF_OK;
+    case EF_OPT_HOST_THREADS: *value = host_threads(); return EF_OK;
     default: return EF_E_INVALID;
   }
 }

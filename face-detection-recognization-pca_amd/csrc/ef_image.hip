@@ -866,6 +866,17 @@ int ef_preprocess(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const 
   return EF_OK;
 }
 
+// Width of the integral images (host-only, API v7).  uint32 (wrapping) sums need every
+// template area < 2^18 (window sums of I'^2 <= 16384 * area < 2^32) AND fewer than 2^30
+// integral entries, (H + 1)(W + 1): tm_score_kernel<unsigned> forms byte offsets as
+// uint32(entry) * 4 (a 32k x 32k frame wrapped them).  Otherwise int64.
+int ef_tm_sums_bits(int32_t frame_h, int32_t frame_w, int64_t max_template_area) {
+  if (frame_h <= 0 || frame_w <= 0 || max_template_area < 0) return EF_E_INVALID;
+  if (max_template_area >= (int64_t)1 << 18) return 64;
+  if ((int64_t)(frame_h + 1) * (int64_t)(frame_w + 1) >= (int64_t)1 << 30) return 64;
+  return 32;
+}
+
 int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_offsets, const int32_t* templ_h,
                   const int32_t* templ_w, int32_t n_templates, const int32_t* prob_templ, const int32_t* prob_h,
                   const int32_t* prob_w, int32_t n_problems, int32_t frame_h, int32_t frame_w, uint32_t flags) {
@@ -884,6 +895,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
   t->nprob = n_problems;
   t->pitch = rup((int64_t)frame_w + 640, 64);  // a 512-column tile's rows read past the frame
   t->ii64 = c->opt_tm_int64 != 0;
+  if (ef_tm_sums_bits(frame_h, frame_w, 1) == 64) t->ii64 = true;  // frame-size rule alone
   const bool dev = flags & EF_MEM_DEVICE;
 
   int64_t raw_bytes = 0;
@@ -923,7 +935,7 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
     map_total += (int64_t)pb.hr * pb.wr;
     max_pos = std::max<int64_t>(max_pos, (int64_t)pb.hr * pb.wr);
     max_h = std::max(max_h, th);
-    if ((int64_t)th * tw >= (int64_t)1 << 18) t->ii64 = true;
+    if (ef_tm_sums_bits(frame_h, frame_w, (int64_t)th * tw) == 64) t->ii64 = true;
     for (int q = 0; q < npiece; ++q) {
       TmPiece pc{};
       pc.prob = p;

@@ -103,6 +103,8 @@ struct ef_ctx {
   ef::DevBuf W;     // float[d][kpw]
   bool bf16 = false;   // EF_MODEL_BF16: project with W16 on bf16 MFMA
   ef::DevBuf W16;      // bf16[kpw][d]
+  ef::DevBuf W16f;     // W16 in MFMA-fragment order (frag-form projection), when supported
+  bool w16f_ok = false;
   ef::DevBuf mean_r;   // float[d] round(mean)
   ef::DevBuf mean_u8;  // uint8[d] round(mean) (wide bf16 kernel) + int counter
   bool mean_u8_ok = false;  // every round(mean) in 0..255
@@ -210,6 +212,7 @@ hipError_t allow_dynamic_lds(const void* fn, int bytes);
 // Jobs from concurrent callers run one at a time.  Spawning threads per call cost ~1-2 ms
 // per 16 threads in the sandboxed containers, as much as the host work it split.
 void host_parallel(int n, const std::function<void(int)>& fn);
+int host_threads();  // EF_OPT_HOST_THREADS (the job's CPU share)
 // all-gather over the attached communicator on ctx->stream (bytes per rank)
 int comm_allgather(ef_ctx* c, const void* send, void* recv, size_t bytes_per_rank);
 hipError_t launch_pad_rows(hipStream_t s, const float* src, int64_t rows, int k, int64_t rows_pad,
@@ -227,11 +230,14 @@ hipError_t launch_project_reduce(hipStream_t s, const float* part, int nsplit, i
 // bf16 model (EF_MODEL_BF16): W16 [kpw][d] bf16, round(mean), fp64-derived correction row
 hipError_t launch_bf16_model(hipStream_t s, const float* W, const float* mean, int64_t d, int ldw,
                              unsigned short* Wt16, float* mean_r, float* corr, double* corr_part, int nchunk);
-int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int64_t bpad, int64_t d, int ldw,
-                        int64_t* pix_per_split);
+int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, const void* Wf, int64_t bpad, int64_t d,
+                        int ldw, int64_t* pix_per_split);
 hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_t b, int64_t bpad, int64_t d,
-                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16, int ldw,
-                               float* part, int nsplit, int64_t pps);
+                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16,
+                               const void* Wf, int ldw, float* part, int nsplit, int64_t pps);
+// fragment-native copy of W16 for the frag-form projection (d % 64 == 0, ldw % 128 == 0)
+bool bf16_frag_supported(int64_t d, int ldw);
+hipError_t launch_bf16_frag(hipStream_t s, const unsigned short* Wt16, int64_t d, int ldw, void* Wf);
 hipError_t launch_mean_u8(hipStream_t s, const float* mean_r, int64_t d, uint8_t* out, int* bad);
 
 }  // namespace ef

@@ -1382,8 +1382,7 @@ void build_batch(const uint8_t* data, const int64_t* offsets, const int64_t* siz
     int st = 0, seg_beg = 0, seg_end = 0;
   };
   std::vector<FileRes> R((size_t)std::max(count, 0));
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int nt = count >= 512 ? (int)std::min<unsigned>(16u, hw) : 1;
+  const int nt = count >= 512 ? host_threads() : 1;
   std::vector<Tables> TT(nt);
   std::vector<std::vector<JSeg>> SS(nt);
   auto work = [&](int t, int a, int e) {
@@ -1489,8 +1488,7 @@ void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t*
     }
   };
   const int64_t bytes = B.words * 4;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t nt = bytes < ((int64_t)4 << 20) ? 1 : std::min<size_t>({16, hw, n});
+  const size_t nt = bytes < ((int64_t)4 << 20) ? 1 : std::min<size_t>((size_t)host_threads(), n);
   host_parallel((int)nt, [&](int t) { work(n * t / nt, n * (t + 1) / nt); });
 }
 
@@ -1840,10 +1838,16 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     std::vector<int32_t> st;
     int rc = EF_OK;
     std::string err;
+    double host_ms = 0.0;  // wall time of prepare() (EF_KERNEL_JPEG_HOST)
   };
   int64_t call_chunk_bits = 0;
   auto prepare = [&](Part& P) {
     (void)hipSetDevice(c->device);  // a fresh host thread starts on device 0
+    struct Stamp {  // every return path records the part's host time
+      Part& P;
+      std::chrono::steady_clock::time_point t0;
+      ~Stamp() { P.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } stamp{P, std::chrono::steady_clock::now()};
     StageTimer tm;
     P.st.assign(P.m, 0);
     build_batch(data, offsets + P.a, sizes + P.a, P.m, mode, nullptr, P.st.data(), P.B);
@@ -1890,6 +1894,10 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       if (next.joinable()) next.join();  // before any return: the thread uses parts[i + 1]
       if (rc != EF_OK) return rc;
       if (status) std::memcpy(status + P.a, P.st.data(), (size_t)P.m * 4);
+      if (c->timing) {  // host staging time of this part (recorded on the calling thread)
+        c->t_ms[EF_KERNEL_JPEG_HOST] += P.host_ms;
+        c->t_n[EF_KERNEL_JPEG_HOST] += 1;
+      }
       P.B = Batch();  // release the part's host tables
     }
     if (!(flags & EF_MEM_DEVICE)) {

@@ -308,6 +308,189 @@ __global__ __launch_bounds__(512, 1) void project_bf16_wide_kernel(const uint8_t
       }
 }
 
+// ---------------------------------------------------------------------------------
+// Fragment form (round 6): the wide kernel above staged BOTH operands
+// through LDS.  Per 32x32x16 MFMA a wave read 768 B of fragments from LDS (2 A + 4 B per
+// 8 MFMAs), which with the W16 and pixel stores kept the LDS busy ~1,900 of the 2,048
+// MFMA cycles of a stage (MFMA busy 41 %), and each probe tile was read by two column tiles.
+// Here W16 is kept in MFMA-fragment-native order (`Wf`, built once per model by
+// bf16_frag_kernel): the 16 B a lane needs for one B fragment sit at ((ct * KB + kb) * 64
+// + lane) * 16 B, so a wave's fragment is ONE contiguous 1 KiB global_load_dwordx4 straight
+// into VGPRs, with no LDS round trip, prefetched four k-steps ahead in a register ring.
+// Only the probes go through LDS (they need the p - round(mean) conversion, done once per
+// pixel): a workgroup owns RM = 128 * MG probes x NT components, NT = 64 * NG, MG * NG = 8
+// waves; each wave 128 probes x 64 components (4 x 2 accumulators of 32 x 32, 128 AGPRs),
+// per k-step 4 A fragments from LDS (512 B per MFMA, 1,024 of the 2,048 cycles) and 2 B
+// fragments from L2 (32 B/clk/CU).  At NT = ldw = 512 every probe tile is read once.
+// Barriers are LDS-only (lgkmcnt(0) + s_barrier), so the B ring's loads stay in flight.
+__device__ __forceinline__ void frag_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NT, int WK>
+__global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t* __restrict__ P, int64_t b, int64_t d,
+                                                                   const uint8_t* __restrict__ mean_u8,
+                                                                   const uint4* __restrict__ Wf, int ldw,
+                                                                   float* __restrict__ part, int64_t bpad,
+                                                                   int64_t pps, int mt, int nt, int ns) {
+  constexpr int NG = NT / 64;          // wave columns (64 components each)
+  constexpr int MG = 8 / NG;           // wave rows (128 probes each)
+  constexpr int RM = 128 * MG;         // probes per workgroup
+  constexpr int SUB = WK / 16;         // MFMA k-steps per stage
+  constexpr int WS = WK + 8;           // LDS row stride (bf16): conflict-free ds_read_b128 / ds_write_b128
+  constexpr int PT = RM * WK / 512;    // pixels per thread per stage
+  constexpr int TPR = WK / PT;         // threads per probe row
+  constexpr int NV = PT / 16;          // uint4 of raw pixels per thread per stage
+  constexpr int RD = 4;                // B ring depth (k-steps in flight)
+  static_assert(NG * MG == 8 && PT % 16 == 0 && TPR >= 1 && SUB % RD == 0, "frag tile");
+  __shared__ __attribute__((aligned(16))) unsigned short sA[2][RM * WS];
+
+  // XCD-aware deal (as the wide kernel): XCD x takes the contiguous run of (split, m-tile,
+  // n-tile) items [x * per, (x + 1) * per), split-major, so one K split's Wf slice streams
+  // through one XCD's L2 for all its probe tiles
+  const int total = mt * nt * ns;
+  const int per = (total + 7) / 8;
+  const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (item >= total) return;
+  const int split = item / (mt * nt);
+  const int rem = item - split * (mt * nt);
+  const int mi = rem / nt, ni = rem - (rem / nt) * nt;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int ng = wave % NG, mg = wave / NG;
+  const int64_t m0 = (int64_t)mi * RM;
+  const int col0 = ni * NT;
+  const int64_t k_beg = (int64_t)split * pps;
+  const int64_t k_end = k_beg + pps < d ? k_beg + pps : d;
+  const int nsteps = (int)((k_end - k_beg) / WK);  // host guarantees whole stages
+  const int nsub = nsteps * SUB;
+
+  // probe staging: thread -> (row tid / TPR, PT pixels); raw bytes two stages ahead
+  const int sr = tid / TPR, sh = (tid % TPR) * PT;
+  const int64_t arow = m0 + sr;
+  const bool arow_ok = arow < b;
+  const uint8_t* pa = P + (arow_ok ? arow : 0) * d + sh;
+  struct Raw {
+    uint4 p[NV], m[NV];
+  };
+  auto load_raw = [&](int step, Raw& r) {
+    const int64_t px0 = k_beg + (int64_t)step * WK;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      r.p[v] = arow_ok ? *reinterpret_cast<const uint4*>(pa + px0 + 16 * v) : make_uint4(0, 0, 0, 0);
+      r.m[v] = *reinterpret_cast<const uint4*>(mean_u8 + px0 + sh + 16 * v);
+    }
+  };
+  auto convert_store = [&](const Raw& r, int buf) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const unsigned pw[4] = {r.p[v].x, r.p[v].y, r.p[v].z, r.p[v].w};
+      const unsigned mw[4] = {r.m[v].x, r.m[v].y, r.m[v].z, r.m[v].w};
+      unsigned pk[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned w = pw[q], m = mw[q];
+        const float f0 = (float)(w & 0xffu) - (float)(m & 0xffu);
+        const float f1 = (float)((w >> 8) & 0xffu) - (float)((m >> 8) & 0xffu);
+        const float f2 = (float)((w >> 16) & 0xffu) - (float)((m >> 16) & 0xffu);
+        const float f3 = (float)(w >> 24) - (float)(m >> 24);
+        pk[2 * q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+        pk[2 * q + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+      }
+      const uint4 a0 = arow_ok ? make_uint4(pk[0], pk[1], pk[2], pk[3]) : make_uint4(0, 0, 0, 0);
+      const uint4 a1 = arow_ok ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(&sA[buf][sr * WS + sh + 16 * v]) = a0;
+      *reinterpret_cast<uint4*>(&sA[buf][sr * WS + sh + 16 * v + 8]) = a1;
+    }
+  };
+
+  // B fragments: wave columns ct0, ct0 + 1 (32 each); k-step g of this split is fragment
+  // row kb0 + g
+  const int64_t KB = d / 16;
+  const int64_t ct0 = (col0 + ng * 64) / 32;
+  const uint4* wb0 = Wf + (ct0 * KB + k_beg / 16) * 64 + lane;
+  const uint4* wb1 = wb0 + KB * 64;
+  uint4 ring[RD][2];
+  auto load_b = [&](int g, uint4* dst) {
+    dst[0] = wb0[(int64_t)g * 64];
+    dst[1] = wb1[(int64_t)g * 64];
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  Raw r0, r1;
+  if (nsteps > 0) load_raw(0, r0);
+#pragma unroll
+  for (int g = 0; g < RD; ++g)
+    if (g < nsub) load_b(g, ring[g]);
+  if (nsteps > 1) load_raw(1, r1);
+  if (nsteps > 0) convert_store(r0, 0);
+  frag_lds_barrier();
+  const unsigned short* arow_lds = &sA[0][(mg * 128 + c32) * WS + 8 * h];
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 2 < nsteps) load_raw(st + 2, r0);
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) {  // lane (r, h) holds A[r][16s + 8h + j], B[16s + 8h + j][r]
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(arow_lds + buf * (RM * WS) + i * 32 * WS + 16 * s);
+      const int slot = s % RD;
+      bf16x8 w0, w1;
+      __builtin_memcpy(&w0, &ring[slot][0], 16);
+      __builtin_memcpy(&w1, &ring[slot][1], 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], w0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], w1, acc[i][1], 0, 0, 0);
+      }
+      const int g = st * SUB + s + RD;
+      if (g < nsub) load_b(g, ring[slot]);
+    }
+    if (st + 1 < nsteps) convert_store(r1, buf ^ 1);
+    frag_lds_barrier();
+    r1 = r0;
+  }
+
+  float* out = part + (int64_t)split * bpad * ldw + col0 + ng * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + mg * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < bpad) out[row * ldw + j * 32 + c32] = acc[i][j][r];
+      }
+}
+
+// Wf[(ct * KB + kb) * 64 + lane] (16 B) = W16[32 ct + (lane & 31)][16 kb + 8 (lane >> 5) .. + 8]
+__global__ void bf16_frag_kernel(const unsigned short* __restrict__ Wt16, int64_t d, int64_t total,
+                                 uint4* __restrict__ Wf) {
+  const int64_t KB = d / 16;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int ln = (int)(idx & 63);
+    const int64_t rest = idx >> 6;
+    const int64_t kb = rest % KB, ct = rest / KB;
+    Wf[idx] = *reinterpret_cast<const uint4*>(Wt16 + (ct * 32 + (ln & 31)) * d + kb * 16 + 8 * (ln >> 5));
+  }
+}
+
+bool bf16_frag_supported(int64_t d, int ldw) { return d % 64 == 0 && ldw % 128 == 0; }
+
+hipError_t launch_bf16_frag(hipStream_t s, const unsigned short* Wt16, int64_t d, int ldw, void* Wf) {
+  if (!bf16_frag_supported(d, ldw)) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)(ldw / 32) * (d / 16) * 64;
+  hipLaunchKernelGGL(bf16_frag_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 65536)), dim3(256), 0, s,
+                     Wt16, d, total, static_cast<uint4*>(Wf));
+  return hipGetLastError();
+}
+
 // Wt16[c][px] = bf16(W[px][c]) (32 x 32 tiles through LDS), mean_r = round(mean).
 __global__ void bf16_model_kernel(const float* __restrict__ W, const float* __restrict__ mean, int64_t d, int ldw,
                                   unsigned short* __restrict__ Wt16, float* __restrict__ mean_r) {
@@ -380,9 +563,32 @@ hipError_t launch_mean_u8(hipStream_t s, const float* mean_r, int64_t d, uint8_t
   return hipGetLastError();
 }
 
-int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int64_t bpad, int64_t d, int ldw,
-                        int64_t* pix_per_split) {
+// Frag-form column tile: the widest of 512 / 256 / 128 dividing ldw
+static int frag_nt(int ldw) { return ldw % 512 == 0 ? 512 : ldw % 256 == 0 ? 256 : 128; }
+static bool use_frag(const void* Wf) {
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_FRAG=0: round 5's wide kernel (A/B)
+  if (const char* e = getenv("EF_PROJ_FRAG")) return Wf && atoi(e) != 0;
+#endif
+  return Wf != nullptr;
+}
+constexpr int FWK = 64;  // frag form: pixels per stage
+
+int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, const void* Wf, int64_t bpad, int64_t d,
+                        int ldw, int64_t* pix_per_split) {
   const int64_t steps = (d + HK - 1) / HK;
+  if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8) && use_frag(Wf)) {
+    const int NT = frag_nt(ldw);
+    const int64_t RM = 128 * (8 / (NT / 64));
+    const int64_t wsteps = d / FWK;
+    const int64_t tiles = (bpad + RM - 1) / RM * (ldw / NT);
+    int64_t ns = (256 + tiles - 1) / tiles;  // one workgroup per CU
+    if (ns > wsteps) ns = wsteps;
+    if (ns < 1) ns = 1;
+    while ((tiles * ns) % 8 != 0 && ns < wsteps) ++ns;
+    const int64_t steps_per = (wsteps + ns - 1) / ns;
+    *pix_per_split = steps_per * FWK;
+    return (int)((d + *pix_per_split - 1) / *pix_per_split);
+  }
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8)) {
     const int64_t wsteps = d / WKS;
     const int nt = ldw % 256 == 0 ? ldw / 256 : ldw / 128;
@@ -408,9 +614,29 @@ int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, int6
 }
 
 hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_t b, int64_t bpad, int64_t d,
-                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16, int ldw,
-                               float* part, int nsplit, int64_t pps) {
+                               const float* mean_r, const uint8_t* mean_u8, const unsigned short* Wt16,
+                               const void* Wf, int ldw, float* part, int nsplit, int64_t pps) {
   if (ldw % HN != 0) return hipErrorInvalidValue;
+  if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8) && use_frag(Wf)) {
+    const int NT = frag_nt(ldw);
+    const int64_t RM = 128 * (8 / (NT / 64));
+    const int nt = ldw / NT;
+    const int mt = (int)((bpad + RM - 1) / RM);
+    const int grid = (mt * nt * nsplit + 7) / 8 * 8;
+    if (pps % FWK != 0) return hipErrorInvalidValue;
+    const uint8_t* p8 = static_cast<const uint8_t*>(P);
+    const uint4* wf = static_cast<const uint4*>(Wf);
+    if (NT == 512)
+      hipLaunchKernelGGL((project_bf16_frag_kernel<512, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
+                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
+    else if (NT == 256)
+      hipLaunchKernelGGL((project_bf16_frag_kernel<256, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
+                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
+    else
+      hipLaunchKernelGGL((project_bf16_frag_kernel<128, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
+                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
+    return hipGetLastError();
+  }
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8)) {
     const bool n256 = ldw % 256 == 0;
     const int nt = n256 ? ldw / 256 : ldw / 128;

@@ -22,7 +22,7 @@ EF_MODEL_BF16 = 0x2
 EF_MEM_DEVICE = 0x100
 EF_IMG_RGB = 0x200
 EF_KERNEL_SEARCH, EF_KERNEL_PROJECT, EF_KERNEL_TMATCH, EF_KERNEL_INGEST, EF_KERNEL_HAAR, EF_KERNEL_JPEG, \
-    EF_KERNEL_SYRK = 0, 1, 2, 3, 4, 5, 6
+    EF_KERNEL_SYRK, EF_KERNEL_JPEG_HOST = 0, 1, 2, 3, 4, 5, 6, 7
 EF_JPEG_GRAY, EF_JPEG_BGR = 0, 1
 EF_JPEG_E_UNSUPPORTED, EF_JPEG_E_CORRUPT = -10, -11
 EF_KEY_NONE = (1 << 63) - 1
@@ -33,6 +33,7 @@ EF_OPT_JPEG_CHUNK_BITS = 6
 EF_OPT_SEARCH_SPLIT_BF16 = 7
 EF_OPT_JPEG_PART_FILES = 8
 EF_OPT_FIT_CHEBYSHEV = 9
+EF_OPT_HOST_THREADS = 10
 EF_E_NUMERIC = -5
 
 
@@ -104,6 +105,7 @@ _SIGS = {
     "ef_tm_prepare": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, u32], C.c_int),
     "ef_tm_match": ([vp, vp, i64, vp, vp, vp, vp, u32], C.c_int),
     "ef_tm_info": ([vp, C.POINTER(i32), C.POINTER(i64), vp, vp], C.c_int),
+    "ef_tm_sums_bits": ([i32, i32, i64], C.c_int),
     "ef_haar_set_cascade": ([vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "ef_haar_detect": ([vp, vp, i32, i32, i64, C.c_double, i32, i32, i32, i32, i32, vp, i32, C.POINTER(i32), vp, i32,
                         C.POINTER(i32), u32], C.c_int),
@@ -151,7 +153,7 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        if h.ef_api_version() != 6:
+        if h.ef_api_version() != 7:
             raise NativeLibraryError("libeigenface.so API version mismatch")
         _lib = h
         return h

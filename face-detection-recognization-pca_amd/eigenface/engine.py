@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
+import os
 import sys
 from dataclasses import dataclass
 
@@ -39,7 +40,22 @@ _OPTIONS = {"fit_max_iters": N.EF_OPT_FIT_MAX_ITERS, "fit_fp32_coarse": N.EF_OPT
             "cov_slab_bytes": N.EF_OPT_COV_SLAB_BYTES, "tm_int64_sums": N.EF_OPT_TM_INT64_SUMS,
             "haar_ordered": N.EF_OPT_HAAR_ORDERED, "jpeg_chunk_bits": N.EF_OPT_JPEG_CHUNK_BITS,
             "search_split_bf16": N.EF_OPT_SEARCH_SPLIT_BF16, "jpeg_part_files": N.EF_OPT_JPEG_PART_FILES,
-            "fit_chebyshev": N.EF_OPT_FIT_CHEBYSHEV}
+            "fit_chebyshev": N.EF_OPT_FIT_CHEBYSHEV, "host_threads": N.EF_OPT_HOST_THREADS}
+
+
+def host_cpu_share():
+    """The job's CPU share for the library's host workers: OMP_NUM_THREADS when set (the
+    GPU pool presets it to the job's share), else the affinity mask, capped at 16."""
+    share = None
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    if v.strip().isdigit() and int(v) > 0:
+        share = int(v)
+    if share is None:
+        try:
+            share = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            share = os.cpu_count() or 1
+    return max(1, min(16, share))
 
 
 def _option(o):
@@ -102,6 +118,7 @@ class Engine:
             raise N.EigenfaceError(rc, f"ef_create(device={device}) failed (no usable HIP device?)")
         self._h = h
         self.device = int(device)
+        self._chk(self._lib.ef_set_option(h, N.EF_OPT_HOST_THREADS, host_cpu_share()))
         # The engine's own stream is a torch pool stream when torch is present: pool streams
         # live as long as the process, so a tensor marked with record_stream (_torch_order)
         # never outlives the stream it was recorded on.  A stream the library created would
@@ -204,7 +221,8 @@ class Engine:
     def set_option(self, option, value):
         """Context tunable (include/eigenface.h EF_OPT_*): "fit_max_iters",
         "fit_fp32_coarse", "cov_slab_bytes", "tm_int64_sums", "haar_ordered", "jpeg_chunk_bits",
-        "search_split_bf16", "jpeg_part_files", "fit_chebyshev" or the code."""
+        "search_split_bf16", "jpeg_part_files", "fit_chebyshev", "host_threads" (process-wide) or
+        the code."""
         self._chk(self._lib.ef_set_option(self._h, _option(option), int(value)))
 
     def get_option(self, option):
@@ -822,7 +840,7 @@ class Engine:
     def timing_get(self, kernel="search"):
         kid = {"search": N.EF_KERNEL_SEARCH, "project": N.EF_KERNEL_PROJECT, "tmatch": N.EF_KERNEL_TMATCH,
                "ingest": N.EF_KERNEL_INGEST, "haar": N.EF_KERNEL_HAAR, "jpeg": N.EF_KERNEL_JPEG,
-               "syrk": N.EF_KERNEL_SYRK}[kernel]
+               "syrk": N.EF_KERNEL_SYRK, "jpeg_host": N.EF_KERNEL_JPEG_HOST}[kernel]
         ms = C.c_double(0)
         n = C.c_int64(0)
         self._chk(self._lib.ef_timing_get(self._h, kid, C.byref(ms), C.byref(n)))

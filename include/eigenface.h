@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define EF_API_VERSION 6
+#define EF_API_VERSION 7
 
 /* status codes */
 #define EF_OK 0
@@ -62,6 +62,8 @@ extern "C" {
 #define EF_KERNEL_HAAR 4    /* Haar cascade detection, one frame (GPU part) */
 #define EF_KERNEL_JPEG 5    /* JPEG entropy decode + IDCT + colour, one batch */
 #define EF_KERNEL_SYRK 6    /* the fit's int8 covariance/Gram SYRK, all passes of one fit */
+#define EF_KERNEL_JPEG_HOST 7 /* host staging of one ef_jpeg_ingest part (marker parse, destuff, tables):
+                                wall time on the host, not a device kernel (API v7) */
 
 /* No-result sentinel in a key array (empty gallery). */
 #define EF_KEY_NONE INT64_MAX
@@ -263,6 +265,9 @@ int ef_comm_info(const ef_ctx* ctx, int32_t* nranks, int32_t* rank);
 #define EF_OPT_FIT_CHEBYSHEV 9     /* 1 [default]: the subspace iteration advances a Chebyshev
                                       three-term recurrence on [0, theta_m] between Rayleigh-Ritz
                                       steps; 0: one shifted power step per iteration */
+#define EF_OPT_HOST_THREADS 10     /* host worker threads for the JPEG parse / destuff, PROCESS-WIDE
+                                      (any context sets it) [0: min(16, hardware threads)]; the
+                                      Python Engine sets the job's CPU share (API v7) */
 int ef_set_option(ef_ctx* ctx, int32_t option, int64_t value);
 int ef_get_option(const ef_ctx* ctx, int32_t option, int64_t* value);
 
@@ -334,6 +339,11 @@ int ef_tm_match(ef_ctx* ctx, const uint8_t* frame, int64_t frame_ld, float* best
                 int32_t* y_out, float* maps_out, uint32_t flags);
 int ef_tm_info(ef_ctx* ctx, int32_t* n_problems, int64_t* map_elems, int32_t* result_h,
                int32_t* result_w);
+/* Host-only (API v7): the integral-image width ef_tm_prepare picks for a frame_h x frame_w
+ * frame whose largest template area is max_template_area: 32 (wrapping uint32 sums) when
+ * every area is < 2^18 and (frame_h + 1)(frame_w + 1) < 2^30, else 64 (int64 sums); the
+ * EF_OPT_TM_INT64_SUMS option forces 64 per context.  EF_E_INVALID on bad sizes. */
+int ef_tm_sums_bits(int32_t frame_h, int32_t frame_w, int64_t max_template_area);
 
 /* --------------------------------------------------------- Haar cascade detector
  * Replaces face_cascade.detectMultiScale(gray, scaleFactor, minNeighbors, minSize)

@@ -162,6 +162,28 @@ def test_match_template_integral_width(eng, monkeypatch, ts, force64):
     assert (best[0], xs[0], ys[0]) == (np.float32(v), mx, my) == (np.float32(v), 12, 25)
 
 
+def test_match_template_frame_past_uint32_offsets(eng):
+    """a 32767 x 32767 frame has (H + 1)(W + 1) = 2^30 integral entries,
+    so the uint32 form's byte offsets (uint32(entry) * 4) would wrap; ef_tm_prepare must
+    pick int64 sums (ef_tm_sums_bits) even though the template area is tiny.  A random
+    frame with the template cut from its far corner: the maximum (1.0) must be found there,
+    with the first-max position of minMaxLoc."""
+    import eigenface._native as nat
+    H = W = 32767
+    assert nat.lib().ef_tm_sums_bits(H, W, 24 * 24) == 64
+    rng = np.random.default_rng(99)
+    frame = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    y0, x0 = 32700, 32720
+    t = frame[y0:y0 + 24, x0:x0 + 24].copy()
+    eng.tm_prepare([t], [(0, 24, 24)], frame.shape)
+    best, xs, ys = eng.tm_match(frame)
+    assert (int(xs[0]), int(ys[0])) == (x0, y0)
+    R = io.match_template_ccoeff_normed(frame[y0 - 8:y0 + 40, x0 - 8:x0 + 40], t)
+    assert best[0] == np.float32(R.max()) == R[8, 8]
+    eng.tm_prepare([t], [(0, 24, 24)], (32, 32))  # release the ~20 GB of operands
+    del frame
+
+
 def test_scaled_templates_resized_on_gpu(eng):
     """Problems at 0.8/1.2 scale: the GPU resizes the template (INTER_LINEAR) first."""
     from eigenface.image import scaled_sizes

@@ -61,7 +61,7 @@ def test_one_hip_runtime_per_process():
 def test_api_version_and_no_device_here():
     from eigenface import _native
     lib = _native.lib()
-    assert lib.ef_api_version() == 6
+    assert lib.ef_api_version() == 7
     n = ctypes.c_int(-1)
     assert lib.ef_device_count(ctypes.byref(n)) == 0
     if n.value == 0:  # build container: creating a context must fail cleanly, not crash
@@ -233,3 +233,34 @@ def test_search_schedule_plans_each_piece_from_its_launched_rows():
         assert np.all(p[:, 4] % 8 == 0) and np.all(p[:, 4] * p[:, 5] * (64 if kp <= 128 else 128 if not split else 256)
                                                     >= n)
     assert lib.ef_search_schedule(10, 0, 10, 0, None, 0, ctypes.byref(i32())) != 0
+
+
+def test_tm_integral_width_rule():
+    """the wrapping uint32 integral images index bytes as
+    uint32(entry) * 4, so ef_tm_prepare must pick int64 sums once a frame has 2^30 or more
+    integral entries, (H + 1)(W + 1), as well as for template areas >= 2^18."""
+    from eigenface import _native
+    lib = _native.lib()
+    assert lib.ef_tm_sums_bits(480, 640, 150 * 360) == 32
+    assert lib.ef_tm_sums_bits(480, 640, (1 << 18) - 1) == 32
+    assert lib.ef_tm_sums_bits(480, 640, 1 << 18) == 64
+    # the frame-size edge: 32768 x 32767 entries stay uint32, 32768 x 32768 = 2^30 do not
+    assert lib.ef_tm_sums_bits(32767, 32766, 16) == 32   # 32768 * 32767 < 2^30
+    assert lib.ef_tm_sums_bits(32767, 32767, 16) == 64   # 32768 * 32768 = 2^30
+    assert lib.ef_tm_sums_bits(1 << 20, 1023, 16) == 64  # tall frames too
+    assert lib.ef_tm_sums_bits(0, 640, 16) < 0
+
+
+def test_host_cpu_share_rule(monkeypatch):
+    """the library's host workers (JPEG parse / destuff) are sized to the
+    job's CPU share — OMP_NUM_THREADS as the GPU pool presets it, else the affinity mask —
+    not to the machine's hardware threads (256 on the pool's boxes), capped at 16."""
+    from eigenface.engine import host_cpu_share
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert host_cpu_share() == 16
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert host_cpu_share() == 3
+    monkeypatch.setenv("OMP_NUM_THREADS", "256")
+    assert host_cpu_share() == 16
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert host_cpu_share() == max(1, min(16, len(os.sched_getaffinity(0))))

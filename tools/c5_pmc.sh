@@ -23,7 +23,7 @@ python tools/pmc_summary.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$R" --pmc TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d /tmp/ph -o run -- python $B > $O/h.txt 2>&1 || exit $?
 python tools/pmc_kernels.py /tmp/ph/run_counter_collection.csv > $O/l2.txt
 # bf16 projection: the same passes for project_bf16_wide_kernel
-P="project_bf16_wide"
+P="project_bf16_frag"
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$P" --pmc FETCH_SIZE --output-format csv -d $O/proj_fetch -o run -- python $B > $O/qf.txt 2>&1 || exit $?
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$P" --pmc WRITE_SIZE --output-format csv -d $O/proj_write -o run -- python $B > $O/qw.txt 2>&1 || exit $?
 timeout -s KILL 180 rocprofv3 --kernel-include-regex "$P" --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $O/proj_sq -o run -- python $B > $O/qs.txt 2>&1 || exit $?

@@ -28,7 +28,7 @@ CONFIGS = {
     "c5s3w3": ("search_wide3_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
     "c5": ("search_wide_kernel<512, 0, false>", 1_000_000 * 512 * 4 + 1_000_000 * 4 + 4096 * 512 * 4),
     # C5 bf16 projection: uint8 probe pixels + bf16 W + fp32 partial features
-    "c5proj": ("project_bf16_wide_kernel", 4096 * 65536 + 512 * 65536 * 2 + 4096 * 512 * 4),
+    "c5proj": ("project_bf16_frag_kernel", 4096 * 65536 + 512 * 65536 * 2 + 4096 * 512 * 4),
 }
 SIMDS = 1024  # 256 CUs x 4
 XCDS = 8
