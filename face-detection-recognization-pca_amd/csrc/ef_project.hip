@@ -22,7 +22,12 @@ constexpr int SA = BK + 4;        // LDS row stride of the pixel tile (conflict-
 
 // KPW = columns of this workgroup's tile (64 | 128); ldw = total padded columns of W and of
 // the partial slabs (KPW, or a multiple of 128 with gridDim.z = ldw / 128 column tiles).
-template <int KPW, int PDT, bool VEC>
+// FAST (uint8 probes, d and the split a whole number of 32-pixel stages, 16-B aligned
+// rows): every load in the main loop is unconditional — rows past b read row b - 1 and are
+// zeroed at conversion, the prefetch after the last stage re-reads it — so the loop has no
+// branches and the compiler's vmcnt accounting stays exact (a load under a branch made it
+// wait for every load in flight; the generic form also carries the per-element fallback).
+template <int KPW, int PDT, bool VEC, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict__ Pv, int64_t b,
                                                          int64_t d, const float* __restrict__ mu,
                                                          const float* __restrict__ W, int ldw,
@@ -61,6 +66,7 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
   bool raw_ok = false;
   float4 wv[W4_PT];
 
+  const bool row_ok = m0 + pr < b;
   auto load_stage = [&](int step) {
     const int64_t kb = k_beg + (int64_t)step * BK;
     const int64_t row = m0 + pr;
@@ -132,6 +138,49 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
     }
   };
 
+  // FAST forms (no branch, no per-element fallback); the staged registers are a value
+  // (FastRaw) rather than the captured arrays, which the compiler kept in scratch here
+  struct FastRaw {
+    uint4 raw;
+    float4 mu[4];
+    float4 w[W4_PT];
+  };
+  auto load_fast = [&](int step) {
+    FastRaw r;
+    const int64_t kb = k_beg + (int64_t)step * BK;
+    const int64_t px0 = kb + ph;
+    const uint8_t* P = reinterpret_cast<const uint8_t*>(Pv);
+    r.raw = *reinterpret_cast<const uint4*>(P + (row_ok ? m0 + pr : b - 1) * d + px0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.mu[j] = *reinterpret_cast<const float4*>(mu + px0 + 4 * j);
+#pragma unroll
+    for (int j = 0; j < W4_PT; ++j) {
+      const int idx = tid + 256 * j;
+      const int kr = idx / (KPW / 4), c4 = idx % (KPW / 4);
+      r.w[j] = reinterpret_cast<const float4*>(W + (kb + kr) * ldw + col0)[c4];
+    }
+    return r;
+  };
+  auto store_fast = [&](const FastRaw& r, int buf) {
+    const unsigned w4[4] = {r.raw.x, r.raw.y, r.raw.z, r.raw.w};
+    float* a = &sA[buf][pr * SA + ph];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned u = w4[j];
+      const float4 m = r.mu[j];
+      const float4 v = row_ok ? make_float4((float)(u & 0xffu) - m.x, (float)((u >> 8) & 0xffu) - m.y,
+                                            (float)((u >> 16) & 0xffu) - m.z, (float)(u >> 24) - m.w)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(a + 4 * j) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < W4_PT; ++j) {
+      const int idx = tid + 256 * j;
+      const int kr = idx / (KPW / 4), c4 = idx % (KPW / 4);
+      *reinterpret_cast<float4*>(&sW[buf][kr * SW + c4 * 4]) = r.w[j];
+    }
+  };
+
   f32x16 acc[AB][BB];
 #pragma unroll
   for (int i = 0; i < AB; ++i)
@@ -139,14 +188,25 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
     for (int j = 0; j < BB; ++j) acc[i][j] = f32x16{};
 
   if (nsteps > 0) {
-    load_stage(0);
-    store_stage(0);
+    if constexpr (FAST) {
+      store_fast(load_fast(0), 0);
+    } else {
+      load_stage(0);
+      store_stage(0);
+    }
   }
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
     const int buf = st & 1;
-    const bool more = st + 1 < nsteps;
-    if (more) load_stage(st + 1);
+    const bool more = st + 1 < nsteps;  // (FAST: the last prefetch re-reads the last stage)
+    FastRaw fr;
+    if constexpr (FAST)
+      fr = load_fast(st + 1 < nsteps ? st + 1 : st);
+    else if (more)
+      load_stage(st + 1);
+    // the next stage's loads issue before this stage's MFMAs (the scheduler would sink
+    // them next to the stores and wait out their latency there)
+    if constexpr (FAST) __builtin_amdgcn_sched_barrier(0);
     // k permutation inside the stage: lane half h owns pixels [16h, 16h+16)
 #pragma unroll
     for (int s4 = 0; s4 < 16; s4 += 4) {
@@ -167,7 +227,12 @@ __global__ __launch_bounds__(256, 2) void project_kernel(const void* __restrict_
         }
       }
     }
-    if (more) store_stage(buf ^ 1);
+    // (and their conversion stays after the MFMAs: hoisted above them it waits for the loads)
+    if constexpr (FAST) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FAST)
+      store_fast(fr, buf ^ 1);
+    else if (more)
+      store_stage(buf ^ 1);
     __syncthreads();
   }
 
@@ -222,7 +287,14 @@ static hipError_t proj_t(hipStream_t s, const void* P, int64_t b, int64_t bpad, 
                          const float* mean, const float* W, int ldw, float* part, int nsplit, int64_t pps) {
   const dim3 grid((unsigned)(bpad / BM), (unsigned)nsplit, (unsigned)(ldw / KPW));
   const bool vec = (d % 16 == 0) && ((reinterpret_cast<uintptr_t>(P) & 15) == 0) && (pps % 16 == 0);
-  if (vec)
+  bool fast = PDT == EF_U8 && vec && d % BK == 0 && pps % BK == 0 && b >= 1;
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_FAST=0: the generic kernel (A/B)
+  if (const char* e = getenv("EF_PROJ_FAST")) fast = fast && atoi(e) != 0;
+#endif
+  if (fast)
+    hipLaunchKernelGGL((project_kernel<KPW, PDT, true, true>), grid, dim3(256), 0, s, P, b, d, mean, W, ldw, part,
+                       bpad, pps);
+  else if (vec)
     hipLaunchKernelGGL((project_kernel<KPW, PDT, true>), grid, dim3(256), 0, s, P, b, d, mean, W, ldw, part,
                        bpad, pps);
   else

@@ -372,11 +372,15 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
   struct Raw {
     uint4 p[NV], m[NV];
   };
+  // Every load in the main loop is unconditional (rows past b read row 0 and are zeroed
+  // at conversion; steps past the end re-read the last one): a load under a branch makes
+  // the compiler's vmcnt accounting path-dependent, and it then waited for ALL loads in
+  // flight (the just-issued HBM pixel loads too) before each stage's first MFMA.
   auto load_raw = [&](int step, Raw& r) {
     const int64_t px0 = k_beg + (int64_t)step * WK;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      r.p[v] = arow_ok ? *reinterpret_cast<const uint4*>(pa + px0 + 16 * v) : make_uint4(0, 0, 0, 0);
+      r.p[v] = *reinterpret_cast<const uint4*>(pa + px0 + 16 * v);
       r.m[v] = *reinterpret_cast<const uint4*>(mean_u8 + px0 + sh + 16 * v);
     }
   };
@@ -421,40 +425,64 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
+  // (the host guarantees nsteps >= 1: splits are whole 64-pixel stages of d % 64 == 0)
   Raw r0, r1;
-  if (nsteps > 0) load_raw(0, r0);
+  load_raw(0, r0);
 #pragma unroll
-  for (int g = 0; g < RD; ++g)
-    if (g < nsub) load_b(g, ring[g]);
-  if (nsteps > 1) load_raw(1, r1);
-  if (nsteps > 0) convert_store(r0, 0);
+  for (int g = 0; g < RD; ++g) load_b(g < nsub ? g : nsub - 1, ring[g]);
+  load_raw(nsteps > 1 ? 1 : 0, r1);
+  convert_store(r0, 0);
   frag_lds_barrier();
   const unsigned short* arow_lds = &sA[0][(mg * 128 + c32) * WS + 8 * h];
-  for (int st = 0; st < nsteps; ++st) {
+  auto read_a = [&](int buf, int s, bf16x8 (&a)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const bf16x8*>(arow_lds + buf * (RM * WS) + i * 32 * WS + 16 * s);
+  };
+  // Order held by sched_barrier: without it the scheduler sank every ring refill below the
+  // stage's last MFMA (next to the barrier), so each stage's first MFMA waited out a full
+  // L2 round trip.  Per k-step: the k-step's A fragments are read, its 8 MFMAs issue, then
+  // its ring slot is refilled four k-steps ahead.  The raw pixel registers alternate
+  // between two sets by stage parity (the loop is unrolled by two), so no register copy
+  // has to wait for the loads issued at the stage's start.
+  auto run_stage = [&](int st, Raw& ld, Raw& cv) {
     const int buf = st & 1;
-    if (st + 2 < nsteps) load_raw(st + 2, r0);
+    load_raw(st + 2 < nsteps ? st + 2 : nsteps - 1, ld);
+    bf16x8 acur[4], anxt[4];
+    read_a(buf, 0, acur);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {  // lane (r, h) holds A[r][16s + 8h + j], B[16s + 8h + j][r]
-      bf16x8 a[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(arow_lds + buf * (RM * WS) + i * 32 * WS + 16 * s);
+      if (s + 1 < SUB) read_a(buf, s + 1, anxt);
+      // the next k-step's A reads issue before this k-step's MFMAs (8 MFMAs = 256 cycles of
+      // cover for the LDS latency; the scheduler otherwise sank them below 7 of the 8)
+      __builtin_amdgcn_sched_barrier(0);
       const int slot = s % RD;
       bf16x8 w0, w1;
       __builtin_memcpy(&w0, &ring[slot][0], 16);
       __builtin_memcpy(&w1, &ring[slot][1], 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], w0, acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], w1, acc[i][1], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[i], w0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[i], w1, acc[i][1], 0, 0, 0);
       }
       const int g = st * SUB + s + RD;
-      if (g < nsub) load_b(g, ring[slot]);
+      load_b(g < nsub ? g : nsub - 1, ring[slot]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < SUB) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acur[i] = anxt[i];
+      }
     }
-    if (st + 1 < nsteps) convert_store(r1, buf ^ 1);
+    convert_store(cv, buf ^ 1);  // stage st + 1 (after the last stage: a buffer nobody reads)
     frag_lds_barrier();
-    r1 = r0;
+  };
+  int st = 0;
+  for (; st + 1 < nsteps; st += 2) {
+    run_stage(st, r0, r1);
+    run_stage(st + 1, r1, r0);
   }
+  if (st < nsteps) run_stage(st, r0, r1);
 
   float* out = part + (int64_t)split * bpad * ldw + col0 + ng * 64;
 #pragma unroll
@@ -571,7 +599,15 @@ static bool use_frag(const void* Wf) {
 #endif
   return Wf != nullptr;
 }
-constexpr int FWK = 64;  // frag form: pixels per stage
+// frag form: pixels per stage, 128 at NT = 512 (half the barriers per pixel; the
+// 256 / 128-column forms would spill or exceed the LDS at 128), else 64
+static int frag_wk(int NT, int64_t d) {
+  if (NT != 512 || d % 128 != 0) return 64;  // (every split a whole number of stages)
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_WK=64|128 (A/B)
+  if (const char* e = getenv("EF_PROJ_WK")) return atoi(e) == 64 ? 64 : 128;
+#endif
+  return 128;
+}
 
 int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, const void* Wf, int64_t bpad, int64_t d,
                         int ldw, int64_t* pix_per_split) {
@@ -579,6 +615,7 @@ int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, cons
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8) && use_frag(Wf)) {
     const int NT = frag_nt(ldw);
     const int64_t RM = 128 * (8 / (NT / 64));
+    const int FWK = frag_wk(NT, d);
     const int64_t wsteps = d / FWK;
     const int64_t tiles = (bpad + RM - 1) / RM * (ldw / NT);
     int64_t ns = (256 + tiles - 1) / tiles;  // one workgroup per CU
@@ -623,18 +660,21 @@ hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_
     const int nt = ldw / NT;
     const int mt = (int)((bpad + RM - 1) / RM);
     const int grid = (mt * nt * nsplit + 7) / 8 * 8;
+    const int FWK = frag_wk(NT, d);
     if (pps % FWK != 0) return hipErrorInvalidValue;
     const uint8_t* p8 = static_cast<const uint8_t*>(P);
     const uint4* wf = static_cast<const uint4*>(Wf);
-    if (NT == 512)
-      hipLaunchKernelGGL((project_bf16_frag_kernel<512, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
-                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
-    else if (NT == 256)
-      hipLaunchKernelGGL((project_bf16_frag_kernel<256, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
-                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
-    else
-      hipLaunchKernelGGL((project_bf16_frag_kernel<128, FWK>), dim3((unsigned)grid), dim3(512), 0, s, p8, b, d,
-                         mean_u8, wf, ldw, part, bpad, pps, mt, nt, nsplit);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 0, s, p8, b, d, mean_u8, wf, ldw, part, bpad, pps, mt,
+                         nt, nsplit);
+    };
+    if (FWK == 128) {
+      go(project_bf16_frag_kernel<512, 128>);
+    } else {
+      if (NT == 512) go(project_bf16_frag_kernel<512, 64>);
+      else if (NT == 256) go(project_bf16_frag_kernel<256, 64>);
+      else go(project_bf16_frag_kernel<128, 64>);
+    }
     return hipGetLastError();
   }
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8)) {

@@ -74,10 +74,12 @@ BF16_REL = 2.0 ** -8  # stated tolerance: |f_bf16 - f| <= 2^-8 * sum_px |p - rou
 
 
 @pytest.mark.parametrize("d,k,b,mean_lo,mean_hi", [
-    (4096, 64, 300, 60, 200),      # wide kernel, 128-column tiles
+    (4096, 64, 300, 60, 200),      # frag kernel, 128-column tiles (512 probes per workgroup)
     (10000, 200, 129, 60, 200),    # d % 64 != 0: the 128 x 128 kernel
-    (65536, 512, 256, 60, 200),    # config 5: wide kernel, 256-column tiles
-    (8192, 256, 257, 60, 200),     # ragged batch through the wide kernel
+    (65536, 512, 256, 60, 200),    # config 5: frag kernel, 512-column tiles, 128-pixel stages
+    (8192, 256, 257, 60, 200),     # ragged batch through the frag kernel (256 x 256 tiles)
+    (4160, 512, 300, 60, 200),     # d % 128 != 0 at 512 columns: 64-pixel stages, ragged batch
+    (8192, 1024, 130, 60, 200),    # two 512-column tiles
     (4096, 128, 200, -40, 300)])   # round(mean) outside 0..255: the byte-mean wide kernel is skipped
 def test_project_bf16_tolerance(eng, d, k, b, mean_lo, mean_hi):
     """Config 5 bf16 projection: uint8 pixels minus round(mean) are exact in bf16, so the
