@@ -219,9 +219,10 @@ def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cp
             reps.append(time.perf_counter() - t0)
         eng.timing(False)
         s_ms, s_n = eng.timing_get("search")
-        legs[opt] = (reps, s_ms / max(s_n, 1), s_n)
+        p_ms, p_n = eng.timing_get("project")
+        legs[opt] = (reps, s_ms / max(s_n, 1), s_n, p_ms / max(p_n, 1), p_n)
     eng.set_option("search_split_bf16", 0)
-    reps, s_avg, s_n = legs[split_opt]
+    reps, s_avg, s_n, p_avg, p_n = legs[split_opt]
     el = float(np.median(reps))
     idx, _ = decode_keys(keys[split_opt].cpu().numpy(), "l2")
     traffic, traffic_src = pmc_traffic("c5hi" if split_opt == 3 else "c5s3")
@@ -235,14 +236,26 @@ def c5_bench(eng, dev, with_cpu: bool, steps: int, warmup: int, repeats: int, cp
            "roofline": dict(scan_roofline(True, s_avg, bsz, n, k, split_opt), traffic=traffic,
                             traffic_source=traffic_src, launches=s_n),
            "setup_s": round(setup_s, 1)}
+    # the bf16 projection kernel (project_bf16_frag_kernel): 2 B d k flop per
+    # launch on bf16 MFMA; algorithmic bytes = uint8 pixels + bf16 W + fp32 features
+    pf = 2.0 * bsz * d * k
+    ptraf, ptraf_src = pmc_traffic("c5proj")
+    proj_tf = pf / (p_avg * 1e-3) / 1e12 if p_avg > 0 else None
+    out["projection"] = {"kernel": "project_bf16_frag_kernel<512, 128> (W16 in MFMA-fragment order, B from L2 "
+                                   "into VGPRs)", "bound": "mfma", "avg_launch_ms": round(p_avg, 4),
+                         "launches": p_n, "flops_per_launch": pf,
+                         "achieved": round(proj_tf, 2) if proj_tf else None, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(proj_tf / PEAK_BF16_TFLOPS, 4) if proj_tf else None,
+                         "algorithmic_bytes": bsz * d + k * d * 2 + bsz * k * 4,
+                         "traffic": ptraf, "traffic_source": ptraf_src}
     if split_opt != 1:
-        reps1, s1_avg, s1_n = legs[1]
+        reps1, s1_avg, s1_n, _, _ = legs[1]
         el1 = float(np.median(reps1))
         out["scan_split_bf16"] = {"value": round(bsz * steps / el1, 1), "unit": "faces/s",
                                   "ms_per_step": round(el1 / steps * 1e3, 4),
                                   "keys_identical_to_headline": bool(torch.equal(keys[1], keys[split_opt])),
                                   "roofline": dict(scan_roofline(True, s1_avg, bsz, n, k, 1), launches=s1_n)}
-    reps32, s32_avg, s32_n = legs[0]
+    reps32, s32_avg, s32_n, _, _ = legs[0]
     el32 = float(np.median(reps32))
     traffic32, src32 = pmc_traffic("c5")
     out["scan_fp32"] = {"value": round(bsz * steps / el32, 1), "unit": "faces/s",

@@ -1100,3 +1100,43 @@ extern "C" int ef_colstats(ef_ctx* c, const void* Xv, int32_t x_dtype, int64_t n
   EF_HIP(c, hipStreamSynchronize(s), "sync");
   return EF_OK;
 }
+
+// The fit's CholQR factor on its own (API v7; ADVICE r5: a direct check of the blocked
+// factor for padded and odd orders and of the failed-pivot contract): Li = L^-1 for
+// G = L L^T (m <= 256, row-major, ldg >= m), host pointers.  A pivot <= tol_rel x max diag(G)
+// sets *info = -(column + 1) and leaves Li as given (the subspace iteration then
+// eigen-orthonormalises); *info = 0 on success.
+extern "C" int ef_chol_inv(ef_ctx* c, const double* G, int32_t m, int64_t ldg, double tol_rel, double* Li,
+                           int32_t* info) {
+  using namespace ef;
+  if (!c) return EF_E_INVALID;
+  if (!G || !Li || !info || m < 1 || ldg < m || !chol_inv_supported(m))
+    return set_err(c, EF_E_INVALID, "ef_chol_inv: bad arguments (1 <= m <= 256, ldg >= m)");
+  EF_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  DevBuf dG, dL, dW, dI;
+  auto done = [&](int rc) {
+    release(dG);
+    release(dL);
+    release(dW);
+    release(dI);
+    return rc;
+  };
+  int rc = ensure(c, dG, (size_t)m * ldg * sizeof(double));
+  if (rc == EF_OK) rc = ensure(c, dL, (size_t)m * m * sizeof(double));
+  if (rc == EF_OK) rc = ensure(c, dW, chol_inv_work_elems(m) * sizeof(double));
+  if (rc == EF_OK) rc = ensure(c, dI, sizeof(int));
+  if (rc != EF_OK) return done(rc);
+  hipError_t e = hipMemcpyAsync(dG.p, G, (size_t)m * ldg * sizeof(double), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(dL.p, Li, (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = launch_chol_inv(s, static_cast<const double*>(dG.p), m, ldg, tol_rel, static_cast<double*>(dL.p),
+                        static_cast<int*>(dI.p), static_cast<double*>(dW.p));
+  int hinfo = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(Li, dL.p, (size_t)m * m * sizeof(double), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(&hinfo, dI.p, sizeof(int), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return done(hip_err(c, e, "ef_chol_inv"));
+  *info = hinfo;
+  return done(EF_OK);
+}

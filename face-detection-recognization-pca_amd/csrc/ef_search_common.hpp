@@ -70,5 +70,10 @@ constexpr int kWide3ProbeTile = 256;  // split-bf16 wide kernel: probes per work
 hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, int s3, const SearchPlan& pl,
                               const float* qpad, const float* G, const float* aux, int64_t n, int64_t bpad,
                               const SearchWs& ws);
+// the single-bf16 screen's main pass with the gallery operand in VGPRs (ef_search_screen.hip;
+// kh = k / 2 in {128, 256}); screen_vg_enabled: the product default (diagnostic A/B knob)
+bool screen_vg_enabled();
+hipError_t launch_search_screen(hipStream_t s, int kh, int metric, const SearchPlan& pl, const float* q1,
+                                const float* G1, const float* aux, int64_t n, int64_t bpad, const SearchWs& ws);
 
 }  // namespace ef

@@ -1056,6 +1056,9 @@ hipError_t launch_search_wide(hipStream_t s, int kp, int metric, bool collect, i
     if (kp % 128 != 0 || bpad * (int64_t)kh * 4 >= ((int64_t)1 << 31) ||
         (int64_t)std::max(pl.tiles_per_chunk, pl.c_tpc) * ns >= ((int64_t)1 << 31))
       return hipErrorInvalidValue;
+    // main pass at the compiled widths: the gallery-in-VGPRs screen (ef_search_screen.hip)
+    if (!collect && (kh == 128 || kh == 256) && screen_vg_enabled())
+      return launch_search_screen(s, kh, metric, pl, qpad, G, aux, n, bpad, ws);
     switch (kp) {
       case 256:
         return l2 ? wide3_t<128, EF_METRIC_L2, true>(s, collect, true, pl, qpad, G, aux, n, bpad, ws, kh)

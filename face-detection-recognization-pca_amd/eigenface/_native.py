@@ -78,6 +78,7 @@ _SIGS = {
     "ef_fit_ex": ([vp, vp, i32, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), C.POINTER(i32)],
                   C.c_int),
     "ef_colstats": ([vp, vp, i32, i64, i64, u32, vp, vp], C.c_int),
+    "ef_chol_inv": ([vp, vp, i32, i64, C.c_double, vp, vp], C.c_int),
     "ef_fit_shard_stats": ([vp, vp, i64, i64, vp, vp, vp, u32], C.c_int),
     "ef_fit_from_stats": ([vp, vp, vp, vp, i64, i64, i32, u32, vp, vp, vp, vp, vp, vp, C.POINTER(i32),
                            C.POINTER(i32)], C.c_int),

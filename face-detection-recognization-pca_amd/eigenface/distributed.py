@@ -113,7 +113,7 @@ class ShardedGallery:
             if key not in self._rbuf:
                 self._rbuf[key] = torch.empty((self.world * b, 3), dtype=torch.int64, device=rec.device)
             parts = self._rbuf[key]
-            if rec.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: gather on host
+            if rec.is_cuda and not _device_collectives(self.group):  # gloo: gather on host
                 chunks = [torch.empty((b, 3), dtype=torch.int64) for _ in range(self.world)]
                 dist.all_gather(chunks, rec.cpu(), group=self.group)
                 parts.copy_(torch.cat(chunks))
@@ -138,7 +138,7 @@ class ShardedGallery:
         k = local_keys if isinstance(local_keys, torch.Tensor) else torch.from_numpy(
             np.ascontiguousarray(local_keys, dtype=np.int64))
         if self.world > 1:
-            if k.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: reduce on host
+            if k.is_cuda and not _device_collectives(self.group):  # gloo: reduce on host
                 t = k.cpu()
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
                 k.copy_(t)
@@ -172,7 +172,7 @@ class ShardedGallery:
         import torch
         import torch.distributed as dist
 
-        if loc.is_cuda and dist.get_backend(self.group) != "nccl":  # gloo: gather on host
+        if loc.is_cuda and not _device_collectives(self.group):  # gloo: gather on host
             parts = [torch.empty_like(loc, device="cpu") for _ in range(self.world)]
             dist.all_gather(parts, loc.cpu(), group=self.group)
             out.copy_(torch.cat(parts))
@@ -246,7 +246,7 @@ class ShardedGallery:
         loc = torch.zeros((c, k), dtype=torch.float32, device=device)
         full = torch.empty((self.world * c, k), dtype=torch.float32, device=device)
         rec = torch.zeros((b, 3), dtype=torch.int64, device=device)
-        gloo = dist.get_backend(self.group) != "nccl"
+        gloo = not _device_collectives(self.group)
         parts = torch.empty((self.world * b, 3), dtype=torch.int64, device=device)
 
         kmin = torch.zeros(b, dtype=torch.int64, device=device)
@@ -273,19 +273,38 @@ class ShardedGallery:
 
 
 # ------------------------------------------------------------------ sharded fit
-def allreduce_fit_stats(pieces, group=None):
+def _device_collectives(group=None):
+    """True when ``group``'s backend reduces device tensors (RCCL, "nccl" on ROCm); every
+    other backend (gloo) reduces host tensors.  The one predicate ShardedGallery and the
+    sharded fit use."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "nccl"
+
+
+def allreduce_fit_stats(pieces, group=None, device=None):
     """Sum the exact integer fit pieces (sum x, sum x^2, X'^T X'; int64) over the ranks of
-    ``group`` in place: an integer sum, so the result is exact in any order.  RCCL takes
-    device tensors directly; gloo reduces host copies.  Of X'^T X' only the upper 64-blocks
-    travel (d % 64 == 0)."""
+    ``group`` in place: an integer sum, so the result is exact in any order.  RCCL reduces
+    device tensors (host pieces — a host X_local — travel through ``device``, default the
+    current GPU, and are copied back); gloo reduces host copies.  Of X'^T X' only the upper
+    64-blocks travel (d % 64 == 0)."""
     import torch
     import torch.distributed as dist
 
-    gloo = dist.get_backend(group) == "gloo"
+    on_device = _device_collectives(group)
+    if on_device and device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
 
     def reduce(t):
-        if gloo and t.is_cuda:
+        if not on_device and t.is_cuda:
             h = t.cpu()
+            dist.all_reduce(h, group=group)
+            t.copy_(h)
+        elif on_device and not t.is_cuda and torch.device(device).type != t.device.type:
+            h = t.to(device)
+            dist.all_reduce(h, group=group)
+            t.copy_(h.cpu())
+        elif on_device and not t.is_cuda:  # (tests: a host "device")
+            h = t.clone()
             dist.all_reduce(h, group=group)
             t.copy_(h)
         else:
@@ -331,11 +350,14 @@ def sharded_fit(engine, X_local, n_components: int, standardize: bool = False, g
     transform_fn = transform_fn or engine.fit_transform_rows
     n_local = int(X_local.shape[0])
     n = torch.tensor([n_local], dtype=torch.int64)
-    if dist.get_backend(group) != "gloo":
-        n = n.to(X_local.device if isinstance(X_local, torch.Tensor) and X_local.is_cuda else "cuda")
+    dev = None
+    if _device_collectives(group):
+        dev = X_local.device if isinstance(X_local, torch.Tensor) and X_local.is_cuda else \
+            torch.device("cuda", torch.cuda.current_device())
+        n = n.to(dev)
     dist.all_reduce(n, group=group)
     n_total = int(n.item())
-    pieces = allreduce_fit_stats(stats_fn(X_local), group)
+    pieces = allreduce_fit_stats(stats_fn(X_local), group, device=dev)
     if not isinstance(X_local, torch.Tensor) or not X_local.is_cuda:
         pieces = [p.cpu().numpy() if isinstance(p, torch.Tensor) else p for p in pieces]
     res = fit_fn(*pieces, n_total, n_components, standardize)

@@ -218,6 +218,18 @@ class Engine:
         """Free the fit workspaces the context keeps between fits (ef_trim)."""
         self._chk(self._lib.ef_trim(self._h))
 
+    def chol_inv(self, G, tol_rel=1e-13, Li=None):
+        """The fit's CholQR factor alone (ef_chol_inv): (Li, info) with Li = L^-1 for
+        G = L L^T (1 <= m <= 256).  On a failed pivot info = -(column + 1) and Li is returned
+        as given (zeros by default)."""
+        G = np.ascontiguousarray(G, dtype=np.float64)
+        m = int(G.shape[0])
+        L = np.zeros((m, m), np.float64) if Li is None else np.array(Li, dtype=np.float64, order="C", copy=True)
+        info = C.c_int32(0)
+        self._chk(self._lib.ef_chol_inv(self._h, G.ctypes.data, m, int(G.shape[1]), float(tol_rel), L.ctypes.data,
+                                        C.byref(info)))
+        return L, int(info.value)
+
     def set_option(self, option, value):
         """Context tunable (include/eigenface.h EF_OPT_*): "fit_max_iters",
         "fit_fp32_coarse", "cov_slab_bytes", "tm_int64_sums", "haar_ordered", "jpeg_chunk_bits",

@@ -132,6 +132,11 @@ int ef_fit_ex(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d,
  * _incremental_mean_and_var form).  var_out may be NULL. */
 int ef_colstats(ef_ctx* ctx, const void* X, int32_t x_dtype, int64_t n, int64_t d, uint32_t flags,
                 double* mean_out, double* var_out);
+/* The fit's CholQR factor alone (API v7): Li = L^-1 (row-major, zeros above the diagonal)
+ * for G = L L^T, 1 <= m <= 256, G row-major with row stride ldg >= m; host pointers.  A
+ * pivot <= tol_rel * max diag(G) sets *info = -(column + 1) and leaves Li as given;
+ * *info = 0 on success. */
+int ef_chol_inv(ef_ctx* ctx, const double* G, int32_t m, int64_t ldg, double tol_rel, double* Li, int32_t* info);
 
 /* ---------------------------------------------------- sample-sharded fit (API v6)
  * The fit collective of SURVEY §8(e): rank r holds uint8 rows X_r (n_r x d) on its GPU.

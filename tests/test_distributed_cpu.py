@@ -395,3 +395,37 @@ def test_sharded_fit_pieces_allreduce(world):
     proj = np.concatenate([out[r][2] for r in range(world)])
     z = (x.astype(np.float64) - ref.mean) / ref.scale
     np.testing.assert_allclose(proj, z @ ref.components.T, atol=1e-9)
+
+
+def test_fit_stats_allreduce_routes_host_pieces_for_device_backends(monkeypatch):
+    """with a device-collective backend (RCCL, "nccl" on ROCm) the host
+    pieces of a host X_local must travel through the device instead of being handed to
+    all_reduce as CPU tensors (which RCCL rejects), and come back summed; with gloo, device
+    pieces reduce through host copies.  One predicate (_device_collectives) decides for
+    the gallery and the fit.  Backend and all_reduce are mocked (x2 = a two-rank sum)."""
+    _paths()
+    import torch
+    import torch.distributed as dist
+    from eigenface import distributed as D
+    seen = []
+
+    def fake_all_reduce(t, group=None, op=None):
+        seen.append(t.device.type)
+        t.mul_(2)
+
+    monkeypatch.setattr(dist, "all_reduce", fake_all_reduce)
+    for backend, expect in (("nccl", True), ("gloo", False)):
+        monkeypatch.setattr(dist, "get_backend", lambda group=None, b=backend: b)
+        assert D._device_collectives() is expect
+        seen.clear()
+        sx = np.arange(128, dtype=np.int64)
+        gram = np.arange(128 * 128, dtype=np.int64).reshape(128, 128)
+        out = D.allreduce_fit_stats([sx.copy(), gram.copy()], device="cpu")
+        np.testing.assert_array_equal(out[0].numpy(), 2 * sx)
+        iu = np.triu_indices(2)
+        blocks = out[1].numpy().reshape(2, 64, 2, 64).transpose(0, 2, 1, 3)
+        ref = gram.reshape(2, 64, 2, 64).transpose(0, 2, 1, 3)
+        for a, b in zip(*iu):  # the upper 64-blocks travel (and come back summed)
+            np.testing.assert_array_equal(blocks[a, b], 2 * ref[a, b])
+        np.testing.assert_array_equal(blocks[1, 0], ref[1, 0])  # the lower block stays local
+        assert seen == ["cpu", "cpu"]

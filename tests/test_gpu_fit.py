@@ -477,3 +477,37 @@ def test_device_tensors_outlive_a_closed_engine():
                          cwd=__import__("conftest").ROOT)
     assert res.returncode == 0, (res.returncode, res.stderr[-2000:])
     assert res.stdout.strip().startswith("ok")
+
+
+@pytest.mark.parametrize("m", [1, 15, 17, 100, 255, 256])
+def test_chol_inv_blocked_vs_fp64(eng, m):
+    """the blocked CholQR factor (ef_chol_blk.hip, the default for every
+    fit at m <= 256) checked directly, for odd orders and orders that pad the diagonal to a
+    multiple of 16: Li equals numpy's fp64 inv(cholesky(G)) to 1e-12 of its scale, is lower
+    triangular, and Li G Li^T = I to 1e-12."""
+    rng = np.random.default_rng(m)
+    A = rng.standard_normal((m + 12, m)) * np.geomspace(1.0, 1e-2, m)  # condition ~1e4
+    G = A.T @ A
+    Li, info = eng.chol_inv(G)
+    assert info == 0
+    ref = np.linalg.inv(np.linalg.cholesky(G))
+    np.testing.assert_allclose(Li, ref, rtol=0, atol=1e-12 * np.abs(ref).max())
+    assert np.all(np.triu(Li, 1) == 0.0)
+    np.testing.assert_allclose(Li @ G @ Li.T, np.eye(m), rtol=0, atol=1e-10)  # ~ eps x cond(G) = 1e-12
+
+
+@pytest.mark.parametrize("m,j", [(17, 9), (64, 0), (256, 200)])
+def test_chol_inv_failed_pivot_leaves_li(eng, m, j):
+    """The failed-pivot contract tri_inv_blk_kernel and the subspace iteration rely on:
+    the first pivot <= tol x max diag(G) gives info = -(column + 1), and Li is left exactly
+    as the caller gave it."""
+    rng = np.random.default_rng(m + j)
+    A = rng.standard_normal((m + 12, m))
+    G = A.T @ A
+    # make column j's pivot G[j,j] - |L^-1 G[:j, j]|^2 negative, leaving columns < j valid
+    piv = G[j, j] - (np.sum(np.linalg.solve(np.linalg.cholesky(G[:j, :j]), G[:j, j]) ** 2) if j else 0.0)
+    G[j, j] -= piv + 1.0
+    sentinel = np.full((m, m), 7.25)
+    Li, info = eng.chol_inv(G, Li=sentinel)
+    assert info == -(j + 1)
+    np.testing.assert_array_equal(Li, sentinel)
