@@ -325,7 +325,11 @@ __global__ __launch_bounds__(512, 1) void project_bf16_wide_kernel(const uint8_t
 // Barriers are LDS-only (lgkmcnt(0) + s_barrier), so the B ring's loads stay in flight.
 __device__ __forceinline__ void frag_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int NT, int WK>
+// ML: round(mean)'s bytes of the split (pps <= kFragMeanLds) are copied into LDS once, so
+// the stage loop issues only pixel and fragment loads (the 512 threads' per-stage mean loads
+// were 2 of every 20 vector-memory instructions, all for the same 128 bytes).
+constexpr int kFragMeanLds = 16384;
+template <int NT, int WK, bool ML>
 __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t* __restrict__ P, int64_t b, int64_t d,
                                                                    const uint8_t* __restrict__ mean_u8,
                                                                    const uint4* __restrict__ Wf, int ldw,
@@ -342,6 +346,7 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
   constexpr int RD = 4;                // B ring depth (k-steps in flight)
   static_assert(NG * MG == 8 && PT % 16 == 0 && TPR >= 1 && SUB % RD == 0, "frag tile");
   __shared__ __attribute__((aligned(16))) unsigned short sA[2][RM * WS];
+  __shared__ __attribute__((aligned(16))) uint8_t sMean[ML ? kFragMeanLds : 16];
 
   // XCD-aware deal (as the wide kernel): XCD x takes the contiguous run of (split, m-tile,
   // n-tile) items [x * per, (x + 1) * per), split-major, so one K split's Wf slice streams
@@ -381,14 +386,16 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       r.p[v] = *reinterpret_cast<const uint4*>(pa + px0 + 16 * v);
-      r.m[v] = *reinterpret_cast<const uint4*>(mean_u8 + px0 + sh + 16 * v);
+      if constexpr (!ML) r.m[v] = *reinterpret_cast<const uint4*>(mean_u8 + px0 + sh + 16 * v);
     }
   };
-  auto convert_store = [&](const Raw& r, int buf) {
+  auto convert_store = [&](const Raw& r, int step, int buf) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const unsigned pw[4] = {r.p[v].x, r.p[v].y, r.p[v].z, r.p[v].w};
-      const unsigned mw[4] = {r.m[v].x, r.m[v].y, r.m[v].z, r.m[v].w};
+      uint4 mq = r.m[v];
+      if constexpr (ML) mq = *reinterpret_cast<const uint4*>(sMean + step * WK + sh + 16 * v);
+      const unsigned mw[4] = {mq.x, mq.y, mq.z, mq.w};
       unsigned pk[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -427,11 +434,16 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
 
   // (the host guarantees nsteps >= 1: splits are whole 64-pixel stages of d % 64 == 0)
   Raw r0, r1;
+  if constexpr (ML) {
+    for (int i = tid * 16; i < (int)(k_end - k_beg); i += 512 * 16)
+      *reinterpret_cast<uint4*>(sMean + i) = *reinterpret_cast<const uint4*>(mean_u8 + k_beg + i);
+    __syncthreads();
+  }
   load_raw(0, r0);
 #pragma unroll
   for (int g = 0; g < RD; ++g) load_b(g < nsub ? g : nsub - 1, ring[g]);
   load_raw(nsteps > 1 ? 1 : 0, r1);
-  convert_store(r0, 0);
+  convert_store(r0, 0, 0);
   frag_lds_barrier();
   const unsigned short* arow_lds = &sA[0][(mg * 128 + c32) * WS + 8 * h];
   auto read_a = [&](int buf, int s, bf16x8 (&a)[4]) {
@@ -474,7 +486,7 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
         for (int i = 0; i < 4; ++i) acur[i] = anxt[i];
       }
     }
-    convert_store(cv, buf ^ 1);  // stage st + 1 (after the last stage: a buffer nobody reads)
+    convert_store(cv, st + 1 < nsteps ? st + 1 : st, buf ^ 1);  // stage st + 1 (after the last: unread)
     frag_lds_barrier();
   };
   int st = 0;
@@ -668,12 +680,17 @@ hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_
       hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 0, s, p8, b, d, mean_u8, wf, ldw, part, bpad, pps, mt,
                          nt, nsplit);
     };
+    bool ml = pps <= kFragMeanLds;
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_MEAN_LDS=0: the per-stage global mean loads (A/B)
+    if (const char* e = getenv("EF_PROJ_MEAN_LDS")) ml = ml && atoi(e) != 0;
+#endif
     if (FWK == 128) {
-      go(project_bf16_frag_kernel<512, 128>);
+      if (ml) go(project_bf16_frag_kernel<512, 128, true>);
+      else go(project_bf16_frag_kernel<512, 128, false>);
     } else {
-      if (NT == 512) go(project_bf16_frag_kernel<512, 64>);
-      else if (NT == 256) go(project_bf16_frag_kernel<256, 64>);
-      else go(project_bf16_frag_kernel<128, 64>);
+      if (NT == 512) go(project_bf16_frag_kernel<512, 64, false>);
+      else if (NT == 256) go(project_bf16_frag_kernel<256, 64, false>);
+      else go(project_bf16_frag_kernel<128, 64, false>);
     }
     return hipGetLastError();
   }
