@@ -329,22 +329,25 @@ __device__ __forceinline__ void frag_lds_barrier() { asm volatile("s_waitcnt lgk
 // the stage loop issues only pixel and fragment loads (the 512 threads' per-stage mean loads
 // were 2 of every 20 vector-memory instructions, all for the same 128 bytes).
 constexpr int kFragMeanLds = 16384;
-template <int NT, int WK, bool ML>
-__global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t* __restrict__ P, int64_t b, int64_t d,
+// NW = 4: a 256-thread workgroup (one wave per SIMD, 128 probes x 256 components at
+// NT = 256), two per CU, so one workgroup's barrier is covered by the other's MFMAs.
+template <int NT, int WK, bool ML, int NW = 8>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void project_bf16_frag_kernel(const uint8_t* __restrict__ P, int64_t b, int64_t d,
                                                                    const uint8_t* __restrict__ mean_u8,
                                                                    const uint4* __restrict__ Wf, int ldw,
                                                                    float* __restrict__ part, int64_t bpad,
                                                                    int64_t pps, int mt, int nt, int ns) {
   constexpr int NG = NT / 64;          // wave columns (64 components each)
-  constexpr int MG = 8 / NG;           // wave rows (128 probes each)
+  constexpr int MG = NW / NG;          // wave rows (128 probes each)
+  constexpr int NTH = 64 * NW;         // threads
   constexpr int RM = 128 * MG;         // probes per workgroup
   constexpr int SUB = WK / 16;         // MFMA k-steps per stage
   constexpr int WS = WK + 8;           // LDS row stride (bf16): conflict-free ds_read_b128 / ds_write_b128
-  constexpr int PT = RM * WK / 512;    // pixels per thread per stage
+  constexpr int PT = RM * WK / NTH;    // pixels per thread per stage
   constexpr int TPR = WK / PT;         // threads per probe row
   constexpr int NV = PT / 16;          // uint4 of raw pixels per thread per stage
   constexpr int RD = 4;                // B ring depth (k-steps in flight)
-  static_assert(NG * MG == 8 && PT % 16 == 0 && TPR >= 1 && SUB % RD == 0, "frag tile");
+  static_assert(NG * MG == NW && PT % 16 == 0 && TPR >= 1 && SUB % RD == 0, "frag tile");
   __shared__ __attribute__((aligned(16))) unsigned short sA[2][RM * WS];
   __shared__ __attribute__((aligned(16))) uint8_t sMean[ML ? kFragMeanLds : 16];
 
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(512, 1) void project_bf16_frag_kernel(const uint8_t
   // (the host guarantees nsteps >= 1: splits are whole 64-pixel stages of d % 64 == 0)
   Raw r0, r1;
   if constexpr (ML) {
-    for (int i = tid * 16; i < (int)(k_end - k_beg); i += 512 * 16)
+    for (int i = tid * 16; i < (int)(k_end - k_beg); i += NTH * 16)
       *reinterpret_cast<uint4*>(sMean + i) = *reinterpret_cast<const uint4*>(mean_u8 + k_beg + i);
     __syncthreads();
   }
@@ -603,34 +606,46 @@ hipError_t launch_mean_u8(hipStream_t s, const float* mean_r, int64_t d, uint8_t
   return hipGetLastError();
 }
 
-// Frag-form column tile: the widest of 512 / 256 / 128 dividing ldw
-static int frag_nt(int ldw) { return ldw % 512 == 0 ? 512 : ldw % 256 == 0 ? 256 : 128; }
 static bool use_frag(const void* Wf) {
 #ifdef EF_DIAGNOSTICS  // EF_PROJ_FRAG=0: round 5's wide kernel (A/B)
   if (const char* e = getenv("EF_PROJ_FRAG")) return Wf && atoi(e) != 0;
 #endif
   return Wf != nullptr;
 }
-// frag form: pixels per stage, 128 at NT = 512 (half the barriers per pixel; the
-// 256 / 128-column forms would spill or exceed the LDS at 128), else 64
-static int frag_wk(int NT, int64_t d) {
-  if (NT != 512 || d % 128 != 0) return 64;  // (every split a whole number of stages)
-#ifdef EF_DIAGNOSTICS  // EF_PROJ_WK=64|128 (A/B)
-  if (const char* e = getenv("EF_PROJ_WK")) return atoi(e) == 64 ? 64 : 128;
+// Frag-form launch shape: column tile NT (the widest of 512 / 256 / 128 dividing ldw),
+// waves per workgroup NW (8, or 4 with two workgroups per CU), pixels per stage WK (128 at
+// NT = 512: half the barriers per pixel; the 256 / 128-column forms would spill or exceed
+// the LDS at 128), probes per workgroup RM, workgroups per CU.
+struct FragCfg {
+  int NT, NW, WK, RM, per_cu;
+};
+static FragCfg frag_cfg(int ldw, int64_t d) {
+  FragCfg c;
+  c.NT = ldw % 512 == 0 ? 512 : ldw % 256 == 0 ? 256 : 128;
+  c.NW = 8;
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_NW=4: 256-thread workgroups of 128 x 256, two per CU (A/B)
+  if (const char* e = getenv("EF_PROJ_NW"))
+    if (atoi(e) == 4 && ldw % 256 == 0) c.NT = 256, c.NW = 4;
 #endif
-  return 128;
+  c.WK = (c.NT == 512 && c.NW == 8 && d % 128 == 0) ? 128 : 64;  // (every split whole stages)
+#ifdef EF_DIAGNOSTICS  // EF_PROJ_WK=64: 64-pixel stages at 512 columns (A/B)
+  if (const char* e = getenv("EF_PROJ_WK"))
+    if (atoi(e) == 64) c.WK = 64;
+#endif
+  c.RM = 128 * (c.NW / (c.NT / 64));
+  c.per_cu = c.NW == 4 ? 2 : 1;
+  return c;
 }
 
 int project_bf16_nsplit(int p_dtype, const void* P, const uint8_t* mean_u8, const void* Wf, int64_t bpad, int64_t d,
                         int ldw, int64_t* pix_per_split) {
   const int64_t steps = (d + HK - 1) / HK;
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8) && use_frag(Wf)) {
-    const int NT = frag_nt(ldw);
-    const int64_t RM = 128 * (8 / (NT / 64));
-    const int FWK = frag_wk(NT, d);
+    const FragCfg fc = frag_cfg(ldw, d);
+    const int FWK = fc.WK;
     const int64_t wsteps = d / FWK;
-    const int64_t tiles = (bpad + RM - 1) / RM * (ldw / NT);
-    int64_t ns = (256 + tiles - 1) / tiles;  // one workgroup per CU
+    const int64_t tiles = (bpad + fc.RM - 1) / fc.RM * (ldw / fc.NT);
+    int64_t ns = (256 * fc.per_cu + tiles - 1) / tiles;  // every CU busy
     if (ns > wsteps) ns = wsteps;
     if (ns < 1) ns = 1;
     while ((tiles * ns) % 8 != 0 && ns < wsteps) ++ns;
@@ -667,30 +682,33 @@ hipError_t launch_project_bf16(hipStream_t s, int p_dtype, const void* P, int64_
                                const void* Wf, int ldw, float* part, int nsplit, int64_t pps) {
   if (ldw % HN != 0) return hipErrorInvalidValue;
   if (bf16_wide_ok(p_dtype, P, d, ldw, mean_u8) && use_frag(Wf)) {
-    const int NT = frag_nt(ldw);
-    const int64_t RM = 128 * (8 / (NT / 64));
+    const FragCfg fc = frag_cfg(ldw, d);
+    const int NT = fc.NT;
     const int nt = ldw / NT;
-    const int mt = (int)((bpad + RM - 1) / RM);
+    const int mt = (int)((bpad + fc.RM - 1) / fc.RM);
     const int grid = (mt * nt * nsplit + 7) / 8 * 8;
-    const int FWK = frag_wk(NT, d);
+    const int FWK = fc.WK;
     if (pps % FWK != 0) return hipErrorInvalidValue;
     const uint8_t* p8 = static_cast<const uint8_t*>(P);
     const uint4* wf = static_cast<const uint4*>(Wf);
-    auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 0, s, p8, b, d, mean_u8, wf, ldw, part, bpad, pps, mt,
-                         nt, nsplit);
+    auto go = [&](auto kern, int threads) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), 0, s, p8, b, d, mean_u8, wf, ldw, part, bpad, pps,
+                         mt, nt, nsplit);
     };
     bool ml = pps <= kFragMeanLds;
 #ifdef EF_DIAGNOSTICS  // EF_PROJ_MEAN_LDS=0: the per-stage global mean loads (A/B)
     if (const char* e = getenv("EF_PROJ_MEAN_LDS")) ml = ml && atoi(e) != 0;
 #endif
-    if (FWK == 128) {
-      if (ml) go(project_bf16_frag_kernel<512, 128, true>);
-      else go(project_bf16_frag_kernel<512, 128, false>);
+    if (fc.NW == 4) {
+      if (ml) go(project_bf16_frag_kernel<256, 64, true, 4>, 256);
+      else go(project_bf16_frag_kernel<256, 64, false, 4>, 256);
+    } else if (FWK == 128) {
+      if (ml) go(project_bf16_frag_kernel<512, 128, true>, 512);
+      else go(project_bf16_frag_kernel<512, 128, false>, 512);
     } else {
-      if (NT == 512) go(project_bf16_frag_kernel<512, 64, false>);
-      else if (NT == 256) go(project_bf16_frag_kernel<256, 64, false>);
-      else go(project_bf16_frag_kernel<128, 64, false>);
+      if (NT == 512) go(project_bf16_frag_kernel<512, 64, false>, 512);
+      else if (NT == 256) go(project_bf16_frag_kernel<256, 64, false>, 512);
+      else go(project_bf16_frag_kernel<128, 64, false>, 512);
     }
     return hipGetLastError();
   }
