@@ -714,10 +714,11 @@ def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
            "host_parse_ms": round(h_ms / reps, 3), "host_parts_per_batch": round(h_n / reps, 2),
            "host_threads": _host_threads(), "upload_MB_per_batch": round(nbytes / 1e6, 1),
            "note": "a batch's host staging (host_parse_ms: marker parse + destuff into the pinned slot + tables, "
-                   "on the job's CPU share) and then its upload (the destuffed entropy words, ~the file bytes, "
-                   "over PCIe) must both finish before its decode starts; their sum runs within ~10 % of the "
-                   "device time, so the stream runs at the larger of the two chains plus jitter — the gap "
-                   "between ms_per_batch and decode + resize is that chain, not a device wait",
+                   "on the job's CPU share) and its upload (the destuffed entropy words, ~the file bytes, over "
+                   "PCIe, sent in 4 pieces while the batch is still being destuffed) must both finish before its "
+                   "decode starts; that chain runs close to the device time (decode + resize), so the stream "
+                   "runs at the larger of the two plus jitter — the gap between ms_per_batch and decode + "
+                   "resize is that chain, not a device wait",
            "file_MBs": round(nbytes / wall / 1e6, 1)}
     if with_cpu:
         import io as _io

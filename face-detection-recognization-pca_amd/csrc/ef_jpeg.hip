@@ -1478,8 +1478,9 @@ void destuff(const uint8_t* src, int64_t n, JSeg& sg, uint8_t* dst) {
   sg.nbits = (int)(o * 8);
 }
 
-void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* words) {
-  const size_t n = B.segs.size();
+// segments [s0, s1) of the batch (all of them: destuff_all)
+void destuff_range(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* words, size_t s0, size_t s1) {
+  const size_t n = s1 - s0;
   auto work = [&](size_t a, size_t e) {
     for (size_t k = a; k < e; ++k) {
       JSeg& sg = B.segs[k];
@@ -1487,9 +1488,12 @@ void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t*
       destuff(file + sg.beg, sg.end - sg.beg, sg, words + sg.word_off * 4);
     }
   };
-  const int64_t bytes = B.words * 4;
+  const int64_t bytes = ((s1 < B.segs.size() ? B.segs[s1].word_off : B.words) - (n ? B.segs[s0].word_off : 0)) * 4;
   const size_t nt = bytes < ((int64_t)4 << 20) ? 1 : std::min<size_t>((size_t)host_threads(), n);
-  host_parallel((int)nt, [&](int t) { work(n * t / nt, n * (t + 1) / nt); });
+  host_parallel((int)nt, [&](int t) { work(s0 + n * t / nt, s0 + n * (t + 1) / nt); });
+}
+void destuff_all(Batch& B, const uint8_t* data, const int64_t* offsets, uint8_t* words) {
+  destuff_range(B, data, offsets, words, 0, B.segs.size());
 }
 
 // Chunk size: about 128k chunks for the batch (4 per SIMD lane group of the chip), kept in
@@ -1519,14 +1523,24 @@ struct Staged {
   char* h = nullptr;
   size_t o_words = 0, o_imgs = 0, o_pool = 0, o_q = 0, o_seg = 0, o_bs = 0, o_ic = 0, o_ps = 0, o_desc = 0, o_cseg = 0;
   size_t pin_need = 0, up_bytes = 0;
+  size_t words_up = 0;  // leading bytes already uploaded into the device slot (early upload)
 };
 
 // Host half of a decode: size / allocate pinned slot `slot` (waiting for the upload that last
 // read it), destuff the entropy segments into it, copy the tables, cut the chunks.  Touches
 // only this slot and B, so it may run on a host thread while another slot's batch decodes.
 // Returns EF_OK, or an error code with the message in *err (the caller records it).
+int jpeg_ensure(ef_ctx* c, DevBuf& b, size_t bytes);
+hipError_t jpeg_event(hipEvent_t* ev, hipStream_t record_on);
+constexpr int kUploadPhases = 4;  // early upload: destuff + upload pieces per batch
+bool jpeg_early_upload() {
+#ifdef EF_DIAGNOSTICS  // EF_JPEG_EARLY_UP=0: the whole upload after staging, round 5's order (A/B)
+  if (const char* e = getenv("EF_JPEG_EARLY_UP")) return atoi(e) != 0;
+#endif
+  return true;
+}
 int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_t* offsets, Staged& S,
-                std::string* err, int64_t chunk_bits = 0) {
+                std::string* err, int64_t chunk_bits = 0, bool early_upload = false) {
   StageTimer tm;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t off = 0;
@@ -1566,7 +1580,31 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
   char* h = static_cast<char*>(c->jpeg_pinned[slot]);
   S.h = h;
   tm.mark("pinned");
-  destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + S.o_words));
+  S.words_up = 0;
+  // The destuffed words go up in kUploadPhases pieces as they are produced (copy stream,
+  // behind the kernels that last read this device slot), so a batch's upload overlaps its
+  // own destuffing instead of following the whole host staging; launch_batch uploads the
+  // rest (padding, tables, chunk table).  Only into a device slot already large enough
+  // (launch_batch sizes slots by pin_need; this may run on a staging thread, which must
+  // not reallocate): the first call at a new size uploads whole, as without early upload.
+  if (early_upload && c->jpeg_copy && !B.segs.empty() && c->jpeg_up[slot].p &&
+      c->jpeg_up[slot].bytes >= S.pin_need + 16) {
+    hipError_t e = jpeg_event(&c->jpeg_ws_free[slot], c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->jpeg_copy, c->jpeg_ws_free[slot], 0);
+    char* up = static_cast<char*>(c->jpeg_up[slot].p);
+    const size_t nseg = B.segs.size();
+    for (int ph = 0; ph < kUploadPhases && e == hipSuccess; ++ph) {
+      const size_t a = nseg * ph / kUploadPhases, b = nseg * (ph + 1) / kUploadPhases;
+      if (a == b) continue;
+      destuff_range(B, data, offsets, reinterpret_cast<uint8_t*>(h + S.o_words), a, b);
+      const size_t w0 = (size_t)B.segs[a].word_off * 4, w1 = (size_t)(b < nseg ? B.segs[b].word_off : B.words) * 4;
+      e = hipMemcpyAsync(up + S.o_words + w0, h + S.o_words + w0, w1 - w0, hipMemcpyHostToDevice, c->jpeg_copy);
+    }
+    if (e != hipSuccess) { *err = hipGetErrorString(e); return EF_E_HIP; }
+    S.words_up = S.o_words + (size_t)B.words * 4;
+  } else {
+    destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + S.o_words));
+  }
   tm.mark("destuff");
   make_chunks(B, c->opt_jpeg_chunk_bits > 0 ? c->opt_jpeg_chunk_bits : chunk_bits);
   std::memcpy(h + S.o_imgs, B.imgs.data(), B.imgs.size() * sizeof(JImage));
@@ -1632,7 +1670,7 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
   if (e != hipSuccess) return hip_err(c, e, "jpeg decode");
   {
     int rc = jpeg_ensure(c, c->jpeg_ws, off);
-    if (rc == EF_OK) rc = jpeg_ensure(c, c->jpeg_up[slot], S.up_bytes + 16);
+    if (rc == EF_OK) rc = jpeg_ensure(c, c->jpeg_up[slot], std::max(S.pin_need, S.up_bytes) + 16);
     if (rc != EF_OK) return rc;
   }
   char* up = static_cast<char*>(c->jpeg_up[slot].p);
@@ -1641,7 +1679,8 @@ int launch_batch(ef_ctx* c, Batch& B, const Staged& S, uint8_t* dout, uint8_t* r
   // the compute stream waits for it and for the previous decode (shared workspace)
   hipStream_t cs = c->jpeg_copy;
   e = hipStreamWaitEvent(cs, c->jpeg_ws_free[slot], 0);
-  if (e == hipSuccess) e = hipMemcpyAsync(up, S.h, S.up_bytes, hipMemcpyHostToDevice, cs);
+  if (e == hipSuccess)  // (the words went up already with an early upload: the rest)
+    e = hipMemcpyAsync(up + S.words_up, S.h + S.words_up, S.up_bytes - S.words_up, hipMemcpyHostToDevice, cs);
   if (e == hipSuccess) e = hipEventRecord(c->jpeg_up_done[slot], cs);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, c->jpeg_up_done[slot], 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, c->jpeg_done, 0);
@@ -1820,6 +1859,10 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     return set_err(c, EF_E_INVALID, "ef_jpeg_ingest: bad arguments");
   if (count == 0) return EF_OK;
   (void)hipSetDevice(c->device);
+  if (!c->jpeg_copy) {  // (created here, before any staging thread can use it)
+    const hipError_t e = hipStreamCreateWithFlags(&c->jpeg_copy, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_err(c, e, "jpeg ingest");
+  }
   const int64_t row = (int64_t)out_h * out_w;
   // Parts of ~kIngestPart files, each staged (parse, destuff, tables, chunks, file -> image
   // map) into one of the context's two upload slots, the next part on a host thread
@@ -1856,7 +1899,7 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
     Batch& B = P.B;
     B.file_img.assign((size_t)P.m, -1);  // file j of the part -> row j
     for (size_t q = 0; q < B.imgs.size(); ++q) B.file_img[(size_t)B.img_of[q]] = (int)q;
-    P.rc = stage_batch(c, P.slot, B, data, offsets + P.a, P.S, &P.err, call_chunk_bits);
+    P.rc = stage_batch(c, P.slot, B, data, offsets + P.a, P.S, &P.err, call_chunk_bits, jpeg_early_upload());
   };
   for (int32_t a0 = 0; a0 < count; a0 += 65535) {  // the resize launch's per-launch image limit
     const int32_t m0 = std::min<int32_t>(65535, count - a0);
