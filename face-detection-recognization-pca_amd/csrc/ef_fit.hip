@@ -349,6 +349,19 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     else
       cvt64to32(s, C, dim * dim, C32);
   }
+  // fp64-accuracy products on the int8 matrix cores (launch_cq_i8: C and Q in base-256
+  // digits, 21 exact digit-pair products): the row planes of C once, at the first fine
+  // product.
+  bool cq_i8 = cq_i8_supported(dim, m) && tall_gemm_supported(dim, C, 8);
+#ifdef EF_DIAGNOSTICS  // EF_FIT_CQ_I8=0: the fp64 MFMA product (A/B)
+  if (const char* e = getenv("EF_FIT_CQ_I8")) cq_i8 = cq_i8 && atoi(e) != 0;
+#endif
+  uint8_t *cq_planes = nullptr, *cq_work = nullptr;
+  bool cq_ready = false;
+  if (cq_i8) {
+    EF_TRY(B.get(c, cq_i8_plane_bytes(dim), &cq_planes));
+    EF_TRY(B.get(c, cq_i8_work_bytes(dim, m), &cq_work));
+  }
   std::vector<double> th(m), prev(m, 0.0);
   bool have_prev = false, prev_fine = false;
   // Spectral shift: the iteration multiplies by C - sigma I.  Convergence of eigenpair i
@@ -405,6 +418,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
                               kWorkElems * 2),
              "Y = C.Q (fp32)");
       hipLaunchKernelGGL(f32_to_f64_shift_kernel, dim3(ew_blocks), dim3(256), 0, s, Y32, Q, dim * m, sigma, Y);
+    } else if (cq_i8) {
+      if (!cq_ready) EF_HIP(c, launch_cq_i8_planes(s, C, dim, cq_planes), "C (int8 digit planes)");
+      cq_ready = true;
+      EF_HIP(c, launch_cq_i8(s, cq_planes, dim, Q, m, sigma, cq_work, Y), "Y = C.Q (int8 digits)");
     } else {
       EF_HIP(c, dense_gemm(c, s, Operand::symmetric(C, dim), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
                            kWorkElems, Bt),

@@ -210,6 +210,15 @@ bool proj_i8_supported(const uint8_t* X, int64_t n, int64_t d, int kk);
 size_t proj_i8_work_bytes(int64_t n, int64_t d, int kk);
 hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, const double* mu, const double* w,
                           const double* E, int kk, void* work, double* F);
+// The fit's fine-phase product Y = C.Q - sigma Q (C symmetric dim x dim, Q dim x m) on the
+// int8 matrix cores with C and Q cut into base-256 digits (ef_proj_i8.hip, launch_cq_i8):
+// planes (cq_i8_plane_bytes) from launch_cq_i8_planes once per C; work: cq_i8_work_bytes.
+bool cq_i8_supported(int64_t dim, int m);
+size_t cq_i8_plane_bytes(int64_t dim);
+size_t cq_i8_work_bytes(int64_t dim, int m);
+hipError_t launch_cq_i8_planes(hipStream_t s, const double* C, int64_t dim, void* planes);
+hipError_t launch_cq_i8(hipStream_t s, const void* planes, int64_t dim, const double* Q, int m, double sigma,
+                        void* work, double* Y);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 // Float input (EF_F32 / EF_F64): column mean and population variance in fp64 by two
