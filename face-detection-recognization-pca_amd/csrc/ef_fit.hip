@@ -572,10 +572,19 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
         // it should be met (an earlier step would also restart the recurrence and lose the
         // acceleration).  p Chebyshev products shrink the slowest kept vector's residual by
         // T_p(x) = cosh(p acosh x), x = theta_k / sigma - 1; a factor 2 of margin.  (C3: the
-        // steps at 23 and 24 that the value rule placed are skipped, 22 -> 25.)
+        // steps at 23 and 24 that the value rule placed are skipped, 22 -> 25.  The
+        // asymptotic rate rho^p >= 1.5 need — diagnostic EF_FIT_GAP_MARGIN=1.5 — placed the
+        // step at 24, where the residual had shrunk only 5.2x, not rho^2 = 11x, right after
+        // the restart: 1.345e-5 of the gap, one more step, 0.1390 vs 0.1378 s;
+        // profiles/r06/fit_gap_sched_ab.txt.)
         if (gap_need > 1.0 && rate_next > 0.0 && !coarse) {
           const double x = th[kk - 1] / sig_next - 1.0;
-          int p = (int)std::ceil(std::acosh(2.0 * gap_need) / std::acosh(x));
+          double margin = 0.0;
+#ifdef EF_DIAGNOSTICS  // EF_FIT_GAP_MARGIN (A/B; > 0: p = log(margin need) / log(rho))
+          if (const char* e = getenv("EF_FIT_GAP_MARGIN")) margin = atof(e);
+#endif
+          int p = margin > 0.0 ? (int)std::ceil(std::log(margin * gap_need) / std::log(x + std::sqrt(x * x - 1.0)))
+                               : (int)std::ceil(std::acosh(2.0 * gap_need) / std::acosh(x));
           next_rr = std::max(next_rr, it + std::max(p, 1));
         }
       }
