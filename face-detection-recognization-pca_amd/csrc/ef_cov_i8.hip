@@ -447,7 +447,11 @@ __device__ __forceinline__ int syrk16_swz(int b) { return (0x78 >> (2 * b)) & 3;
 #define EF_S16_HI 3
 #endif
 
-template <int NJB, int NB>
+// OZ (the fit's int8 digit-pair products, ef_cq_i8.hip; NJB = 4: 256 x 256 items): At is
+// the digits' K-blocked array of `dim` = R rows, kps the order of C (odim), ntiles the row
+// blocks per XCD, [st_begin, st_end) all K stages; items per XCD: its row blocks' 20 whole
+// pairs, then the 4 K-parts of pair (0, 5); each writes its pair block of slabs (odim x 256).
+template <int NJB, int NB, bool OZ = false>
 __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                            int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
                                                            int nitems, const int2* __restrict__ order,
@@ -461,13 +465,42 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
   const int total = gridDim.x;
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
   if (lin >= nitems) return;
-  const int ks = lin / ntiles;
-  const int2 tt = order[lin - ks * ntiles];
-  const int64_t i0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.x) * YT;
-  const int64_t j0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.y) * TJ;
-  const int64_t sb = st_begin + ks * kps;
-  const int64_t se = sb + kps < st_end ? sb + kps : st_end;
-  const int64_t nst = se > sb ? se - sb : 0;
+  int64_t i0, j0, sb, nst;
+  int ks = 0;
+  int64_t oz_row0 = 0;  // OZ: the item's first output row
+  if constexpr (OZ) {
+    const int64_t odim = kps;
+    const int per = total >> 3, x = lin / per, r = lin - x * per;
+    int p, mt;
+    sb = st_begin;
+    nst = st_end - st_begin;
+    if (r < ntiles * kOzPairsWhole) {
+      mt = x * ntiles + r / kOzPairsWhole;
+      p = r % kOzPairsWhole;
+      ks = p;
+    } else {
+      const int r2 = r - ntiles * kOzPairsWhole;
+      mt = x * ntiles + r2 / kOzSplitParts;
+      const int part = r2 % kOzSplitParts;
+      p = kOzPairsWhole;
+      ks = p + part;
+      sb = st_begin + nst * part / kOzSplitParts;
+      nst = st_begin + nst * (part + 1) / kOzSplitParts - sb;
+    }
+    int a, b;
+    oz_pair(p, a, b);
+    i0 = (int64_t)a * odim + (int64_t)mt * YT;
+    j0 = 6 * odim + (int64_t)b * TJ;
+    oz_row0 = (int64_t)mt * YT;
+  } else {
+    ks = lin / ntiles;
+    const int2 tt = order[lin - ks * ntiles];
+    i0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.x) * YT;
+    j0 = (int64_t)__builtin_amdgcn_readfirstlane(tt.y) * TJ;
+    sb = st_begin + ks * kps;
+    const int64_t se = sb + kps < st_end ? sb + kps : st_end;
+    nst = se > sb ? se - sb : 0;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -555,6 +588,21 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
       __builtin_amdgcn_sched_barrier(0);
     }
     dma_wait_all();
+  }
+  if constexpr (OZ) {
+    int* out = slabs + (int64_t)ks * kps * TJ;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJB; ++j) {
+        const int col = wn * 16 * NJB + j * 16 + r16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = oz_row0 + wm * 128 + i * 16 + 4 * (lane >> 4) + r;
+          out[row * TJ + col] = acc[i][j][r];
+        }
+      }
+    return;
   }
   int* out = slabs + (int64_t)ks * dim * dim;
 #pragma unroll
@@ -942,6 +990,16 @@ hipError_t launch_cov_from_cross(hipStream_t s, const long long* S64, const unsi
   hipLaunchKernelGGL(shifted_sums_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, S1, n, d, cvec);
   hipLaunchKernelGGL(d % 4 == 0 ? cov_finalize4_kernel : cov_finalize_kernel, dim3((unsigned)nfb, (unsigned)nfb),
                      dim3(256), 0, s, nullptr, 0, S64, d, n, 0, cvec, nullptr, nullptr, w, C);
+  return hipGetLastError();
+}
+
+// The fit's digit-pair products (ef_cq_i8.hip): 64 row blocks of 256 x 24 items at C3
+hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I) {
+  if (dim % 2048 != 0) return hipErrorInvalidValue;
+  const int nrb = (int)(dim / YT);
+  const int nitems = nrb * kOzBlocks;  // a multiple of 8
+  hipLaunchKernelGGL((syrk16_i8_kernel<4, 4, true>), dim3((unsigned)nitems), dim3(512), 0, s, Z, R, (int64_t)0,
+                     dim / YK, dim, nrb / 8, nitems, nullptr, I);
   return hipGetLastError();
 }
 

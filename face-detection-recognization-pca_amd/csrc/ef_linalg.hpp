@@ -211,14 +211,32 @@ size_t proj_i8_work_bytes(int64_t n, int64_t d, int kk);
 hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d, const double* mu, const double* w,
                           const double* E, int kk, void* work, double* F);
 // The fit's fine-phase product Y = C.Q - sigma Q (C symmetric dim x dim, Q dim x m) on the
-// int8 matrix cores with C and Q cut into base-256 digits (ef_proj_i8.hip, launch_cq_i8):
-// planes (cq_i8_plane_bytes) from launch_cq_i8_planes once per C; work: cq_i8_work_bytes.
+// int8 matrix cores with C and Q cut into base-256 digits (ef_cq_i8.hip, launch_cq_i8):
+// planes (cq_i8_plane_bytes: C's digit planes + room for Q's) from launch_cq_i8_planes once
+// per C; work: cq_i8_work_bytes.
 bool cq_i8_supported(int64_t dim, int m);
 size_t cq_i8_plane_bytes(int64_t dim);
 size_t cq_i8_work_bytes(int64_t dim, int m);
 hipError_t launch_cq_i8_planes(hipStream_t s, const double* C, int64_t dim, void* planes);
-hipError_t launch_cq_i8(hipStream_t s, const void* planes, int64_t dim, const double* Q, int m, double sigma,
-                        void* work, double* Y);
+hipError_t launch_cq_i8(hipStream_t s, void* planes, int64_t dim, const double* Q, int m, double sigma, void* work,
+                        double* Y);
+// Its digit-pair products (ef_cov_i8.hip, syrk16_i8_kernel's OZ items): pair p < 20 is
+// (a, b), a = 5 .. 1 descending, b = 5 - a .. 5; pair (0, 5) runs in kOzSplitParts K-parts
+// (so 64 row blocks x 24 items fill 256 CUs in 5.25 rounds of whole-item time); output
+// block p, then 20 + part, each dim x 256 int32.  Z: the K-blocked [dim/64][R][64] digits.
+constexpr int kOzPairsWhole = 20;
+constexpr int kOzSplitParts = 4;
+constexpr int kOzBlocks = kOzPairsWhole + kOzSplitParts;
+__host__ __device__ inline void oz_pair(int p, int& a, int& b) {
+  a = 5;
+  int base = 0;
+  while (p >= base + a + 1) {
+    base += a + 1;
+    --a;
+  }
+  b = 5 - a + (p - base);
+}
+hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 // Float input (EF_F32 / EF_F64): column mean and population variance in fp64 by two

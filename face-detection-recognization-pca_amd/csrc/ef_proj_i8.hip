@@ -102,31 +102,6 @@ __global__ void cc_kernel(const double* __restrict__ E, const double* __restrict
 #ifndef EF_PROJ_HI
 #define EF_PROJ_HI 3
 #endif
-// Digit pairs of the fit's int8-digit product (launch_cq_i8): plane a of C's row digits
-// against digit b of Q's column digits for every a + b >= kOzDigits - 1, a descending (the
-// pairs of one plane consecutive, so they run together and share its rows in L2).
-constexpr int kOzDigits = 6;   // base-256 digits per operand (largest scaled entry < 2^46)
-constexpr int kOzTop = 46;
-constexpr int kOzPairs = kOzDigits * (kOzDigits + 1) / 2;
-// Work items per row block: the first kOzPairs - 1 pairs whole, the last pair (0, 5) in
-// kOzSplit K-parts (its own output blocks), so a launch of 64 row blocks is 5.25 rounds of
-// whole items on 256 CUs, not 6 (21 x 64 = 1344 = 5.25 x 256; the quarter items fill the
-// last round); blocks: kOzPairs - 1 + kOzSplit.
-constexpr int kOzSplit = 4;
-constexpr int kOzItems = kOzPairs - 1 + kOzSplit;
-constexpr int kOzBlocks = kOzItems;
-__device__ __forceinline__ void oz_pair(int p, int& a, int& b) {
-  a = kOzDigits - 1;
-  int base = 0;
-  while (p >= base + a + 1) {
-    base += a + 1;
-    --a;
-  }
-  b = kOzDigits - 1 - a + (p - base);
-}
-
-// OZ: the work item is (row block, digit pair p = (a, b)); X holds kOzDigits planes of
-// n x d biased digits (digit + 128), D digit b's TN rows, C the pair's own n x ldc block.
 template <int TN, bool OZ = false>
 __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
                                                          const int8_t* __restrict__ D, int ntn, int nblocks,
@@ -141,37 +116,7 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   // major, so the N-tiles of a row block run together and share its X rows in L2
   const int lin = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
   if (lin >= nblocks) return;
-  int mt, nt;
-  int64_t c0 = 0;  // OZ: output columns are the pair block's own
-  int64_t s0 = 0, nst = d / PK;  // K stages of the item
-  if constexpr (OZ) {
-    // per XCD (ntn = row blocks per XCD): its row blocks' whole pairs, then the split parts
-    const int per = total >> 3, x = lin / per, r = lin - x * per;
-    int p, blk;
-    if (r < ntn * (kOzPairs - 1)) {
-      mt = x * ntn + r / (kOzPairs - 1);
-      p = r % (kOzPairs - 1);
-      blk = p;
-    } else {
-      const int r2 = r - ntn * (kOzPairs - 1);
-      mt = x * ntn + r2 / kOzSplit;
-      const int part = r2 % kOzSplit;
-      p = kOzPairs - 1;
-      blk = p + part;
-      const int64_t all = nst;
-      s0 = all * part / kOzSplit;
-      nst = all * (part + 1) / kOzSplit - s0;
-    }
-    int a, b;
-    oz_pair(p, a, b);
-    nt = b;
-    X += (int64_t)a * n * d;
-    C += (int64_t)blk * n * ldc;
-    c0 = (int64_t)b * TN;
-  } else {
-    mt = lin / ntn;
-    nt = lin - mt * ntn;
-  }
+  const int mt = lin / ntn, nt = lin - (lin / ntn) * ntn;
   const int64_t m0 = (int64_t)mt * PM, n0 = (int64_t)nt * TN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -191,10 +136,10 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   for (int jj = 0; jj < 2; ++jj) {
     int64_t ra = m0 + (wave * 2 + jj) * 16 + lrow;
     ra = ra < n ? ra : n - 1;
-    arow[jj] = X + ra * d + s0 * PK + lchunk * 16;
+    arow[jj] = X + ra * d + lchunk * 16;
   }
-  // D is N x d (< 4 GiB)
-  const unsigned voffB = (unsigned)((n0 + wave * BPW * 16 + lrow) * d + s0 * PK + lchunk * 16);
+  const unsigned voffB = (unsigned)((n0 + wave * BPW * 16 + lrow) * d + lchunk * 16);  // D is N x d (< 4 GiB)
+  const int64_t nst = d / PK;
   auto issue = [&](int64_t st, int buf) {
     const unsigned sbuf = lds_base + (unsigned)(buf * PSTAGE);
 #pragma unroll
@@ -281,7 +226,7 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   for (int i = 0; i < IA; ++i)
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
-      const int64_t col = n0 - c0 + wn * 64 + j * 32 + c32;
+      const int64_t col = n0 + wn * 64 + j * 32 + c32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * (PM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -305,171 +250,7 @@ __global__ void proj_combine_kernel(const int* __restrict__ I, int64_t n, int kk
   F[e] = ldexp(v, -tsh[c]) + cc[c];
 }
 
-// Row digits of the fit's covariance (launch_cq_i8_planes): one block per row i of the
-// symmetric C, t_i such that 2^t_i max_k |C[i][k]| lies in [2^45, 2^46), and plane a
-// (a = 0 least significant) of V = rint(2^t_i C[i][k]) written biased (digit + 128: the
-// GEMM's A fragments flip it back to int8).  8 columns per thread and step.
-__global__ __launch_bounds__(256) void oz_rows_kernel(const double* __restrict__ C, int64_t dim,
-                                                      uint8_t* __restrict__ P, int* __restrict__ tr) {
-  const int64_t i = blockIdx.x;
-  const double* row = C + i * dim;
-  double mx = 0.0;
-  for (int64_t k = threadIdx.x; k < dim; k += 256) mx = fmax(mx, fabs(row[k]));
-  __shared__ double red[256];
-  __shared__ int tsh;
-  red[threadIdx.x] = mx;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    int e = 0;
-    if (red[0] > 0.0) (void)frexp(red[0], &e);
-    tsh = red[0] > 0.0 ? kOzTop - e : 0;
-    tr[i] = tsh;
-  }
-  __syncthreads();
-  const int t = tsh;
-  const int64_t plane = dim * dim;
-  for (int64_t k0 = (int64_t)threadIdx.x * 8; k0 < dim; k0 += 256 * 8) {
-    unsigned lo4[kOzDigits], hi4[kOzDigits];
-#pragma unroll
-    for (int a = 0; a < kOzDigits; ++a) lo4[a] = hi4[a] = 0u;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      long long v = (long long)rint(ldexp(row[k0 + q], t));
-#pragma unroll
-      for (int a = 0; a < kOzDigits; ++a) {
-        const long long lo = ((v + 128) & 255) - 128;
-        const unsigned byte = (unsigned)(lo + 128) << (8 * (q & 3));
-        if (q < 4) lo4[a] |= byte;
-        else hi4[a] |= byte;
-        v = (v - lo) / 256;
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < kOzDigits; ++a)
-      *reinterpret_cast<uint2*>(P + a * plane + i * dim + k0) = make_uint2(lo4[a], hi4[a]);
-  }
-}
-
-// Column maxima of Q (dim x m, m = 256 = blockDim): block b folds rows [b dim / G,
-// (b + 1) dim / G) and merges by atomicMax on the bits (non-negative doubles order as
-// their bit patterns); cmax zeroed before.
-__global__ __launch_bounds__(256) void oz_colmax_kernel(const double* __restrict__ Q, int64_t dim, int m,
-                                                        unsigned long long* __restrict__ cmax) {
-  const int c = threadIdx.x;
-  const int64_t r0 = dim * blockIdx.x / gridDim.x, r1 = dim * (blockIdx.x + 1) / gridDim.x;
-  double mx = 0.0;
-  for (int64_t r = r0; r < r1; ++r) mx = fmax(mx, fabs(Q[r * m + c]));
-  atomicMax(cmax + c, (unsigned long long)__double_as_longlong(mx));
-}
-// Q's column digits, K-contiguous: D[(j m + c) dim + r] = digit j of rint(2^u_c Q[r][c]),
-// u_c from the column maximum ([2^45, 2^46)).  Thread (c, 16-row group): reads Q[r][c]
-// coalesced along c, writes 16 digits of each plane as one 16-byte store.
-__global__ __launch_bounds__(256) void oz_qdigits_kernel(const double* __restrict__ Q, int64_t dim, int m,
-                                                         const unsigned long long* __restrict__ cmax,
-                                                         int8_t* __restrict__ D, int* __restrict__ tc) {
-  const int c = threadIdx.x;  // m = 256
-  const int64_t r0 = (int64_t)blockIdx.x * 16;
-  const double mx = __longlong_as_double((long long)cmax[c]);
-  int e = 0;
-  if (mx > 0.0) (void)frexp(mx, &e);
-  const int t = mx > 0.0 ? kOzTop - e : 0;
-  if (blockIdx.x == 0) tc[c] = t;
-  unsigned w[kOzDigits][4];
-#pragma unroll
-  for (int j = 0; j < kOzDigits; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w[j][q] = 0u;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    long long v = (long long)rint(ldexp(Q[(r0 + q) * m + c], t));
-#pragma unroll
-    for (int j = 0; j < kOzDigits; ++j) {
-      const long long lo = ((v + 128) & 255) - 128;
-      w[j][q >> 2] |= (unsigned)(lo & 255) << (8 * (q & 3));
-      v = (v - lo) / 256;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < kOzDigits; ++j)
-    *reinterpret_cast<uint4*>(D + ((int64_t)j * m + c) * dim + r0) = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
-}
-
-// Y[i][c] = 2^(40 - t_i - u_c) sum_{L=0..5} 256^L S_L - sigma Q[i][c], S_L the exact int64
-// sum of the pair products of level a + b = L + 5 (fp64 Horner from the top level)
-__global__ __launch_bounds__(256) void oz_combine_kernel(const int* __restrict__ I, int64_t dim, int m,
-                                                         const int* __restrict__ tr, const int* __restrict__ tc,
-                                                         const double* __restrict__ Q, double sigma,
-                                                         double* __restrict__ Y) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = dim * m;
-  if (e >= total) return;
-  const int64_t i = e / m;
-  const int c = (int)(e - i * m);
-  long long S[kOzDigits];
-#pragma unroll
-  for (int L = 0; L < kOzDigits; ++L) S[L] = 0;
-  int p = 0;
-#pragma unroll
-  for (int a = kOzDigits - 1; a >= 1; --a)
-#pragma unroll
-    for (int b = kOzDigits - 1 - a; b < kOzDigits; ++b, ++p) S[a + b - (kOzDigits - 1)] += I[(int64_t)p * total + e];
-#pragma unroll
-  for (int q = 0; q < kOzSplit; ++q) S[0] += I[(int64_t)(p + q) * total + e];  // pair (0, 5) by K-parts
-  double v = (double)S[kOzDigits - 1];
-#pragma unroll
-  for (int L = kOzDigits - 2; L >= 0; --L) v = fma(v, 256.0, (double)S[L]);
-  Y[e] = fma(-sigma, Q[e], ldexp(v, 8 * (kOzDigits - 1) - tr[i] - tc[c]));
-}
-
 }  // namespace
-
-// ---- the fit's fp64 products C.Q on the int8 matrix cores (Ozaki-style digit splitting)
-// C (symmetric, dim x dim) is scaled per row and Q (dim x 256) per column to integers
-// below 2^46 and cut into 6 signed base-256 digits each; every pair of digit planes whose
-// weight 256^(a+b) is within 2^-40 of the top (a + b >= 5: 21 of 36) is an exact int32
-// product (|.| <= dim 2^14) on proj_i8_kernel's tiles, and the fp64 combine adds them by
-// level.  Error: the two 2^-46 roundings plus the dropped levels (<= 15 x 2^-46 of
-// rowmax x colmax x dim worst case), the order of an fp64 GEMM's dim x 2^-53.  The row
-// planes are built once per fit (C does not change); Q's digits every product.
-// (dim: whole 256-row blocks, a multiple of 8 of them — the per-XCD item order — and
-// K-parts of whole 64-byte stages)
-bool cq_i8_supported(int64_t dim, int m) { return m == 256 && dim % (8 * PM) == 0 && dim <= 32768; }
-size_t cq_i8_plane_bytes(int64_t dim) { return (size_t)kOzDigits * dim * dim + (size_t)dim * sizeof(int); }
-static size_t cq_off_d(int64_t dim, int m) { return (size_t)kOzBlocks * dim * m * sizeof(int); }
-static size_t cq_off_t(int64_t dim, int m) { return cq_off_d(dim, m) + (size_t)kOzDigits * m * dim; }
-size_t cq_i8_work_bytes(int64_t dim, int m) { return cq_off_t(dim, m) + (size_t)m * (sizeof(int) + 8); }
-hipError_t launch_cq_i8_planes(hipStream_t s, const double* C, int64_t dim, void* planes) {
-  uint8_t* P = static_cast<uint8_t*>(planes);
-  int* tr = reinterpret_cast<int*>(P + (size_t)kOzDigits * dim * dim);
-  hipLaunchKernelGGL(oz_rows_kernel, dim3((unsigned)dim), dim3(256), 0, s, C, dim, P, tr);
-  return hipGetLastError();
-}
-hipError_t launch_cq_i8(hipStream_t s, const void* planes, int64_t dim, const double* Q, int m, double sigma,
-                        void* work, double* Y) {
-  if (!cq_i8_supported(dim, m)) return hipErrorInvalidValue;
-  const uint8_t* P = static_cast<const uint8_t*>(planes);
-  const int* tr = reinterpret_cast<const int*>(P + (size_t)kOzDigits * dim * dim);
-  uint8_t* base = static_cast<uint8_t*>(work);
-  int* I = reinterpret_cast<int*>(base);
-  int8_t* D = reinterpret_cast<int8_t*>(base + cq_off_d(dim, m));
-  int* tc = reinterpret_cast<int*>(base + cq_off_t(dim, m));
-  unsigned long long* cmax = reinterpret_cast<unsigned long long*>(base + cq_off_t(dim, m) + (size_t)m * sizeof(int));
-  hipError_t e = hipMemsetAsync(cmax, 0, (size_t)m * 8, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(oz_colmax_kernel, dim3((unsigned)(dim / 16)), dim3(256), 0, s, Q, dim, m, cmax);
-  hipLaunchKernelGGL(oz_qdigits_kernel, dim3((unsigned)(dim / 16)), dim3(256), 0, s, Q, dim, m, cmax, D, tc);
-  const int nrb = (int)(dim / PM);
-  const int nblocks = nrb * kOzItems;  // a multiple of 8 (cq_i8_supported)
-  hipLaunchKernelGGL((proj_i8_kernel<256, true>), dim3((unsigned)nblocks), dim3(512), 0, s,
-                     reinterpret_cast<const uint8_t*>(P), dim, dim, D, nrb / 8, nblocks, I, (int64_t)m);
-  hipLaunchKernelGGL(oz_combine_kernel, dim3((unsigned)((dim * m + 255) / 256)), dim3(256), 0, s, I, dim, m, tr, tc,
-                     Q, sigma, Y);
-  return hipGetLastError();
-}
 
 struct ProjLayout {
   int64_t np, off_i, off_t, off_c, bytes;
@@ -519,10 +300,10 @@ hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
   if (nblocks > (int64_t)1 << 30) return hipErrorInvalidValue;
   const int grid = (int)((nblocks + 7) / 8 * 8);
   if (L.tn == 256)
-    hipLaunchKernelGGL((proj_i8_kernel<256, false>), dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
+    hipLaunchKernelGGL(proj_i8_kernel<256>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
                        np);
   else
-    hipLaunchKernelGGL((proj_i8_kernel<128, false>), dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
+    hipLaunchKernelGGL(proj_i8_kernel<128>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
                        np);
   hipLaunchKernelGGL(proj_combine_kernel, dim3((unsigned)((n * kk + 255) / 256)), dim3(256), 0, s, I, n, kk, np, tsh,
                      cc, F);

@@ -95,6 +95,33 @@ def test_fit_shapes_vs_oracle(n, d, k, r):
     np.testing.assert_allclose(a[:, gap], o_eig[:, gap], atol=1e-6)
 
 
+@pytest.mark.parametrize("n,d", [(5000, 4096), (4096, 6400)])
+def test_fit_int8_digit_products(n, d):
+    """The fine-phase products C.Q as exact int8 digit pairs (launch_cq_i8, ef_proj_i8.hip:
+    block width 256 = 2k, order a multiple of 2048) on an unstandardised covariance
+    (n >= d) and Gram (n < d) whose rows span very different scales: 64 constant pixels
+    (zero rows: scale exponent 0, all digits 0) and 64 pixels of 1/16 the contrast (the
+    per-row scaling keeps their digits full) — against the oracle's fp64 eigh
+    (useless/train.py:82-116)."""
+    from eigenface import manual_pca
+    side = int(np.sqrt(d))
+    x, _ = orc.synth_faces(n, side, r=64, seed=n + 7)
+    x[:, :64] = 3
+    x[:, 64:128] //= 16
+    eig, mean, proj, lam = manual_pca(x, 128)
+    o_eig, o_mean, o_proj, o_lam = orc.manual_pca(x, 128)
+    keep = o_lam > 1e-9 * o_lam[0]
+    np.testing.assert_allclose(lam[keep], o_lam[keep], rtol=1e-8)
+    gap = np.ones(o_lam.shape[0], bool)
+    rel = np.abs(np.diff(o_lam)) / o_lam[0]
+    gap[:-1] &= rel > 1e-6
+    gap[1:] &= rel > 1e-6
+    gap &= keep
+    assert gap.sum() >= 32
+    a = _align(eig, o_eig)
+    np.testing.assert_allclose(a[:, gap], o_eig[:, gap], atol=1e-6)
+
+
 def test_rank_deficient_duplicates():
     """Duplicate faces make the Gram singular; the fit must stay finite and
     reproduce the non-zero spectrum."""
