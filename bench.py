@@ -684,7 +684,7 @@ def _host_threads():
     return host_cpu_share()
 
 
-def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
+def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=20):
     """JPEG files -> grey 64x64 rows (ef_jpeg_ingest into a device tensor): a stream of
     `reps` batches, each call returning once queued, so batch i+1's host marker parse +
     destuff overlaps batch i's upload / GPU Huffman / IDCT / upsample+YCC / resize; the
@@ -694,7 +694,9 @@ def jpeg_ingest_bench(eng, with_cpu: bool, sides, n=4096, reps=10):
     nbytes = sum(len(b) for b in blobs)
     dev = torch.device("cuda", torch.cuda.current_device())
     out = torch.empty((n, 4096), dtype=torch.uint8, device=dev)
-    for _ in range(2):  # both upload slots allocated before the clock starts
+    # both upload slots allocated (and the early-upload path engaged: it needs a slot already
+    # sized for the batch) and the host pool's pages touched before the clock starts
+    for _ in range(6):
         eng.ingest_jpegs(blobs, (64, 64), "bgr", out=out)
     torch.cuda.synchronize(dev)
     eng.timing_reset()
