@@ -451,7 +451,9 @@ __device__ __forceinline__ int syrk16_swz(int b) { return (0x78 >> (2 * b)) & 3;
 // the digits' K-blocked array of `dim` = R rows, kps the order of C (odim), ntiles the row
 // blocks per XCD, [st_begin, st_end) all K stages; items per XCD: its row blocks' 20 whole
 // pairs, then the 4 K-parts of pair (0, 5); each writes its pair block of slabs (odim x 256).
-template <int NJB, int NB, bool OZ = false>
+// PAIR (diagnostic EF_SYRK_PAIR=1): two stages per barrier — the ring's two older slots
+// are consumed back to back, then retired together at one barrier while the two newer land.
+template <int NJB, int NB, bool OZ = false, bool PAIR = false>
 __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                            int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
                                                            int nitems, const int2* __restrict__ order,
@@ -556,6 +558,76 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
         pend = -1;
       }
     };
+    if constexpr (PAIR) {
+      static_assert(NB == 4, "two consumed + two landing slots");
+      int64_t pend2 = -1;  // the pair's second stage, issued one position after the first
+      for (int64_t st = 0; st < nst; st += 2) {
+        const bool two = st + 1 < nst;  // uniform
+        const uint8_t* c0 = smem + (st % NB) * STG;
+        const uint8_t* c1 = smem + ((st + 1) % NB) * STG;
+        const uint8_t* nx = smem + ((st + 2) % NB) * STG;
+        auto flush2 = [&](int pos) {
+          if (pos == dpos && pend >= 0) {
+            issue(sb + (pend < nst ? pend : 0), (int)(pend % NB));
+            pend = -1;
+          }
+          if (pos == dpos + 1 && pend2 >= 0) {
+            issue(sb + (pend2 < nst ? pend2 : 0), (int)(pend2 % NB));
+            pend2 = -1;
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < NJB - 1; ++j) {
+          bn = fb(c0, j + 1);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][j], 0, 0, 0);
+          bq = bn;
+          flush2(2 + j);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (two) {  // stage st's last column (A refilled from st + 1, visible since the last barrier)
+          bn = fb(c1, 0);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            acc[i][NJB - 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][NJB - 1], 0, 0, 0);
+            a[i] = fa(c1, i);
+          }
+          bq = bn;
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < NJB - 1; ++j) {
+            bn = fb(c1, j + 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][j], 0, 0, 0);
+            bq = bn;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if (pend >= 0) {
+          issue(sb + (pend < nst ? pend : 0), (int)(pend % NB));
+          pend = -1;
+        }
+        if (pend2 >= 0) {
+          issue(sb + (pend2 < nst ? pend2 : 0), (int)(pend2 % NB));
+          pend2 = -1;
+        }
+        // every read of stages st, st+1 is issued; st+2 and st+3 (issued a pair ago) landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        pend = st + NB;  // into the slots of st and st + 1
+        pend2 = st + NB + 1;
+        flush2(0);
+        bn = fb(nx, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // the pair's last column
+          acc[i][NJB - 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], bq, acc[i][NJB - 1], 0, 0, 0);
+          a[i] = fa(nx, i);
+        }
+        bq = bn;
+        flush2(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else
     for (int64_t st = 0; st < nst; ++st) {
       const uint8_t* cur = smem + (st % NB) * STG;
       const uint8_t* nxt = smem + ((st + 1) % NB) * STG;
@@ -914,6 +986,13 @@ hipError_t launch_cov_i8(hipStream_t s, const CovPlan& p, int64_t n, int64_t d, 
   for (int pass = 0; pass < p.passes; ++pass) {
     const int64_t st0 = (int64_t)pass * p.stages_per_pass;
     const int64_t st1 = std::min<int64_t>(p.nst, st0 + p.stages_per_pass);
+#ifdef EF_DIAGNOSTICS  // EF_SYRK_PAIR=1: two stages per barrier (A/B)
+    static const bool syrk_pair = [] { const char* v = getenv("EF_SYRK_PAIR"); return v && atoi(v) != 0; }();
+    if (syrk_pair && p.njb == 6)
+      hipLaunchKernelGGL((syrk16_i8_kernel<6, 4, false, true>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1,
+                         p.kps, p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
+    else
+#endif
     if (p.njb == 6)
       hipLaunchKernelGGL((syrk16_i8_kernel<6, 4>), dim3((unsigned)grid), dim3(512), 0, s, At, dim, st0, st1, p.kps,
                          p.ntiles, nitems, static_cast<const int2*>(order_dev), slabs);
