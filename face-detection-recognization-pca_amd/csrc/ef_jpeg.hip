@@ -1858,6 +1858,18 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       (mode != EF_JPEG_GRAY && mode != EF_JPEG_BGR))
     return set_err(c, EF_E_INVALID, "ef_jpeg_ingest: bad arguments");
   if (count == 0) return EF_OK;
+#ifdef EF_DIAGNOSTICS  // EF_JPEG_CALLTIMES: per call, host ms of the staging and of the whole call (no syncs)
+  struct CallClock {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    bool on = std::getenv("EF_JPEG_CALLTIMES") != nullptr;
+    double prep = 0.0;
+    ~CallClock() {
+      if (on)
+        std::fprintf(stderr, "[ingest] prepare %.3f ms, call %.3f ms\n", prep,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } call_clock;
+#endif
   (void)hipSetDevice(c->device);
   if (!c->jpeg_copy) {  // (created here, before any staging thread can use it)
     const hipError_t e = hipStreamCreateWithFlags(&c->jpeg_copy, hipStreamNonBlocking);
@@ -1937,6 +1949,9 @@ int ef_jpeg_ingest(ef_ctx* c, const uint8_t* data, const int64_t* offsets, const
       if (next.joinable()) next.join();  // before any return: the thread uses parts[i + 1]
       if (rc != EF_OK) return rc;
       if (status) std::memcpy(status + P.a, P.st.data(), (size_t)P.m * 4);
+#ifdef EF_DIAGNOSTICS
+      call_clock.prep += P.host_ms;
+#endif
       if (c->timing) {  // host staging time of this part (recorded on the calling thread)
         c->t_ms[EF_KERNEL_JPEG_HOST] += P.host_ms;
         c->t_n[EF_KERNEL_JPEG_HOST] += 1;
