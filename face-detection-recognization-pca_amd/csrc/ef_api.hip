@@ -431,6 +431,9 @@ void ef_destroy(ef_ctx* c) {
   }
   if (c->jpeg_done) (void)hipEventDestroy(c->jpeg_done);
   if (c->jpeg_copy) (void)hipStreamDestroy(c->jpeg_copy);
+  for (int i = 0; i < 2; ++i)
+    if (c->fit_side_ev[i]) (void)hipEventDestroy(c->fit_side_ev[i]);
+  if (c->fit_side) (void)hipStreamDestroy(c->fit_side);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);

@@ -358,9 +358,34 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
 #endif
   uint8_t *cq_planes = nullptr, *cq_work = nullptr;
   bool cq_ready = false;
+  // C's digit planes are built on the fit's side stream while the coarse phase runs (its
+  // Jacobi rounds and small GEMMs leave most CUs idle); the first fine product waits for
+  // them.  The guard orders the main stream after the side work on every exit, so no
+  // later work (or a pool reallocation on the next fit) can overtake it.
+  struct SideJoin {
+    ef_ctx* c;
+    bool armed = false;
+    ~SideJoin() {
+      if (armed) (void)hipStreamWaitEvent(c->stream, c->fit_side_ev[1], 0);
+    }
+  } side_join{c};
+  bool side = true;
+#ifdef EF_DIAGNOSTICS  // EF_FIT_SIDE=0: the planes on the main stream at the first fine product (A/B)
+  if (const char* e = getenv("EF_FIT_SIDE")) side = atoi(e) != 0;
+#endif
   if (cq_i8) {
     EF_TRY(B.get(c, cq_i8_plane_bytes(dim), &cq_planes));
     EF_TRY(B.get(c, cq_i8_work_bytes(dim, m), &cq_work));
+  }
+  if (cq_i8 && side) {
+    if (!c->fit_side) EF_HIP(c, hipStreamCreateWithFlags(&c->fit_side, hipStreamNonBlocking), "fit side stream");
+    for (int i = 0; i < 2; ++i)
+      if (!c->fit_side_ev[i]) EF_HIP(c, hipEventCreateWithFlags(&c->fit_side_ev[i], hipEventDisableTiming), "fit event");
+    EF_HIP(c, hipEventRecord(c->fit_side_ev[0], s), "C ready");
+    EF_HIP(c, hipStreamWaitEvent(c->fit_side, c->fit_side_ev[0], 0), "side waits C");
+    EF_HIP(c, launch_cq_i8_planes(c->fit_side, C, dim, cq_planes), "C (int8 digit planes)");
+    EF_HIP(c, hipEventRecord(c->fit_side_ev[1], c->fit_side), "planes ready");
+    side_join.armed = true;
   }
   std::vector<double> th(m), prev(m, 0.0);
   bool have_prev = false, prev_fine = false;
@@ -419,7 +444,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
              "Y = C.Q (fp32)");
       hipLaunchKernelGGL(f32_to_f64_shift_kernel, dim3(ew_blocks), dim3(256), 0, s, Y32, Q, dim * m, sigma, Y);
     } else if (cq_i8) {
-      if (!cq_ready) EF_HIP(c, launch_cq_i8_planes(s, C, dim, cq_planes), "C (int8 digit planes)");
+      if (!cq_ready) {
+        if (side) EF_HIP(c, hipStreamWaitEvent(s, c->fit_side_ev[1], 0), "planes ready");
+        else EF_HIP(c, launch_cq_i8_planes(s, C, dim, cq_planes), "C (int8 digit planes)");
+      }
       cq_ready = true;
       EF_HIP(c, launch_cq_i8(s, cq_planes, dim, Q, m, sigma, cq_work, Y), "Y = C.Q (int8 digits)");
     } else {

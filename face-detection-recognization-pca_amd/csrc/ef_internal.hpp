@@ -146,6 +146,10 @@ struct ef_ctx {
   hipEvent_t jpeg_ws_free[2] = {nullptr, nullptr};
   hipEvent_t jpeg_done = nullptr;
   hipStream_t jpeg_copy = nullptr;  // upload stream (created on first use)
+  // the fit's side stream (created on first use): work off the critical path of the
+  // subspace iteration, e.g. the int8 digit planes of C during the coarse phase
+  hipStream_t fit_side = nullptr;
+  hipEvent_t fit_side_ev[2] = {nullptr, nullptr};
   int jpeg_slot = 0;                // slot of the next staged batch
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
