@@ -42,8 +42,7 @@ constexpr int PNB = 4;            // LDS ring stages
 constexpr int kDigits = 7;        // base-256 digits of the scaled eigenvector entries
 constexpr int kTopBit = 54;       // largest scaled entry ~ 2^54
 
-// t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^(TOP-1), 2^TOP); zero columns get t_c = 0.
-template <int TOP = kTopBit>
+// t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^53, 2^54); zero columns get t_c = 0.
 __global__ void digit_scale_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
                                    int* __restrict__ tsh) {
   const int c = blockIdx.x;
@@ -59,12 +58,11 @@ __global__ void digit_scale_kernel(const double* __restrict__ E, const double* _
   if (threadIdx.x == 0) {
     int e = 0;
     if (red[0] > 0.0) (void)frexp(red[0], &e);  // red[0] in [2^(e-1), 2^e)
-    tsh[c] = red[0] > 0.0 ? TOP - e : 0;
+    tsh[c] = red[0] > 0.0 ? kTopBit - e : 0;
   }
 }
 
 // D[(j * kk + c) * d + r] = digit j of rint(w_r E[r][c] 2^t_c); rows kk * P .. Npad are zero.
-template <int ND = kDigits>
 __global__ void digits_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
                               const int* __restrict__ tsh, int8_t* __restrict__ D) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -73,7 +71,7 @@ __global__ void digits_kernel(const double* __restrict__ E, const double* __rest
   const int c = (int)(e - r * kk);
   long long v = (long long)rint(ldexp((w ? w[r] : 1.0) * E[r * kk + c], tsh[c]));
 #pragma unroll
-  for (int j = 0; j < ND; ++j) {
+  for (int j = 0; j < kDigits; ++j) {
     const long long lo = ((v + 128) & 255) - 128;  // signed low byte
     D[((int64_t)j * kk + c) * d + r] = (int8_t)lo;
     v = (v - lo) / 256;
@@ -102,7 +100,7 @@ __global__ void cc_kernel(const double* __restrict__ E, const double* __restrict
 #ifndef EF_PROJ_HI
 #define EF_PROJ_HI 3
 #endif
-template <int TN, bool OZ = false>
+template <int TN>
 __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
                                                          const int8_t* __restrict__ D, int ntn, int nblocks,
                                                          int* __restrict__ C, int64_t ldc) {
@@ -292,8 +290,8 @@ hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
   double* cc = reinterpret_cast<double*>(base + L.off_c);
   hipError_t e = hipMemsetAsync(D, 0, (size_t)(np * d), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(digit_scale_kernel<>, dim3((unsigned)kk), dim3(256), 0, s, E, w, d, kk, tsh);
-  hipLaunchKernelGGL(digits_kernel<>, dim3((unsigned)((d * kk + 255) / 256)), dim3(256), 0, s, E, w, d, kk, tsh, D);
+  hipLaunchKernelGGL(digit_scale_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, d, kk, tsh);
+  hipLaunchKernelGGL(digits_kernel, dim3((unsigned)((d * kk + 255) / 256)), dim3(256), 0, s, E, w, d, kk, tsh, D);
   hipLaunchKernelGGL(cc_kernel, dim3((unsigned)kk), dim3(256), 0, s, E, w, mu, d, kk, cc);
   const int ntn = (int)(np / L.tn);
   const int64_t nblocks = (n + PM - 1) / PM * ntn;
