@@ -349,9 +349,8 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     else
       cvt64to32(s, C, dim * dim, C32);
   }
-  // fp64-accuracy products on the int8 matrix cores (launch_cq_i8: C and Q in base-256
-  // digits, 21 exact digit-pair products): the row planes of C once, at the first fine
-  // product.
+  // fp64-accuracy products on the int8 matrix cores (launch_cq_i8, ef_cq_i8.hip: C and Q in
+  // base-256 digits, 21 exact digit-pair products); C's digit planes are built once.
   bool cq_i8 = cq_i8_supported(dim, m) && tall_gemm_supported(dim, C, 8);
 #ifdef EF_DIAGNOSTICS  // EF_FIT_CQ_I8=0: the fp64 MFMA product (A/B)
   if (const char* e = getenv("EF_FIT_CQ_I8")) cq_i8 = cq_i8 && atoi(e) != 0;
