@@ -453,7 +453,7 @@ __device__ __forceinline__ int syrk16_swz(int b) { return (0x78 >> (2 * b)) & 3;
 // pairs, then the 4 K-parts of pair (0, 5); each writes its pair block of slabs (odim x 256).
 // PAIR (diagnostic EF_SYRK_PAIR=1): two stages per barrier — the ring's two older slots
 // are consumed back to back, then retired together at one barrier while the two newer land.
-template <int NJB, int NB, bool OZ = false, bool PAIR = false>
+template <int NJB, int NB, bool OZ = false, bool PAIR = false, bool OZMED = false>
 __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __restrict__ At, int64_t dim,
                                                            int64_t st_begin, int64_t st_end, int64_t kps, int ntiles,
                                                            int nitems, const int2* __restrict__ order,
@@ -476,21 +476,22 @@ __global__ __launch_bounds__(512, 1) void syrk16_i8_kernel(const uint8_t* __rest
     int p, mt;
     sb = st_begin;
     nst = st_end - st_begin;
-    if (r < ntiles * kOzPairsWhole) {
-      mt = x * ntiles + r / kOzPairsWhole;
-      p = r % kOzPairsWhole;
+    constexpr int whole = oz_pairs(OZMED) - 1;
+    if (r < ntiles * whole) {
+      mt = x * ntiles + r / whole;
+      p = r % whole;
       ks = p;
     } else {
-      const int r2 = r - ntiles * kOzPairsWhole;
+      const int r2 = r - ntiles * whole;
       mt = x * ntiles + r2 / kOzSplitParts;
       const int part = r2 % kOzSplitParts;
-      p = kOzPairsWhole;
+      p = whole;
       ks = p + part;
       sb = st_begin + nst * part / kOzSplitParts;
       nst = st_begin + nst * (part + 1) / kOzSplitParts - sb;
     }
     int a, b;
-    oz_pair(p, a, b);
+    oz_pair(p, OZMED, a, b);
     i0 = (int64_t)a * odim + (int64_t)mt * YT;
     j0 = 6 * odim + (int64_t)b * TJ;
     oz_row0 = (int64_t)mt * YT;
@@ -1073,12 +1074,16 @@ hipError_t launch_cov_from_cross(hipStream_t s, const long long* S64, const unsi
 }
 
 // The fit's digit-pair products (ef_cq_i8.hip): 64 row blocks of 256 x 24 items at C3
-hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I) {
+hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I, bool med) {
   if (dim % 2048 != 0) return hipErrorInvalidValue;
   const int nrb = (int)(dim / YT);
-  const int nitems = nrb * kOzBlocks;  // a multiple of 8
-  hipLaunchKernelGGL((syrk16_i8_kernel<4, 4, true>), dim3((unsigned)nitems), dim3(512), 0, s, Z, R, (int64_t)0,
-                     dim / YK, dim, nrb / 8, nitems, nullptr, I);
+  const int nitems = nrb * oz_blocks(med);  // a multiple of 8
+  if (med)
+    hipLaunchKernelGGL((syrk16_i8_kernel<4, 4, true, false, true>), dim3((unsigned)nitems), dim3(512), 0, s, Z, R,
+                       (int64_t)0, dim / YK, dim, nrb / 8, nitems, nullptr, I);
+  else
+    hipLaunchKernelGGL((syrk16_i8_kernel<4, 4, true>), dim3((unsigned)nitems), dim3(512), 0, s, Z, R, (int64_t)0,
+                       dim / YK, dim, nrb / 8, nitems, nullptr, I);
   return hipGetLastError();
 }
 

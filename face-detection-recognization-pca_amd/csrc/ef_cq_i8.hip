@@ -11,6 +11,9 @@
 //     per level, and applies 2^-(t_i + u_c) and the shift -sigma Q.
 // Error: the two roundings (2^-46 of the row / column maximum) and the dropped levels,
 // the order of an fp64 GEMM's own dim x 2^-53 (useless/train.py:88 computes eigh in fp64).
+// The medium form (15 pairs: a, b >= 1, a + b >= 6; ~2^-40 of the product) serves the
+// products whose errors later products damp: ef_fit uses it for every fine product that is
+// neither read by a Rayleigh-Ritz step nor the one before it.
 //
 // Operand layout: one K-blocked int8 array [dim / 64][R][64] (the SYRK's At layout),
 // R = 6 dim + 6 x 256 rows: C's digit plane a at rows a dim + i, Q's digit b at rows
@@ -121,32 +124,36 @@ __global__ __launch_bounds__(256) void oz_qdigits_kernel(const double* __restric
     *reinterpret_cast<uint4*>(base + (int64_t)j * kOzQ * kZK) = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
 }
 
-// Y[i][c] = 2^(40 - t_i - u_c) sum_{L=0..5} 256^L S_L - sigma Q[i][c]: S_L the exact int64
-// sum of the pair products of level a + b = L + 5 (block order of syrk16_i8_kernel's OZ
-// items: pairs with a >= 1, a descending, then the K-parts of pair (0, 5)).
+// Y[i][c] = 2^(8 lev - t_i - u_c) sum_L 256^L S_L - sigma Q[i][c]: S_L the exact int64 sum
+// of the pair products of level a + b = L + lev (lev = 5 full, 6 medium), in the block
+// order of syrk16_i8_kernel's OZ items (oz_pair, then the K-parts of the last pair); fp64
+// Horner from the top level.
+template <bool MED>
 __global__ __launch_bounds__(256) void oz_combine_kernel(const int* __restrict__ I, int64_t dim,
                                                          const int* __restrict__ tr, const int* __restrict__ tc,
                                                          const double* __restrict__ Q, double sigma,
                                                          double* __restrict__ Y) {
+  constexpr int lev = MED ? 6 : 5, nlev = 11 - lev, np = oz_pairs(MED);
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = dim * kOzQ;
   if (e >= total) return;
   const int64_t i = e / kOzQ;
   const int c = (int)(e - i * kOzQ);
-  long long S[kOzDigits];
+  long long S[nlev];
 #pragma unroll
-  for (int L = 0; L < kOzDigits; ++L) S[L] = 0;
-  int p = 0;
+  for (int L = 0; L < nlev; ++L) S[L] = 0;
 #pragma unroll
-  for (int a = kOzDigits - 1; a >= 1; --a)
+  for (int p = 0; p < np - 1; ++p) {
+    int a = 0, b = 0;
+    oz_pair(p, MED, a, b);
+    S[a + b - lev] += I[(int64_t)p * total + e];
+  }
 #pragma unroll
-    for (int b = kOzDigits - 1 - a; b < kOzDigits; ++b, ++p) S[a + b - (kOzDigits - 1)] += I[(int64_t)p * total + e];
+  for (int q = 0; q < kOzSplitParts; ++q) S[0] += I[(int64_t)(np - 1 + q) * total + e];  // the lowest level
+  double v = (double)S[nlev - 1];
 #pragma unroll
-  for (int q = 0; q < kOzSplitParts; ++q) S[0] += I[(int64_t)(p + q) * total + e];
-  double v = (double)S[kOzDigits - 1];
-#pragma unroll
-  for (int L = kOzDigits - 2; L >= 0; --L) v = fma(v, 256.0, (double)S[L]);
-  Y[e] = fma(-sigma, Q[e], ldexp(v, 8 * (kOzDigits - 1) - tr[i] - tc[c]));
+  for (int L = nlev - 2; L >= 0; --L) v = fma(v, 256.0, (double)S[L]);
+  Y[e] = fma(-sigma, Q[e], ldexp(v, 8 * lev - tr[i] - tc[c]));
 }
 
 size_t oz_layout_bytes(int64_t dim) { return (size_t)oz_rows(dim) * dim; }
@@ -167,7 +174,7 @@ hipError_t launch_cq_i8_planes(hipStream_t s, const double* C, int64_t dim, void
 }
 
 hipError_t launch_cq_i8(hipStream_t s, void* planes, int64_t dim, const double* Q, int m, double sigma, void* work,
-                        double* Y) {
+                        double* Y, bool medium) {
   if (!cq_i8_supported(dim, m)) return hipErrorInvalidValue;
   int8_t* Z = static_cast<int8_t*>(planes);
   const int* tr = reinterpret_cast<const int*>(Z + oz_layout_bytes(dim));
@@ -179,10 +186,14 @@ hipError_t launch_cq_i8(hipStream_t s, void* planes, int64_t dim, const double* 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(oz_colmax_kernel, dim3((unsigned)(dim / 16)), dim3(256), 0, s, Q, dim, cmax);
   hipLaunchKernelGGL(oz_qdigits_kernel, dim3((unsigned)(dim / 16)), dim3(256), 0, s, Q, dim, cmax, Z, tc);
-  e = launch_oz_syrk16(s, reinterpret_cast<const uint8_t*>(Z), dim, oz_rows(dim), I);
+  e = launch_oz_syrk16(s, reinterpret_cast<const uint8_t*>(Z), dim, oz_rows(dim), I, medium);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(oz_combine_kernel, dim3((unsigned)(dim * kOzQ / 256)), dim3(256), 0, s, I, dim, tr, tc, Q, sigma,
-                     Y);
+  if (medium)
+    hipLaunchKernelGGL(oz_combine_kernel<true>, dim3((unsigned)(dim * kOzQ / 256)), dim3(256), 0, s, I, dim, tr, tc, Q,
+                       sigma, Y);
+  else
+    hipLaunchKernelGGL(oz_combine_kernel<false>, dim3((unsigned)(dim * kOzQ / 256)), dim3(256), 0, s, I, dim, tr, tc,
+                       Q, sigma, Y);
   return hipGetLastError();
 }
 

@@ -448,7 +448,16 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
         else EF_HIP(c, launch_cq_i8_planes(s, C, dim, cq_planes), "C (int8 digit planes)");
       }
       cq_ready = true;
-      EF_HIP(c, launch_cq_i8(s, cq_planes, dim, Q, m, sigma, cq_work, Y), "Y = C.Q (int8 digits)");
+      // the medium form (15 digit pairs, ~2^-40) unless a Rayleigh-Ritz step reads this
+      // product or the next: the errors of earlier products are damped by the later ones
+      // (residual floor 1e-12 theta_1), the accepted step's Ritz pairs come from full ones
+      // (iterations <= 4 may hold the small orders' early Rayleigh-Ritz steps)
+      bool medium = it >= 5 && it + 1 < next_rr && it + 1 < max_iters;
+#ifdef EF_DIAGNOSTICS  // EF_FIT_CQ_MED=0: every fine product in the full form (A/B)
+      static const bool med_on = [] { const char* e = getenv("EF_FIT_CQ_MED"); return !(e && atoi(e) == 0); }();
+      medium = medium && med_on;
+#endif
+      EF_HIP(c, launch_cq_i8(s, cq_planes, dim, Q, m, sigma, cq_work, Y, medium), "Y = C.Q (int8 digits)");
     } else {
       EF_HIP(c, dense_gemm(c, s, Operand::symmetric(C, dim), Operand::dense(Q, m, false), dim, m, dim, 1.0, Y, m, work,
                            kWorkElems, Bt),

@@ -219,24 +219,33 @@ size_t cq_i8_plane_bytes(int64_t dim);
 size_t cq_i8_work_bytes(int64_t dim, int m);
 hipError_t launch_cq_i8_planes(hipStream_t s, const double* C, int64_t dim, void* planes);
 hipError_t launch_cq_i8(hipStream_t s, void* planes, int64_t dim, const double* Q, int m, double sigma, void* work,
-                        double* Y);
-// Its digit-pair products (ef_cov_i8.hip, syrk16_i8_kernel's OZ items): pair p < 20 is
-// (a, b), a = 5 .. 1 descending, b = 5 - a .. 5; pair (0, 5) runs in kOzSplitParts K-parts
-// (so 64 row blocks x 24 items fill 256 CUs in 5.25 rounds of whole-item time); output
-// block p, then 20 + part, each dim x 256 int32.  Z: the K-blocked [dim/64][R][64] digits.
-constexpr int kOzPairsWhole = 20;
+                        double* Y, bool medium = false);
+// Its digit-pair products (ef_cov_i8.hip, syrk16_i8_kernel's OZ items).  Full form
+// (med = false): every pair a + b >= 5 of the 6 + 6 digits, 21; medium form (med = true,
+// the products no Rayleigh-Ritz step reads directly): a, b >= 1 and a + b >= 6, 15 pairs,
+// ~2^-40 of the full product (its lowest level and both lowest digits dropped).  Pair p
+// enumerates a descending, b ascending; the last pair — (0, 5) full, (1, 5) medium — runs
+// in kOzSplitParts K-parts (so 64 row blocks fill 256 CUs in whole-round steps); output
+// block p, then the parts, each dim x 256 int32.  Z: the K-blocked [dim/64][R][64] digits.
 constexpr int kOzSplitParts = 4;
-constexpr int kOzBlocks = kOzPairsWhole + kOzSplitParts;
-__host__ __device__ inline void oz_pair(int p, int& a, int& b) {
+__host__ __device__ constexpr int oz_pairs(bool med) { return med ? 15 : 21; }
+__host__ __device__ constexpr int oz_blocks(bool med) { return oz_pairs(med) - 1 + kOzSplitParts; }
+constexpr int kOzBlocks = oz_blocks(false);  // the larger
+__host__ __device__ inline void oz_pair(int p, bool med, int& a, int& b) {
+  const int lo = med ? 1 : 0, lev = med ? 6 : 5;  // smallest digit, smallest level a + b
   a = 5;
   int base = 0;
-  while (p >= base + a + 1) {
-    base += a + 1;
+  for (;;) {
+    const int b0 = lev - a > lo ? lev - a : lo, cnt = 6 - b0;
+    if (p < base + cnt) {
+      b = b0 + (p - base);
+      return;
+    }
+    base += cnt;
     --a;
   }
-  b = 5 - a + (p - base);
 }
-hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I);
+hipError_t launch_oz_syrk16(hipStream_t s, const uint8_t* Z, int64_t dim, int64_t R, int* I, bool med);
 hipError_t launch_colstats(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
                            unsigned long long* S1, unsigned long long* S2);
 // Float input (EF_F32 / EF_F64): column mean and population variance in fp64 by two
