@@ -56,6 +56,11 @@ __device__ __forceinline__ float min3_raw(float a, float b, float c) {
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ bf16x8w as_bf16x8w(const float4& v) {
   bf16x8w r;
   __builtin_memcpy(&r, &v, 16);
@@ -807,12 +812,23 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
           }
         }
     } else {
-      // 32 values in 16 v_min3 (fminf would re-canonicalise every MFMA result first:
-      // one v_max_f32 x, x per input in IEEE mode)
-      float mn = v[0][0];
+      // L2: v holds the raw accumulators a (score -2 a, exact): the block's best score is
+      // -2 max(a), so the skip test needs 16 v_max3 and one multiply instead of 32
+      // multiplies and 16 v_min3, and only a block that passes it scales its values.
+      // Cosine: v holds the scores.  (fminf / fmaxf would re-canonicalise every MFMA
+      // result first: one v_max_f32 x, x per input in IEEE mode)
+      float mn;
+      if constexpr (METRIC == EF_METRIC_L2) {
+        float mx = v[0][0];
 #pragma unroll
-      for (int e = 1; e + 1 < 32; e += 2) mn = min3_raw(mn, v[e >> 2][e & 3], v[(e + 1) >> 2][(e + 1) & 3]);
-      mn = fminf(mn, v[7][3]);
+        for (int e = 1; e + 1 < 32; e += 2) mx = max3_raw(mx, v[e >> 2][e & 3], v[(e + 1) >> 2][(e + 1) & 3]);
+        mn = -2.f * fmaxf(mx, v[7][3]);
+      } else {
+        mn = v[0][0];
+#pragma unroll
+        for (int e = 1; e + 1 < 32; e += 2) mn = min3_raw(mn, v[e >> 2][e & 3], v[(e + 1) >> 2][(e + 1) & 3]);
+        mn = fminf(mn, v[7][3]);
+      }
       if (!__any(mn < b2[pb])) return;  // exact skip (ef_search.hip consume)
       float m1 = INF, m2 = INF;
       int ir = 0;
@@ -820,7 +836,7 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
       for (int rb = 0; rb < 8; ++rb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = v[rb][r];
+          const float x = METRIC == EF_METRIC_L2 ? -2.f * v[rb][r] : v[rb][r];
           const bool lt = x < m1;
           m2 = __builtin_amdgcn_fmed3f(m1, x, m2);
           ir = lt ? 16 * rb + r : ir;
@@ -905,9 +921,14 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
         const float4 x = *reinterpret_cast<const float4*>(sAux + 16 * rb + 4 * qd);
 #pragma unroll
         for (int pb = 0; pb < 4; ++pb) {
+          // main pass, L2: the raw accumulators go to consume (see there); rows past the
+          // gallery's end become -inf there (score +inf)
+          constexpr bool raw = METRIC == EF_METRIC_L2 && !COLLECT;
           if constexpr (METRIC == EF_METRIC_L2) {
+            if constexpr (!raw) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[rb][pb][r] *= -2.f;
+              for (int r = 0; r < 4; ++r) acc[rb][pb][r] *= -2.f;
+            }
           } else {  // -(q.g) * (1/||g||)
             acc[rb][pb][0] *= -x.x;
             acc[rb][pb][1] *= -x.y;
@@ -917,7 +938,7 @@ __global__ __launch_bounds__(512, 1) void search_wide16_kernel(
           if (tail) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              if (tbase + 16 * rb + 4 * qd + r >= n) acc[rb][pb][r] = INF;
+              if (tbase + 16 * rb + 4 * qd + r >= n) acc[rb][pb][r] = raw ? -INF : INF;
           }
         }
       }
