@@ -1600,7 +1600,11 @@ int stage_batch(ef_ctx* c, int slot, Batch& B, const uint8_t* data, const int64_
       const size_t w0 = (size_t)B.segs[a].word_off * 4, w1 = (size_t)(b < nseg ? B.segs[b].word_off : B.words) * 4;
       e = hipMemcpyAsync(up + S.o_words + w0, h + S.o_words + w0, w1 - w0, hipMemcpyHostToDevice, c->jpeg_copy);
     }
-    if (e != hipSuccess) { *err = hipGetErrorString(e); return EF_E_HIP; }
+    if (e != hipSuccess) {  // (pieces already queued must not outlive the pinned slot's next use)
+      *err = hipGetErrorString(e);
+      (void)hipStreamSynchronize(c->jpeg_copy);
+      return EF_E_HIP;
+    }
     S.words_up = S.o_words + (size_t)B.words * 4;
   } else {
     destuff_all(B, data, offsets, reinterpret_cast<uint8_t*>(h + S.o_words));
