@@ -205,6 +205,13 @@ __global__ void f32_to_f64_shift_kernel(const float* __restrict__ a, const doubl
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     b[i] = fma(-sigma, q[i], (double)a[i]);
 }
+// Deferred CholQR check: the fit's sticky failure flag |= this factor's info
+__global__ void sticky_info_kernel(const int* __restrict__ info, int* __restrict__ sticky) {
+  if (*info != 0) *sticky = 1;
+}
+// subspace_wide's "a deferred Cholesky failed: run again with a host check per iteration"
+constexpr int kRetryChecked = 1000;
+
 // Chebyshev step of the subspace iteration: y = s * y - w (w null: y = s * y)
 __global__ void cheb_combine_kernel(double* __restrict__ y, const double* __restrict__ w, int64_t n, double sc) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -242,8 +249,12 @@ static void cvt64to32(hipStream_t s, const double* a, int64_t n, float* b) {
                      b);
 }
 
+// deferred: the per-iteration Cholesky success check is made at the next Rayleigh-Ritz
+// step instead of by a host round trip every iteration; a failure found there returns
+// kRetryChecked (the caller runs the checked form, which takes the rank-deficient fallback
+// in the iteration that needs it).
 int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int m, double* work, double* U_out,
-                  double* lam_out, int* iters) {
+                  double* lam_out, int* iters, bool deferred) {
   hipStream_t s = c->stream;
   SmallEig se;
   EF_TRY(se.init(c, B, m));
@@ -270,6 +281,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
   EF_TRY(B.get(c, (size_t)dim * m, &Qold));
   EF_TRY(B.get(c, (size_t)dim * m, &Wc));
   bool carried = false;
+  int* sticky;  // deferred Cholesky failures since the fit began
+  EF_TRY(B.get(c, 4, &sticky));
+  const bool defer = deferred && chol_inv_supported(m);
+  if (defer) EF_HIP(c, hipMemsetAsync(sticky, 0, sizeof(int), s), "sticky");
   EF_HIP(c, launch_rand_init(s, Y, dim * m, 0x5eedULL), "rand init");
 
   // Q <- orthonormal basis of span(Y) (Y is overwritten).  carry: also map the block
@@ -294,7 +309,10 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     } else if (m <= kCholeskyMax) {
       EF_HIP(c, launch_cholesky(s, G, m, m, 1e-13, cinfo), "cholesky");
     }
-    if (fused || m <= kCholeskyMax) {
+    if (defer) {  // checked at the next Rayleigh-Ritz step (a failed factor leaves Li as it was)
+      hipLaunchKernelGGL(sticky_info_kernel, dim3(1), dim3(1), 0, s, cinfo, sticky);
+      hinfo = 0;
+    } else if (fused || m <= kCholeskyMax) {
       EF_HIP(c, hipMemcpyAsync(&hinfo, cinfo, sizeof(int), hipMemcpyDeviceToHost, s), "D2H info");
       EF_HIP(c, hipStreamSynchronize(s), "sync");
     }
@@ -475,6 +493,12 @@ int subspace_wide(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, int 
     const bool early = dim < 12288 && (it <= 2 || it == 4);
 #endif
     const bool rr = early || it == next_rr || it == max_iters;
+    if (rr && defer) {  // the deferred Cholesky checks, before anything reads this block
+      int hs = 0;
+      EF_HIP(c, hipMemcpyAsync(&hs, sticky, sizeof(int), hipMemcpyDeviceToHost, s), "D2H sticky");
+      EF_HIP(c, hipStreamSynchronize(s), "sync");
+      if (hs != 0) return kRetryChecked;
+    }
     if (rr) {
       EF_HIP(c, dense_gemm(c, s, Operand::dense(Q, m, true), Operand::dense(Y, m, false), m, m, dim, 1.0, G, m,
                            work, kWorkElems, Bt),
@@ -714,7 +738,17 @@ int eig_topk(ef_ctx* c, Bufs& B, const double* C, int64_t dim, int kk, double* w
     if (e >= kk + 2 && e <= dim) m = (int)(e & ~int64_t(1));
   }
 #endif
-  return subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters);
+  const size_t mark = B.next;  // a checked rerun reuses the same pool slots
+  bool defer = true;
+#ifdef EF_DIAGNOSTICS  // EF_FIT_DEFER=0: the host check of every CholQR factor (A/B)
+  if (const char* e = getenv("EF_FIT_DEFER")) defer = atoi(e) != 0;
+#endif
+  int rc = subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters, defer);
+  if (rc == kRetryChecked) {
+    B.next = mark;
+    rc = subspace_wide(c, B, C, dim, kk, m, work, U_out, lam_out, iters, false);
+  }
+  return rc;
 }
 
 // Numerically null components.  With k = n (train-v5.py:540-545 sets n_components to the

@@ -122,6 +122,24 @@ def test_fit_int8_digit_products(n, d):
     np.testing.assert_allclose(a[:, gap], o_eig[:, gap], atol=1e-6)
 
 
+def test_subspace_rank_deficient_block_retries_checked():
+    """A block wider than the data's rank (order 2116, k = 50 -> block 100, rank 40): the
+    CholQR factor fails in the first iterations.  The fit defers that check to its
+    Rayleigh-Ritz steps, finds the failure there, and reruns with the per-iteration check,
+    whose rank-deficient fallback (eigen-orthonormalisation) completes it: the spectrum
+    equals the oracle's (40 non-zero eigenvalues, the rest at the rounding floor)."""
+    from eigenface import manual_pca
+    base, _ = orc.synth_faces(40, 46, r=32, seed=9)
+    x = np.concatenate([base] * 75)  # 3000 x 2116, rank <= 40
+    eig, mean, proj, lam = manual_pca(x, 50)
+    o_eig, o_mean, o_proj, o_lam = orc.manual_pca(x, 50)
+    assert np.all(np.isfinite(eig)) and np.all(np.isfinite(lam))
+    keep = o_lam > 1e-9 * o_lam[0]
+    assert keep.sum() <= 40
+    np.testing.assert_allclose(lam[keep], o_lam[keep], rtol=1e-8)
+    assert np.all(np.abs(lam[~keep]) <= 1e-7 * o_lam[0])
+
+
 def test_rank_deficient_duplicates():
     """Duplicate faces make the Gram singular; the fit must stay finite and
     reproduce the non-zero spectrum."""
