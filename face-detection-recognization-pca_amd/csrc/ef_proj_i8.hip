@@ -4,12 +4,15 @@
 // X is uint8, so X' = X - 128 is exact int8, and
 //     F = X' . E'' + 1 . c^T,   E'' = diag(w) E,   c = (128 - mu)^T E''
 // (c in fp64 by cc_kernel).  E'' is fp64; per output column it is scaled by 2^t_c so its
-// largest entry is ~2^54 and rounded to an integer V (relative error <= 2^-54, i.e. fp64
-// precision), which is written as P = 7 signed base-256 digits, V = sum_j 256^j D_j with
-// D_j in [-128, 127].  Each X' . D_j is an exact int32 (|.| <= d * 2^14 <= 2^30 for
-// d <= 65536), so the only roundings are the quantisation of E'' and the fp64 Horner
-// combine 2^-t_c sum_j 256^j I_j (proj_combine_kernel) — the same order of error as the
-// fp64 GEMM it replaces (reference: useless/train.py:122 in float64).
+// largest entry lies in [2^45, 2^46) and rounded to an integer V (error <= 2^-46 of the
+// column's largest entry), which is written as P = 6 signed base-256 digits,
+// V = sum_j 256^j D_j with D_j in [-128, 127].  Each X' . D_j is an exact int32
+// (|.| <= d * 2^14 <= 2^30 for d <= 65536), so the only roundings are the quantisation of
+// E'' and the fp64 Horner combine 2^-t_c sum_j 256^j I_j (proj_combine_kernel): an error
+// of ~sqrt(d) 2^-47 of |x'| max|E''|, the order of the fp64 GEMM it replaces (its own
+// sqrt(d) 2^-53 of |x'||E''| per output; reference: useless/train.py:122 in float64), and
+// the same quantisation as the fit's C.Q digit products (ef_cq_i8.hip).  Round 6: 7 -> 6
+// digits, so kk = 128 runs as exactly 3 tiles of 256 digit columns instead of 4.
 //
 // proj_i8_kernel<TN>: C[n][N] (int32) = X' . D^T with D = [N = P * kk padded to TN][d] int8
 // (K-contiguous).  Workgroup tile 256 rows x TN digit-columns, 8 waves (TN = 128: 4 x 2 of
@@ -18,8 +21,8 @@
 // int8 (x ^ 0x80) in registers.  The N-tiles of one row block are consecutive on one XCD,
 // so X is read from HBM about once.  A stage streams (256 + TN) x 64 B from L2 for
 // 256 x TN x 64 MACs: 48 B per MFMA-clock of a CU at TN = 128, 32 at TN = 256 — the L2 -> LDS
-// stream (~30 B/clk per CU, K3) is the limit, so 7 digits x kk = 128 run as 4 tiles of 256
-// (14 % padding) rather than 7 of 128.
+// stream (~30 B/clk per CU, K3) is the limit, so 6 digits x kk = 128 run as 3 tiles of 256
+// rather than 6 of 128.
 // Requires d % 64 == 0 (X rows are DMA'd 64 bytes at a time; otherwise the caller keeps
 // the fp64 GEMM).
 #include <algorithm>
@@ -39,10 +42,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int PM = 256;           // rows per tile
 constexpr int PK = 64;            // K bytes per stage
 constexpr int PNB = 4;            // LDS ring stages
-constexpr int kDigits = 7;        // base-256 digits of the scaled eigenvector entries
-constexpr int kTopBit = 54;       // largest scaled entry ~ 2^54
+constexpr int kDigits = 6;        // base-256 digits of the scaled eigenvector entries
+constexpr int kTopBit = 46;       // largest scaled entry in [2^45, 2^46)
 
-// t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^53, 2^54); zero columns get t_c = 0.
+// t_c: 2^t_c * max_r |w_r E[r][c]| lies in [2^45, 2^46); zero columns get t_c = 0.
 __global__ void digit_scale_kernel(const double* __restrict__ E, const double* __restrict__ w, int64_t d, int kk,
                                    int* __restrict__ tsh) {
   const int c = blockIdx.x;
