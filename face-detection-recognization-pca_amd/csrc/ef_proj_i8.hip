@@ -16,13 +16,14 @@
 //
 // proj_i8_kernel<TN>: C[n][N] (int32) = X' . D^T with D = [N = P * kk padded to TN][d] int8
 // (K-contiguous).  Workgroup tile 256 rows x TN digit-columns, 8 waves (TN = 128: 4 x 2 of
-// 64 x 64; TN = 256: 2 x 4 of 128 x 64), K stages of 64 bytes staged by LDS-DMA into a
+// 64 x 64; TN = 256: 2 x 4 of 128 x 64; TN = 384: 2 x 4 of 128 x 96, 192 accumulator
+// registers, a 4 x 40 KiB ring), K stages of 64 bytes staged by LDS-DMA into a
 // 4-stage ring (same 64-B row swizzle as the covariance kernel); A fragments are flipped to
 // int8 (x ^ 0x80) in registers.  The N-tiles of one row block are consecutive on one XCD,
 // so X is read from HBM about once.  A stage streams (256 + TN) x 64 B from L2 for
 // 256 x TN x 64 MACs: 48 B per MFMA-clock of a CU at TN = 128, 32 at TN = 256 — the L2 -> LDS
-// stream (~30 B/clk per CU, K3) is the limit, so 6 digits x kk = 128 run as 3 tiles of 256
-// rather than 6 of 128.
+// stream (~30 B/clk per CU, K3) is the limit, so 6 digits x kk = 128 run as 2 tiles of 384
+// (26.7 B per MFMA-clock) rather than 3 of 256 or 6 of 128.
 // Requires d % 64 == 0 (X rows are DMA'd 64 bytes at a time; otherwise the caller keeps
 // the fp64 GEMM).
 #include <algorithm>
@@ -107,8 +108,9 @@ template <int TN>
 __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restrict__ X, int64_t n, int64_t d,
                                                          const int8_t* __restrict__ D, int ntn, int nblocks,
                                                          int* __restrict__ C, int64_t ldc) {
-  constexpr int WN = TN / 64, WM = 8 / WN;      // wave grid; a wave owns (PM / WM) x 64
-  constexpr int IA = PM / WM / 32, JB = 2;      // 32 x 32 blocks per wave
+  constexpr int WC = TN == 384 ? 96 : 64;       // columns per wave
+  constexpr int WN = TN / WC, WM = 8 / WN;      // wave grid; a wave owns (PM / WM) x WC
+  constexpr int IA = PM / WM / 32, JB = WC / 32;  // 32 x 32 blocks per wave
   constexpr int BPW = TN / 128;                 // B pieces per wave per stage (A: 2)
   constexpr int PSTAGE = (PM + TN) * PK;        // bytes per stage: A panel, then B panel
   __shared__ __attribute__((aligned(16))) uint8_t smem[PNB * PSTAGE];
@@ -162,8 +164,8 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   // lane (r, h) holds A[r][32s + 16h + j], B[32s + 16h + j][r] for k-step s of a stage
   const unsigned offa[2] = {(unsigned)((wm * (PM / WM) + c32) * PK + ((h ^ sw) * 16)),
                             (unsigned)((wm * (PM / WM) + c32) * PK + (((2 + h) ^ sw) * 16))};
-  const unsigned offb[2] = {(unsigned)(PM * PK + (wn * 64 + c32) * PK + ((h ^ sw) * 16)),
-                            (unsigned)(PM * PK + (wn * 64 + c32) * PK + (((2 + h) ^ sw) * 16))};
+  const unsigned offb[2] = {(unsigned)(PM * PK + (wn * WC + c32) * PK + ((h ^ sw) * 16)),
+                            (unsigned)(PM * PK + (wn * WC + c32) * PK + (((2 + h) ^ sw) * 16))};
   auto fa = [&](const uint8_t* sa, int ks, int i) {
     return *reinterpret_cast<const i32x4*>(sa + offa[ks] + i * 32 * PK) ^ flip;
   };
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(512, 1) void proj_i8_kernel(const uint8_t* __restri
   for (int i = 0; i < IA; ++i)
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 32 + c32;
+      const int64_t col = n0 + wn * WC + j * 32 + c32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * (PM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -260,14 +262,16 @@ struct ProjLayout {
 static ProjLayout proj_layout(int64_t n, int64_t d, int kk) {
   auto a256 = [](int64_t v) { return (v + 255) / 256 * 256; };
   ProjLayout L;
-  // 256-column tiles (two thirds of the L2 -> LDS bytes per MAC) unless they pad the digit
-  // columns by > 15 % more than 128-column tiles do
-  const int64_t p = (int64_t)kDigits * kk, n128 = (p + 127) / 128 * 128, n256 = (p + 255) / 256 * 256;
-  L.tn = n256 * 100 <= n128 * 115 ? 256 : 128;
+  // 384-column tiles (the covariance SYRK's 256 x 384 shape: 26.7 B of L2 -> LDS per
+  // MFMA-clock) where they pad no more than 256-column tiles; 256-column tiles (32 B)
+  // unless they pad the digit columns by > 15 % more than 128-column tiles (48 B) do
+  const int64_t p = (int64_t)kDigits * kk, n128 = (p + 127) / 128 * 128, n256 = (p + 255) / 256 * 256,
+                n384 = (p + 383) / 384 * 384;
+  L.tn = n384 <= n256 ? 384 : n256 * 100 <= n128 * 115 ? 256 : 128;
 #ifdef EF_DIAGNOSTICS
-  if (const char* e = getenv("EF_PROJ_TN")) L.tn = atoi(e) == 256 ? 256 : 128;
+  if (const char* e = getenv("EF_PROJ_TN")) L.tn = atoi(e) == 384 ? 384 : atoi(e) == 256 ? 256 : 128;
 #endif
-  L.np = L.tn == 256 ? n256 : n128;
+  L.np = L.tn == 384 ? n384 : L.tn == 256 ? n256 : n128;
   L.off_i = a256(L.np * d);
   L.off_t = L.off_i + a256(n * L.np * (int64_t)sizeof(int));
   L.off_c = L.off_t + a256((int64_t)kk * sizeof(int));
@@ -300,7 +304,10 @@ hipError_t launch_proj_i8(hipStream_t s, const uint8_t* X, int64_t n, int64_t d,
   const int64_t nblocks = (n + PM - 1) / PM * ntn;
   if (nblocks > (int64_t)1 << 30) return hipErrorInvalidValue;
   const int grid = (int)((nblocks + 7) / 8 * 8);
-  if (L.tn == 256)
+  if (L.tn == 384)
+    hipLaunchKernelGGL(proj_i8_kernel<384>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
+                       np);
+  else if (L.tn == 256)
     hipLaunchKernelGGL(proj_i8_kernel<256>, dim3((unsigned)grid), dim3(512), 0, s, X, n, d, D, ntn, (int)nblocks, I,
                        np);
   else
