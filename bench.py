@@ -377,18 +377,20 @@ def pmc_record(config):
 def tmatch_executed_ops(probs, H, W, tile=128, blk=32):
     """int8 MFMA work tm_corr_kernel's tiles occupy for these maps, against the
     algorithmic 2 (H-h+1)(W-w+1) h w (DESIGN K11): per template row the band's (w + 31)
-    columns rounded up to whole 32-column k-blocks, over whole output tiles — 128 x 128,
-    and in a map's last row band with one or two live 32-row blocks 32 x 512 or 64 x 256
-    (ef_image.hip tm_tile_groups)."""
+    columns rounded up to whole 32-column k-blocks, over whole output row bands — 128
+    rows, and in a map's last row band with one or two live 32-row blocks 32 or 64 (the
+    32 x 512 / 64 x 256 tiles of ef_image.hip tm_tile_groups) — and the map's columns
+    rounded up to whole 32-column blocks (a wave runs only its live column blocks)."""
     ex = 0.0
     for _, ph, pw in probs:
         oh, ow = H - ph + 1, W - pw + 1
         kb = -(-(pw + blk - 1) // blk) * blk
         full, rem = oh // tile, oh % tile
-        area = full * tile * (-(-ow // tile) * tile)
+        rows = full * tile
         if rem:
             ncg = {1: 4, 2: 2}.get(-(-rem // 32), 1)
-            area += (tile // ncg) * (-(-ow // (tile * ncg)) * tile * ncg)
+            rows += tile // ncg
+        area = rows * (-(-ow // blk) * blk)
         ex += 2.0 * area * ph * kb
     return ex
 

@@ -323,40 +323,43 @@ struct TmTail {
   int ea[16], eb[16], ne;
   int tk[32], tn[32];
 };
-constexpr TmTail tm_tail(int nkb, int t) {
+// A wave with ncb live 32-column blocks (the map's last column tile: its columns past wr
+// are dead) runs only blocks n < ncb — ncb·nkb MFMAs on A k-blocks 0 .. nkb + ncb - 2.
+constexpr TmTail tm_tail(int nkb, int ncb, int t) {
   TmTail s{};
   int m = 0;
-  for (int kb = 0; kb < nkb + 3; ++kb)
-    for (int n = 0; n < 4; ++n)
+  for (int kb = 0; kb < nkb + ncb - 1; ++kb)
+    for (int n = 0; n < ncb; ++n)
       if (kb - n >= 0 && kb - n < nkb) {
-        if (m >= 4 * nkb - t) {
+        if (m >= ncb * nkb - t) {
           s.a[kb] = s.b[kb - n] = true;
-          s.tk[m - (4 * nkb - t)] = kb;
-          s.tn[m - (4 * nkb - t)] = n;
+          s.tk[m - (ncb * nkb - t)] = kb;
+          s.tn[m - (ncb * nkb - t)] = n;
         }
         ++m;
       }
-  for (int kb = 0; kb < nkb + 3; ++kb) {  // consumption order: A[kb], then B[kb]
+  for (int kb = 0; kb < nkb + ncb - 1; ++kb) {  // consumption order: A[kb], then B[kb]
     s.ea[kb] = s.a[kb] ? -1 : s.ne++;
     s.eb[kb] = kb < nkb && !s.b[kb] ? s.ne++ : -1;
   }
+  for (int kb = nkb + ncb - 1; kb < 16; ++kb) s.ea[kb] = s.eb[kb] = -1;  // A k-blocks no live block reads
   return s;
 }
 
 // position of MFMA (kb, n) in a template row's kb-major sequence
-constexpr int tm_mfma_index(int nkb, int kb, int n) {
+constexpr int tm_mfma_index(int nkb, int ncb, int kb, int n) {
   int m = 0;
-  for (int k = 0; k < nkb + 3; ++k)
-    for (int q = 0; q < 4; ++q)
+  for (int k = 0; k < nkb + ncb - 1; ++k)
+    for (int q = 0; q < ncb; ++q)
       if (k - q >= 0 && k - q < nkb) {
         if (k == kb && q == n) return m;
         ++m;
       }
   return m;
 }
-template <int NKB, int T>
+template <int NKB, int NCB, int T>
 struct TmTailOf {
-  static constexpr TmTail v = tm_tail(NKB, T);
+  static constexpr TmTail v = tm_tail(NKB, NCB, T);
 };
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction (no reliance on
 // the loop unroller: a table lookup left in a rolled loop lands in scratch memory)
@@ -413,8 +416,10 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
   // compile-time constant so the k-block loop unrolls and the fragment reads are static.
   const bool wact = wk.y0 + 32 * rb < pb.hr && wk.x0 + 128 * cg < pb.wr;
   i32x16 acc[4] = {};
-  auto run = [&](auto nkb_c) {
+  auto run = [&](auto nkb_c, auto ncb_c) {
     constexpr int NKB = decltype(nkb_c)::value;
+    constexpr int NCB = decltype(ncb_c)::value;  // live 32-column blocks of this wave (1..4)
+    constexpr int NKA = NKB + NCB - 1;           // A k-blocks those blocks read
     constexpr int NPC = 2 * NKB + 2;       // DMA pieces per pair: 2 NKB band slices + 2 A rows
     constexpr int Q = (NPC + 7) / 8;       // DMA instructions per wave per pair
     // Pair p's operands: band slices of rows 2p, 2p+1 into stage p % 3 and A rows
@@ -470,14 +475,15 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
     // k-blocks, needed last by the next pair) are re-read after it.  One register set.
     // Stage p % 3 is rewritten by pair p + 3's DMA, issued during pair p + 1 — after this
     // barrier, by which every wave has completed its reads of stage p (lgkmcnt(0) below).
-    constexpr int NM = 4 * NKB;                             // MFMAs per template row
+    constexpr int NM = NCB * NKB;                           // MFMAs per template row
 #ifndef EF_TM_TAIL  // (variant builds: A/B of the tail length)
 #define EF_TM_TAIL 8
 #endif
-    constexpr int T = NM / 2 < EF_TM_TAIL ? NM / 2 : EF_TM_TAIL;  // MFMAs after the barrier
+    // MFMAs after the barrier (at least one: the tail is where pair p + 1's reads go)
+    constexpr int T = NM / 2 < 1 ? 1 : NM / 2 < EF_TM_TAIL ? NM / 2 : EF_TM_TAIL;
     static_assert(T <= 32, "TmTail holds 32 tail MFMAs");
-    using Tail = TmTailOf<NKB, T>;
-    i32x4 A[NKB + 3], B[NKB];
+    using Tail = TmTailOf<NKB, NCB, T>;
+    i32x4 A[NKA], B[NKB];
     // fragment reads of pair p: the tail's (LATE) or the others, in consumption order
     auto frag_read = [&](int p, auto late_c) {
       constexpr bool LATE = decltype(late_c)::value;
@@ -490,18 +496,26 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
             if constexpr (Tail::v.a[kb] == LATE) A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
             if constexpr (kb < NKB && Tail::v.b[kb] == LATE) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
           },
-          std::make_integer_sequence<int, NKB + 3>{});
+          std::make_integer_sequence<int, NKA>{});
     };
     // MFMAs [LO, HI) of a row's sequence (kb-major; block n uses k-block kb - n).  With
     // dma, pair p + 2's pieces go between the first NM - T at evenly spaced positions.
     auto mfmas = [&](auto lo_c, auto hi_c, bool dma, int p) {
       constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
+      if constexpr (LO == 0)  // pieces placed before the first MFMA (short rows: NM - T < Q + 1)
+        tm_static_for(
+            [&](auto ic) {
+              constexpr int i = decltype(ic)::value;
+              if constexpr ((i + 1) * (NM - T) / (Q + 1) == 0)
+                if (dma) issue_piece(p + 2, i);
+            },
+            std::make_integer_sequence<int, Q>{});
       tm_static_for(
           [&](auto kc) {
             constexpr int kb = decltype(kc)::value;
             tm_static_for(
                 [&](auto nc) {
-                  constexpr int n = decltype(nc)::value, m = tm_mfma_index(NKB, kb, n);
+                  constexpr int n = decltype(nc)::value, m = tm_mfma_index(NKB, NCB, kb, n);
                   if constexpr (kb - n >= 0 && kb - n < NKB && m >= LO && m < HI) {
                     acc[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - n], acc[n], 0, 0, 0);
                     tm_static_for(
@@ -516,9 +530,9 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
                         std::make_integer_sequence<int, Q>{});
                   }
                 },
-                std::make_integer_sequence<int, 4>{});
+                std::make_integer_sequence<int, NCB>{});
           },
-          std::make_integer_sequence<int, NKB + 3>{});
+          std::make_integer_sequence<int, NKA>{});
     };
     if (wact && par < J) {
       frag_read(0, std::false_type{});
@@ -561,7 +575,7 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
                     if constexpr (kb < NKB && Tail::v.eb[kb] >= 0 && Tail::v.eb[kb] * T / Tail::v.ne == t)
                       B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
                   },
-                  std::make_integer_sequence<int, NKB + 3>{});
+                  std::make_integer_sequence<int, NKA>{});
               __builtin_amdgcn_sched_barrier(0);
               constexpr int tk = Tail::v.tk[t], tn = Tail::v.tn[t];
               acc[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[tk], B[tk - tn], acc[tn], 0, 0, 0);
@@ -580,9 +594,9 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
       if (wact && j < J) {
         const uint8_t* aslot = smem + wrap(j + 32 * rb + r) * SA + 16 * h + 128 * cg;
         const uint8_t* bst = smem + kTmRing * kTmMaxSA + (p % 3) * kTmBStage + par * kTmMaxNkb * 1024 + 16 * lane;
-        i32x4 A[NKB + 3], B[NKB];
+        i32x4 A[NKA], B[NKB];
 #pragma unroll
-        for (int kb = 0; kb < NKB + 3; ++kb) {  // in the order the MFMAs consume them
+        for (int kb = 0; kb < NKA; ++kb) {  // in the order the MFMAs consume them
           A[kb] = *reinterpret_cast<const i32x4*>(aslot + 32 * kb);
           if (kb < NKB) B[kb] = *reinterpret_cast<const i32x4*>(bst + kb * 1024);
         }
@@ -591,15 +605,18 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
         // its issue phase (~800 cycles per pair) with the MFMA pipe idle
         int m = 0;
 #pragma unroll
-        for (int kb = 0; kb < NKB + 3; ++kb)
+        for (int i = 0; i < Q; ++i)  // pieces placed before the first MFMA (short rows)
+          if ((i + 1) * (NCB * NKB) / (Q + 1) == 0 && ahead) issue_piece(p + 2, i);
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+        for (int kb = 0; kb < NKA; ++kb)
+#pragma unroll
+          for (int n = 0; n < NCB; ++n)
             if (kb - n >= 0 && kb - n < NKB) {
               acc[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[kb], B[kb - n], acc[n], 0, 0, 0);
               ++m;
 #pragma unroll
               for (int i = 0; i < Q; ++i)
-                if (m == (i + 1) * (4 * NKB) / (Q + 1)) {
+                if (m == (i + 1) * (NCB * NKB) / (Q + 1)) {
                   __builtin_amdgcn_sched_barrier(0);
                   if (ahead) issue_piece(p + 2, i);
                   __builtin_amdgcn_sched_barrier(0);
@@ -625,10 +642,21 @@ __global__ __launch_bounds__(512, MAXNKB <= 5 ? 2 : 1) void tm_corr_kernel(const
 #endif
 #undef EF_STAMP
   };
+  // live column blocks of this wave's column group: a map's last column tile runs only
+  // those (waves with none are inactive and run the 4-block loop for its DMA and barriers)
+  const int ncb = __builtin_amdgcn_readfirstlane(wact ? min(4, (pb.wr - wk.x0 - 128 * cg + 31) / 32) : 4);
+  auto run_nkb = [&](auto nkb_c) {
+    switch (ncb) {
+      case 1: run(nkb_c, std::integral_constant<int, 1>{}); break;
+      case 2: run(nkb_c, std::integral_constant<int, 2>{}); break;
+      case 3: run(nkb_c, std::integral_constant<int, 3>{}); break;
+      default: run(nkb_c, std::integral_constant<int, 4>{}); break;
+    }
+  };
   switch (nkb) {
 #define EF_TM_NKB(V)                                     \
   case V:                                                \
-    if constexpr (V <= MAXNKB) run(std::integral_constant<int, V>{}); \
+    if constexpr (V <= MAXNKB) run_nkb(std::integral_constant<int, V>{}); \
     break;
     EF_TM_NKB(1) EF_TM_NKB(2) EF_TM_NKB(3) EF_TM_NKB(4) EF_TM_NKB(5) EF_TM_NKB(6)
     EF_TM_NKB(7) EF_TM_NKB(8) EF_TM_NKB(9) EF_TM_NKB(10) EF_TM_NKB(11) EF_TM_NKB(12)

@@ -66,9 +66,10 @@ def test_launch_ranks_passes_environment(tmp_path, monkeypatch):
 
 
 def test_tmatch_executed_work_model():
-    """bench.tmatch_executed_ops: whole output tiles (128 x 128; 32 x 512 / 64 x 256 for a
-    last row band with one / two live 32-row blocks), band columns rounded up to 32-column
-    k-blocks (DESIGN K11)."""
+    """bench.tmatch_executed_ops: whole output row bands (128 rows; 32 / 64 for a last row
+    band with one / two live 32-row blocks — the 32 x 512 / 64 x 256 tiles), the map's
+    columns rounded up to whole 32-column blocks (a wave runs only its live column blocks),
+    band columns rounded up to 32-column k-blocks (DESIGN K11)."""
     sys.path.insert(0, ROOT)
     import importlib
     bench = importlib.import_module("bench")
@@ -76,15 +77,16 @@ def test_tmatch_executed_work_model():
     H, W, h, w = 127 + 40, 127 + 33, 40, 33
     ex = bench.tmatch_executed_ops([(0, h, w)], H, W)
     assert ex == 2.0 * 128 * 128 * h * 64
-    # one more output column needs a second tile column
-    assert bench.tmatch_executed_ops([(0, h, w)], H, W + 1) == 2 * ex
-    # one live output row across 417 columns: one 32 x 512 tile, not four 128 x 128 ones
-    assert bench.tmatch_executed_ops([(0, h, w)], h, w + 416) == 2.0 * 32 * 512 * h * 64
+    # one more output column opens a second tile column with one live 32-column block
+    assert bench.tmatch_executed_ops([(0, h, w)], H, W + 1) == 2.0 * 128 * 160 * h * 64
+    # one live output row across 417 columns: one 32 x 512 tile, 14 live column blocks
+    assert bench.tmatch_executed_ops([(0, h, w)], h, w + 416) == 2.0 * 32 * 448 * h * 64
     # 168 rows x 256 columns: a full 128-row band, then 40 rows = two live row blocks in
     # one 64 x 256 tile
     assert bench.tmatch_executed_ops([(0, h, w)], 167 + h, 255 + w) == 2.0 * (128 * 256 + 64 * 256) * h * 64
-    # 160 rows x 256 columns: the last band has one live row block, a 32 x 512 tile
-    assert bench.tmatch_executed_ops([(0, h, w)], 159 + h, 255 + w) == 2.0 * (128 * 256 + 32 * 512) * h * 64
+    # 160 rows x 256 columns: the last band has one live row block, a 32 x 512 tile with
+    # 8 live column blocks
+    assert bench.tmatch_executed_ops([(0, h, w)], 159 + h, 255 + w) == 2.0 * (128 * 256 + 32 * 256) * h * 64
 
 
 def test_ingest_touched_bytes_model():
