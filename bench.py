@@ -388,8 +388,7 @@ def tmatch_executed_ops(probs, H, W, tile=128, blk=32):
         full, rem = oh // tile, oh % tile
         rows = full * tile
         if rem:
-            ncg = {1: 4, 2: 2}.get(-(-rem // 32), 1)
-            rows += tile // ncg
+            rows += {1: 32, 2: 64}.get(-(-rem // 32), tile)
         area = rows * (-(-ow // blk) * blk)
         ex += 2.0 * area * ph * kb
     return ex

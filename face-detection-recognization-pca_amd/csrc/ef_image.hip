@@ -299,7 +299,10 @@ __global__ void tm_band_kernel(const uint8_t* __restrict__ scaled, const TmProbl
 // Tile shapes (TmWork::ncg): 128 x 128, and for a map's last row band with one or two live
 // 32-row blocks 32 x 512 or 64 x 256 — wave pair wr4 then owns column group wr4 & (ncg - 1)
 // of row block wr4 / ncg, so no SIMD idles on dead rows (0.397 -> 0.383 ms per bench frame,
-// profiles/r05/tm_tile_shape_ab.txt).
+// profiles/r05/tm_tile_shape_ab.txt; three live row blocks as a 64 x 256 band plus a 32 x 512
+// one measured no faster, profiles/r06/tm_split3_ab.txt).  In a map's last column tile each
+// wave runs only its live 32-column blocks (NCB, a compile-time count per wave; 0.383 ->
+// 0.368 ms per bench frame, profiles/r06/tm_live_cols_ab.txt).
 // One barrier per template-row pair (half the barriers, and half the LDS fragment reads
 // per MFMA, of a one-row-per-barrier, two-blocks-per-wave tiling).  The wide kernel
 // (MAXNKB 12, one workgroup per CU) software-pipelines the pairs: the last 8 MFMAs of pair

@@ -87,6 +87,8 @@ def test_tmatch_executed_work_model():
     # 160 rows x 256 columns: the last band has one live row block, a 32 x 512 tile with
     # 8 live column blocks
     assert bench.tmatch_executed_ops([(0, h, w)], 159 + h, 255 + w) == 2.0 * (128 * 256 + 32 * 256) * h * 64
+    # 200 rows: the last band has three live row blocks, a whole 128 x 128 tile row
+    assert bench.tmatch_executed_ops([(0, h, w)], 199 + h, 255 + w) == 2.0 * (128 * 256 + 128 * 256) * h * 64
 
 
 def test_ingest_touched_bytes_model():

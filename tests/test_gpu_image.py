@@ -67,6 +67,9 @@ CASES = [  # frame (H, W), template (h, w)
     ((200, 600), (150, 180)),   # two live row blocks: 64 x 256 tiles, 148 KiB kernel
     ((100, 640), (80, 400)),    # 32 x 512 tiles over two column pieces
     ((150, 700), (100, 360)),   # 64 x 256 tiles over two column pieces
+    ((300, 500), (215, 90)),    # three live row blocks, one live column block, narrow kernel
+    ((300, 449), (220, 150)),   # three live row blocks, two live column blocks, 148 KiB kernel
+    ((300, 420), (213, 160)),   # three live row blocks, one live column block, 148 KiB kernel
 ]
 
 
