@@ -434,6 +434,9 @@ void ef_destroy(ef_ctx* c) {
   for (int i = 0; i < 2; ++i)
     if (c->fit_side_ev[i]) (void)hipEventDestroy(c->fit_side_ev[i]);
   if (c->fit_side) (void)hipStreamDestroy(c->fit_side);
+  for (int i = 0; i < 2; ++i)
+    if (c->tm_side_ev[i]) (void)hipEventDestroy(c->tm_side_ev[i]);
+  if (c->tm_side) (void)hipStreamDestroy(c->tm_side);
   for (auto& b : c->fit_pool) release(b);
   comm_release(c);
   tm_release(c);

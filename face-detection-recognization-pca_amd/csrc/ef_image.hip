@@ -1071,19 +1071,41 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
   TimerEvt tev;
   timer_begin(c, EF_KERNEL_TMATCH, &tev);
   const dim3 rgrid((unsigned)((H + 1 + 3) / 4)), cgrid((unsigned)((W + 1 + kColW - 1) / kColW));
+  // The integral images' column pass runs on a side stream beside the correlation kernel
+  // (it needs only the row pass; the score kernel joins both): its 8 KiB blocks fit next to
+  // a correlation workgroup's 147 KiB of LDS.
+  bool side = t->nprob > 0 && t->nwork > 0;
+#ifdef EF_DIAGNOSTICS
+  if (std::getenv("EF_TM_NOSIDE")) side = false;  // A/B: column pass in line
+#endif
+  if (side) {
+    if (!c->tm_side) EF_HIP(c, hipStreamCreateWithFlags(&c->tm_side, hipStreamNonBlocking), "tm side stream");
+    for (int i = 0; i < 2; ++i)
+      if (!c->tm_side_ev[i]) EF_HIP(c, hipEventCreateWithFlags(&c->tm_side_ev[i], hipEventDisableTiming), "tm event");
+  }
+  hipStream_t cs = side ? c->tm_side : s;  // the column pass's stream
   if (t->ii64) {
     long long* ii1 = static_cast<long long*>(t->ii1.p);
     long long* ii2 = static_cast<long long*>(t->ii2.p);
     hipLaunchKernelGGL(tm_rows_kernel<long long>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2,
                        keys, t->nprob);
-    hipLaunchKernelGGL(tm_cols_kernel<long long>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
+    if (side) {
+      EF_HIP(c, hipEventRecord(c->tm_side_ev[0], s), "rows done");
+      EF_HIP(c, hipStreamWaitEvent(cs, c->tm_side_ev[0], 0), "side waits rows");
+    }
+    hipLaunchKernelGGL(tm_cols_kernel<long long>, cgrid, dim3(1024), 0, cs, H, W, ii1, ii2);
   } else {
     unsigned* ii1 = static_cast<unsigned*>(t->ii1.p);
     unsigned* ii2 = static_cast<unsigned*>(t->ii2.p);
     hipLaunchKernelGGL(tm_rows_kernel<unsigned>, rgrid, dim3(256), 0, s, f, H, W, frame_ld, f8, t->pitch, ii1, ii2,
                        keys, t->nprob);
-    hipLaunchKernelGGL(tm_cols_kernel<unsigned>, cgrid, dim3(1024), 0, s, H, W, ii1, ii2);
+    if (side) {
+      EF_HIP(c, hipEventRecord(c->tm_side_ev[0], s), "rows done");
+      EF_HIP(c, hipStreamWaitEvent(cs, c->tm_side_ev[0], 0), "side waits rows");
+    }
+    hipLaunchKernelGGL(tm_cols_kernel<unsigned>, cgrid, dim3(1024), 0, cs, H, W, ii1, ii2);
   }
+  if (side) EF_HIP(c, hipEventRecord(c->tm_side_ev[1], cs), "cols done");
   if (t->nprob > 0) {
     if (t->nwork > 0) {
       bool narrow = t->max_nkb <= 5;
@@ -1105,6 +1127,7 @@ int ef_tm_match(ef_ctx* c, const uint8_t* frame, int64_t frame_ld, float* best_o
         maps = static_cast<float*>(t->maps.p);
       }
     }
+    if (side) EF_HIP(c, hipStreamWaitEvent(s, c->tm_side_ev[1], 0), "score waits cols");
     const int64_t sblk = 64;  // row-strided blocks per problem
     const dim3 sgrid((unsigned)sblk, (unsigned)t->nprob);
     const TmProblem* dp = static_cast<const TmProblem*>(t->d_probs.p);

@@ -150,6 +150,10 @@ struct ef_ctx {
   // subspace iteration, e.g. the int8 digit planes of C during the coarse phase
   hipStream_t fit_side = nullptr;
   hipEvent_t fit_side_ev[2] = {nullptr, nullptr};
+  // the template localiser's side stream (created on first use): the integral images' column
+  // pass runs beside the correlation kernel
+  hipStream_t tm_side = nullptr;
+  hipEvent_t tm_side_ev[2] = {nullptr, nullptr};
   int jpeg_slot = 0;                // slot of the next staged batch
 
   void* tm = nullptr;    // template-localiser state (ef_image.hip TmState), ef_tm_prepare
