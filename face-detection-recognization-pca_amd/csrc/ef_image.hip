@@ -998,10 +998,15 @@ int ef_tm_prepare(ef_ctx* c, const uint8_t* templ_data, const int64_t* templ_off
               TmWork{pi, ch * npiece + q, ch * kTmChunk, std::min(pb.th, (ch + 1) * kTmChunk), y0, x0, ncg});
       }
   }
-  // longest work items first (template rows x k-blocks), so the short ones fill the tail
-  std::stable_sort(works.begin(), works.end(), [&](const TmWork& a, const TmWork& b) {
-    return (int64_t)(a.yb - a.ya) * (pieces[a.piece].nkb + 3) > (int64_t)(b.yb - b.ya) * (pieces[b.piece].nkb + 3);
-  });
+  // longest work items first, so the short ones fill the tail: per template row a tile's
+  // fullest wave runs ncb * nkb MFMAs (~32 cycles each; ncb its live column blocks) plus
+  // ~650 cycles of LDS round trip and barrier (DESIGN K11)
+  auto cost = [&](const TmWork& w) {
+    const TmPiece& pc = pieces[w.piece];
+    const int ncb = (int)std::min<int64_t>(4, (t->probs[pc.prob].wr - w.x0 + 31) / 32);
+    return (int64_t)(w.yb - w.ya) * (32 * ncb * pc.nkb + 650);
+  };
+  std::stable_sort(works.begin(), works.end(), [&](const TmWork& a, const TmWork& b) { return cost(a) > cost(b); });
   t->nwork = (int)works.size();
   t->max_pos = max_pos;
   t->map_total = map_total;
